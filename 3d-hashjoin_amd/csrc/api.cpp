@@ -1,0 +1,372 @@
+// api.cpp — the extern "C" surface of libhj3d.so (declared in include/hj3d.h).
+//
+// Argument checking, context / table lifetime, device result slots and HIP-event phase
+// timers live here; the kernels are in the .hip translation units. Every entry point
+// returns an hj3d_status and never throws.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+
+#include "hj3d_internal.hpp"
+
+using namespace hj3d;
+
+namespace {
+
+hj3d_status fail(hj3d_ctx* ctx, hj3d_status st, const char* what, hipError_t e = hipSuccess) {
+  if (ctx) {
+    char buf[512];
+    if (e != hipSuccess)
+      std::snprintf(buf, sizeof(buf), "%s: %s (%d)", what, hipGetErrorString(e), int(e));
+    else
+      std::snprintf(buf, sizeof(buf), "%s", what);
+    ctx->last_error = buf;
+  }
+  return st;
+}
+
+hj3d_status from_hip(hj3d_ctx* ctx, hipError_t e, const char* what) {
+  if (e == hipSuccess) return HJ3D_OK;
+  if (e == hipErrorOutOfMemory) return fail(ctx, HJ3D_ENOMEM, what, e);
+  if (e == hipErrorNotSupported) return fail(ctx, HJ3D_EUNSUPPORTED, what, e);
+  if (e == hipErrorInvalidValue) return fail(ctx, HJ3D_EINVAL, what, e);
+  return fail(ctx, HJ3D_EDEVICE, what, e);
+}
+
+bool rel_ok(const hj3d_rel* r) {
+  if (!r) return false;
+  if (r->n && !r->base) return false;
+  if (r->stride == 0 || (r->stride & 3) || (r->key_off & 3) || r->key_off + 4 > r->stride) return false;
+  if (r->row_off != HJ3D_ROW_IMPLICIT && ((r->row_off & 3) || r->row_off + 4 > r->stride)) return false;
+  if (r->row_off == HJ3D_ROW_IMPLICIT && r->n && r->row_base + r->n - 1 > 0xFFFFFFFFull) return false;
+  return true;
+}
+
+hipEvent_t take_event(hj3d_ctx* ctx) {
+  if (ctx->pool_used == ctx->event_pool.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    ctx->event_pool.push_back(ev);
+  }
+  return ctx->event_pool[ctx->pool_used++];
+}
+
+struct PhaseTimer {  // records [a, b) on the context stream when timing is enabled
+  hj3d_ctx* ctx;
+  int phase;
+  hipEvent_t a = nullptr;
+  PhaseTimer(hj3d_ctx* c, int p) : ctx(c), phase(p) {
+    if (ctx->timing && (a = take_event(ctx))) (void)hipEventRecord(a, ctx->stream);
+  }
+  ~PhaseTimer() {
+    if (!a) return;
+    hipEvent_t b = take_event(ctx);
+    if (!b) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->spans[phase].push_back({a, b});
+  }
+};
+
+constexpr int kResFields = 16;
+
+}  // namespace
+
+extern "C" {
+
+uint64_t hj3d_mix64(uint64_t z) { return mix64(z); }
+
+hj3d_status hj3d_ctx_create(int device, void* stream, hj3d_ctx** out) {
+  if (!out) return HJ3D_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HJ3D_EDEVICE;
+  if (hipSetDevice(device) != hipSuccess) return HJ3D_EDEVICE;
+  hj3d_ctx* ctx = new (std::nothrow) hj3d_ctx();
+  if (!ctx) return HJ3D_ENOMEM;
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+    ctx->num_cus = prop.multiProcessorCount;
+  if (stream) {
+    ctx->stream = static_cast<hipStream_t>(stream);
+  } else {
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete ctx;
+      return HJ3D_EDEVICE;
+    }
+    ctx->own_stream = true;
+  }
+  if (ctx->res.ensure(kResFields * sizeof(uint64_t)) != hipSuccess) {
+    delete ctx;
+    return HJ3D_ENOMEM;
+  }
+  *out = ctx;
+  return HJ3D_OK;
+}
+
+void hj3d_ctx_destroy(hj3d_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& b : ctx->scratch) b.release();
+  ctx->res.release();
+  ctx->misc.release();
+  for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
+  if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+hj3d_status hj3d_ctx_set_stream(hj3d_ctx* ctx, void* stream) {
+  if (!ctx || !stream) return HJ3D_EINVAL;
+  if (ctx->own_stream) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipStreamDestroy(ctx->stream);
+    ctx->own_stream = false;
+  }
+  ctx->stream = static_cast<hipStream_t>(stream);
+  return HJ3D_OK;
+}
+
+void* hj3d_ctx_stream(const hj3d_ctx* ctx) { return ctx ? static_cast<void*>(ctx->stream) : nullptr; }
+
+hj3d_status hj3d_ctx_sync(hj3d_ctx* ctx) {
+  if (!ctx) return HJ3D_EINVAL;
+  return from_hip(ctx, hipStreamSynchronize(ctx->stream), "hj3d_ctx_sync");
+}
+
+const char* hj3d_last_error(const hj3d_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable) {
+  if (!ctx) return HJ3D_EINVAL;
+  ctx->timing = enable != 0;
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count) {
+  if (!ctx || phase < 0 || phase >= HJ3D_T_NTIMERS) return HJ3D_EINVAL;
+  hipError_t e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_ctx_timer");
+  double sum = 0;
+  for (const auto& sp : ctx->spans[phase]) {
+    float ms = 0;
+    if ((e = hipEventElapsedTime(&ms, sp.a, sp.b)) != hipSuccess) return from_hip(ctx, e, "hipEventElapsedTime");
+    sum += ms;
+  }
+  if (ms_total) *ms_total = sum;
+  if (count) *count = ctx->spans[phase].size();
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx) {
+  if (!ctx) return HJ3D_EINVAL;
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& v : ctx->spans) v.clear();
+  ctx->pool_used = 0;
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_table_create(hj3d_ctx* ctx, const hj3d_table_desc* desc, hj3d_table** out) {
+  if (!ctx || !desc || !out) return HJ3D_EINVAL;
+  *out = nullptr;
+  if (desc->kind != HJ3D_CHAIN && desc->kind != HJ3D_NESTED) return fail(ctx, HJ3D_EINVAL, "unknown table kind");
+  if (desc->num_buckets == 0 || desc->num_buckets >= (1ull << 32))
+    return fail(ctx, HJ3D_EINVAL, "num_buckets must be in [1, 2^32)");
+  if (desc->bucket_lo > desc->bucket_hi || desc->bucket_hi > desc->num_buckets)
+    return fail(ctx, HJ3D_EINVAL, "bucket range outside [0, num_buckets]");
+  hj3d_table* t = new (std::nothrow) hj3d_table();
+  if (!t) return HJ3D_ENOMEM;
+  t->desc = *desc;
+  t->nb_local = uint32_t(desc->bucket_hi - desc->bucket_lo);
+  t->fm = FastMod::make(uint32_t(desc->num_buckets));
+  (void)hipSetDevice(ctx->device);
+  hipError_t e = t->off.ensure((uint64_t(t->nb_local) + 1) * sizeof(uint32_t));
+  if (e == hipSuccess) e = t->counts.ensure(4 * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMemsetAsync(t->off.p, 0, (uint64_t(t->nb_local) + 1) * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(t->counts.p, 0, 4 * sizeof(uint64_t), ctx->stream);
+  if (e != hipSuccess) {
+    hj3d_table_destroy(t);
+    return from_hip(ctx, e, "hj3d_table_create");
+  }
+  *out = t;
+  return HJ3D_OK;
+}
+
+void hj3d_table_destroy(hj3d_table* t) {
+  if (!t) return;
+  t->off.release();
+  t->ent.release();
+  t->main.release();
+  t->sub.release();
+  t->counts.release();
+  delete t;
+}
+
+hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  const uint64_t n = max_build ? max_build : 1;
+  hipError_t e = hipSuccess;
+  if (t->desc.kind == HJ3D_CHAIN) {
+    e = t->ent.ensure(n * sizeof(uint2));
+    if (e == hipSuccess) e = ctx->scratch[kScrSlot].ensure(n * sizeof(uint32_t));
+  } else {
+    e = t->main.ensure(n * sizeof(uint4));
+    if (e == hipSuccess) e = t->sub.ensure(n * sizeof(uint32_t));
+    if (e == hipSuccess) e = ctx->scratch[kScrSortK].ensure(3 * n * sizeof(uint32_t));
+    if (e == hipSuccess) e = ctx->scratch[kScrB].ensure((5 * n + 2) * sizeof(uint32_t));
+  }
+  return from_hip(ctx, e, "hj3d_table_reserve");
+}
+
+hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  hipError_t e = hipMemsetAsync(t->off.p, 0, (uint64_t(t->nb_local) + 1) * sizeof(uint32_t), ctx->stream);
+  if (e == hipSuccess) e = hipMemsetAsync(t->counts.p, 0, 4 * sizeof(uint64_t), ctx->stream);
+  t->n_build = 0;
+  return from_hip(ctx, e, "hj3d_table_clear");
+}
+
+hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  if (!rel_ok(build)) return fail(ctx, HJ3D_EINVAL, "hj3d_build: invalid relation");
+  if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
+  PhaseTimer tm(ctx, HJ3D_T_BUILD);
+  const hipError_t e = t->desc.kind == HJ3D_CHAIN ? chain_build(ctx, t, *build, ctx->stream)
+                                                  : nested_build(ctx, t, *build, ctx->stream);
+  t->built = e == hipSuccess;
+  return from_hip(ctx, e, "hj3d_build");
+}
+
+hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out) {
+  if (!ctx || !t || !out) return HJ3D_EINVAL;
+  std::memset(out, 0, sizeof(*out));
+  return from_hip(ctx, table_stats(ctx, t, out, ctx->stream), "hj3d_table_stats");
+}
+
+hj3d_status hj3d_table_size(hj3d_ctx* ctx, const hj3d_table* t, uint64_t* n_entries, uint64_t* n_distinct) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  hj3d_stats st;
+  const hj3d_status s = hj3d_table_stats(ctx, t, &st);
+  if (s != HJ3D_OK) return s;
+  if (n_entries) *n_entries = st.entries;
+  if (n_distinct) *n_distinct = st.distinct;
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe, uint32_t flags, void* out_dev,
+                       uint64_t out_cap) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  if (!rel_ok(probe)) return fail(ctx, HJ3D_EINVAL, "hj3d_probe: invalid relation");
+  if ((flags & HJ3D_PROBE_EMIT) && !out_dev && out_cap) return fail(ctx, HJ3D_EINVAL, "hj3d_probe: EMIT without buffer");
+  if ((flags & HJ3D_PROBE_UNNEST) && t->desc.kind != HJ3D_NESTED)
+    return fail(ctx, HJ3D_EINVAL, "hj3d_probe: UNNEST needs a nested table");
+  PhaseTimer tm(ctx, HJ3D_T_PROBE);
+  uint64_t* res = ctx->res.as<uint64_t>();
+  hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+  if (e == hipSuccess) {
+    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+    e = t->desc.kind == HJ3D_CHAIN ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
+                                   : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+  }
+  // remember what an overflow check needs
+  ctx->res_flags = flags;
+  ctx->res_dense = (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
+  ctx->res_cap = (flags & HJ3D_PROBE_EMIT) ? out_cap : ~0ull;
+  ctx->res_nprobe = probe->n;
+  return from_hip(ctx, e, "hj3d_probe");
+}
+
+hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out) {
+  if (!ctx || !out) return HJ3D_EINVAL;
+  uint64_t h[kResFields];
+  hipError_t e = hipMemcpyAsync(h, ctx->res.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe_result");
+  out->n_probe = h[0];
+  out->n_matched = h[1];
+  out->n_out = h[2];
+  out->n_cmps = h[3];
+  out->sum_a = h[4];
+  out->sum_b = h[5];
+  out->sum_c = h[6];
+  out->sum_h = h[7];
+  out->xor_h = h[8];
+  const uint64_t need = ctx->res_dense ? ctx->res_nprobe : out->n_out;
+  if ((ctx->res_flags & HJ3D_PROBE_EMIT) && need > ctx->res_cap) return fail(ctx, HJ3D_EOVERFLOW, "hj3d_probe: output buffer too small");
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel* probe,
+                        uint32_t flags, void* out_dev, uint64_t out_cap) {
+  if (!ctx || !ts || !tt) return HJ3D_EINVAL;
+  if (!rel_ok(probe)) return fail(ctx, HJ3D_EINVAL, "hj3d_probe2: invalid relation");
+  if (ts->desc.kind != tt->desc.kind) return fail(ctx, HJ3D_EINVAL, "hj3d_probe2: both tables must be of one kind");
+  if (flags & HJ3D_PROBE_EMIT) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_probe2: triple materialisation not implemented");
+  PhaseTimer tm(ctx, HJ3D_T_PROBE);
+  uint64_t* res = ctx->res.as<uint64_t>();
+  hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+  if (e == hipSuccess) {
+    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+    e = probe2(ctx, ts, tt, *probe, flags, out_dev, out_cap, res, ctx->stream);
+  }
+  return from_hip(ctx, e, "hj3d_probe2");
+}
+
+hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out) {
+  if (!ctx || !out) return HJ3D_EINVAL;
+  uint64_t h[kResFields];
+  hipError_t e = hipMemcpyAsync(h, ctx->res.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe2_result");
+  static_assert(sizeof(hj3d_probe2_res) == 12 * sizeof(uint64_t), "probe2 result layout");
+  std::memcpy(out, h, sizeof(hj3d_probe2_res));
+  return HJ3D_OK;
+}
+
+void hj3d_part_range(uint64_t nb, uint32_t parts, uint32_t part, uint64_t* lo, uint64_t* hi) {
+  // owner(b) = b * parts / nb  =>  part p owns b in [ceil(p*nb/parts), ceil((p+1)*nb/parts))
+  const auto first = [&](uint64_t p) -> uint64_t {
+    const unsigned __int128 x = (unsigned __int128)p * nb;
+    return uint64_t((x + parts - 1) / parts);
+  };
+  if (lo) *lo = parts ? first(part) : 0;
+  if (hi) *hi = parts ? first(uint64_t(part) + 1) : nb;
+}
+
+hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t nb, uint32_t parts, void* out_pairs,
+                           void* counts) {
+  if (!ctx || !rel_ok(rel) || !counts || (rel->n && !out_pairs)) return HJ3D_EINVAL;
+  PhaseTimer tm(ctx, HJ3D_T_PARTITION);
+  return from_hip(ctx, partition(ctx, *rel, nb, parts, out_pairs, counts, ctx->stream), "hj3d_partition");
+}
+
+hj3d_status hj3d_gen_keys(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
+                          uint64_t row_base, uint64_t n_keys, uint64_t seed) {
+  if (!ctx || (n && !tuples) || stride == 0 || (stride & 3) || (key_off & 3) || key_off + 4 > stride)
+    return HJ3D_EINVAL;
+  return from_hip(ctx, gen_keys(tuples, n, stride, key_off, row_base, n_keys, seed, ctx->stream), "hj3d_gen_keys");
+}
+
+hj3d_status hj3d_gen_fk(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
+                        uint64_t row_base, uint32_t fk_max, uint64_t seed) {
+  if (!ctx || (n && !tuples) || stride == 0 || (stride & 3) || (key_off & 3) || key_off + 4 > stride || fk_max == 0)
+    return HJ3D_EINVAL;
+  return from_hip(ctx, gen_fk(tuples, n, stride, key_off, row_base, fk_max, seed, ctx->stream), "hj3d_gen_fk");
+}
+
+hj3d_status hj3d_expected_fk_join(hj3d_ctx* ctx, const hj3d_rel* build, const hj3d_rel* probe, uint64_t n_keys,
+                                  int swap, void* res_dev) {
+  if (!ctx || !rel_ok(build) || !rel_ok(probe) || !res_dev) return HJ3D_EINVAL;
+  return from_hip(ctx, expected_fk_join(ctx, *build, *probe, n_keys, swap != 0, res_dev, ctx->stream),
+                  "hj3d_expected_fk_join");
+}
+
+hj3d_status hj3d_expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel* probe, uint64_t n_keys, uint64_t key_seed,
+                                      int swap, void* res_dev) {
+  if (!ctx || !rel_ok(probe) || !res_dev || n_keys == 0) return HJ3D_EINVAL;
+  return from_hip(ctx, expected_fk_join_gen(ctx, *probe, n_keys, key_seed, swap != 0, res_dev, ctx->stream),
+                  "hj3d_expected_fk_join_gen");
+}
+
+}  // extern "C"

@@ -1,0 +1,143 @@
+// hj3d_internal.hpp — host-side internals shared by the C-ABI implementation and the kernel
+// translation units. Not installed; the public surface is include/hj3d.h.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "hj3d.h"
+#include "hj3d_device.hpp"
+
+namespace hj3d {
+
+constexpr int kBlock = 256;           // 4 waves; the default workgroup of every streaming kernel
+constexpr uint32_t kInvalid = 0xFFFFFFFFu;
+
+// Grow-only device buffer (allocation happens outside timed loops once sizes are warm).
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  hipError_t ensure(size_t need) {
+    if (need <= bytes) return hipSuccess;
+    if (p) {
+      (void)hipDeviceSynchronize();  // the old buffer may still be in use by enqueued work
+      hipError_t e = hipFree(p);
+      if (e != hipSuccess) return e;
+      p = nullptr;
+      bytes = 0;
+    }
+    size_t cap = need + need / 8 + 256;  // headroom so small growth does not reallocate
+    hipError_t e = hipMalloc(&p, cap);
+    if (e != hipSuccess) return e;
+    bytes = cap;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  template <typename T> T* as() const { return static_cast<T*>(p); }
+};
+
+}  // namespace hj3d
+
+// Opaque handles of the C ABI.
+struct hj3d_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  int num_cus = 256;
+  std::string last_error;
+  // scratch arena slots (see api for their use)
+  hj3d::DevBuf scratch[8];
+  hj3d::DevBuf res;       // device result slot (u64 fields) for probe / probe2
+  hj3d::DevBuf misc;      // small device reductions (statistics)
+  uint32_t res_flags = 0;     // flags of the last probe (overflow check in hj3d_probe_result)
+  bool res_dense = false;     // last probe emitted one slot per probe tuple
+  uint64_t res_cap = ~0ull;   // output capacity of the last probe
+  uint64_t res_nprobe = 0;    // probe tuples of the last probe
+  // phase timers
+  bool timing = false;
+  struct Span { hipEvent_t a, b; };
+  std::vector<Span> spans[HJ3D_T_NTIMERS];
+  std::vector<hipEvent_t> event_pool;
+  size_t pool_used = 0;
+};
+
+struct hj3d_table {
+  hj3d_table_desc desc{};
+  uint32_t nb_local = 0;  // bucket_hi - bucket_lo
+  hj3d::FastMod fm{};
+  uint64_t n_build = 0;   // tuples in the last build (host-known)
+  bool built = false;
+  // chaining: off[nb_local+1] (u32 CSR offsets), ent[n] = {hash, row}
+  // nested:   off[nb_local+1] over mains, main[d] = {hash, first_row, sub_off, sub_len},
+  //           sub[n] = build rows grouped per key (first occurrence first, then row order)
+  hj3d::DevBuf off, ent, main, sub;
+  hj3d::DevBuf counts;    // device u64[4]: {entries, distinct, max_sub_len, reserved}
+};
+
+namespace hj3d {
+
+// ---- launchers (defined in the .hip translation units); all asynchronous on `s` ----
+// scan.hip: exclusive prefix sum of n values into out[0..n], out[n] = total. in may alias out.
+hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
+hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
+// sort.hip: stable LSD radix sort of (key,val) u32 pairs on key bits [0, bits). Result lands in
+// (k0,v0); (k1,v1) is a same-size scratch double buffer.
+hipError_t radix_sort_pairs(hj3d_ctx* ctx, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n,
+                            int bits, hipStream_t s);
+// chain.hip
+hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                       uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+// nested.hip
+hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                        uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+// exp4.hip
+hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel& r, uint32_t flags,
+                  void* out, uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+// stats.hip
+hipError_t table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out, hipStream_t s);
+// part.hip
+hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t nparts, void* out_pairs,
+                     void* counts, hipStream_t s);
+hipError_t gen_keys(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base,
+                    uint64_t n_keys, uint64_t seed, hipStream_t s);
+hipError_t gen_fk(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,
+                  uint64_t seed, hipStream_t s);
+hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel& probe, uint64_t n_keys,
+                            bool swap, void* res, hipStream_t s);
+hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n_keys, uint64_t seed, bool swap,
+                                void* res, hipStream_t s);
+
+// Scratch slot ids in hj3d_ctx::scratch.
+enum ScratchSlot { kScrScan = 0, kScrSlot = 1, kScrSortK = 2, kScrSortV = 3, kScrA = 4, kScrB = 5, kScrC = 6, kScrD = 7 };
+
+inline RelView view_of(const hj3d_rel& r) {
+  RelView v;
+  v.base = static_cast<const char*>(r.base);
+  v.n = r.n;
+  v.stride = r.stride;
+  v.key_off = r.key_off;
+  v.row_off = r.row_off;
+  v.pad = 0;
+  v.row_base = r.row_base;
+  return v;
+}
+
+// Grid for grid-stride streaming kernels: enough blocks to fill the chip (>= 8 per CU),
+// bounded so that per-block result flushes stay cheap.
+inline unsigned grid_for(const hj3d_ctx* ctx, uint64_t items, unsigned items_per_block) {
+  const uint64_t want = (items + items_per_block - 1) / items_per_block;
+  const uint64_t cap = uint64_t(ctx->num_cus) * 8;
+  uint64_t g = want < cap ? want : cap;
+  return unsigned(g < 1 ? 1 : g);
+}
+
+}  // namespace hj3d

@@ -1,0 +1,366 @@
+// nested.hip — the nested ("3D") hash table (HtNested1, ht_nested.hh) on MI355X.
+//
+// Layout (replaces 32-B MainNodes + 16-B SubNodes chained by pointers):
+//   off[b]   u32, b in [0, nb_local]: main records of bucket b are main[off[b] .. off[b+1])
+//   main[m]  {u32 hash, u32 first_row, u32 sub_off, u32 sub_len}  one per distinct key (16 B)
+//   sub[j]   u32 build rows, grouped per key: sub[sub_off .. sub_off+sub_len) (4 B / tuple)
+// first_row is the key's first inserted tuple = MainNode::data() (ht_nested.hh:386-396).
+// The reference keeps a bucket's main nodes in first-occurrence order (tail append,
+// ht_nested.hh:299-308); the probe reproduces findMainNodeByOther's comparison count
+// (ht_nested.hh:354-382) as 1 + #(mains of the bucket with a smaller first_row).
+//
+// Build: (hash,row) pairs -> stable radix sort by hash (sort.hip) -> run heads -> one main
+// record per run (first row = segmented min) -> bucket CSR of the main records.
+// Probe: as chaining, over main records. Unnest (AlgUnnestHt, algebra.hh:510-541): light
+// matches (<= kInline rows) are expanded by the probing thread; heavy ones (Zipf hot keys)
+// are queued and expanded by whole workgroups, so one hot key cannot serialize a thread.
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kItems = 4;
+constexpr uint32_t kInline = 32;
+
+__device__ __forceinline__ bool is_head(const uint32_t* hk, uint64_t e) { return e == 0 || hk[e] != hk[e - 1]; }
+
+__global__ __launch_bounds__(kBlock) void k_extract(RelView r, FastMod fm, uint32_t lo, uint32_t nbl,
+                                                    uint32_t* __restrict__ hk, uint32_t* __restrict__ rv,
+                                                    uint64_t* __restrict__ counts) {
+  uint64_t owned = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t h = murmur32(r.key(i));
+    hk[i] = h;
+    rv[i] = r.row(i);
+    owned += (fm.mod(h) - lo) < nbl;
+  }
+  uint64_t v[1] = {owned};
+  block_flush<1, 0>(v, counts);  // counts[0] = stored tuples (HtStatistics::_numEntries)
+}
+
+__global__ __launch_bounds__(kBlock) void k_heads(const uint32_t* __restrict__ hk, uint64_t n, uint32_t* __restrict__ x) {
+  for (uint64_t e = uint64_t(blockIdx.x) * kBlock + threadIdx.x; e < n; e += uint64_t(gridDim.x) * kBlock)
+    x[e] = is_head(hk, e) ? 1u : 0u;
+}
+
+// One main record per run: hash and run start; first_row initialised for the min pass.
+__global__ __launch_bounds__(kBlock) void k_runs(const uint32_t* __restrict__ hk, uint64_t n,
+                                                 const uint32_t* __restrict__ x, uint32_t* __restrict__ mh,
+                                                 uint32_t* __restrict__ msub, uint32_t* __restrict__ mfirst) {
+  for (uint64_t e = uint64_t(blockIdx.x) * kBlock + threadIdx.x; e < n; e += uint64_t(gridDim.x) * kBlock) {
+    if (!is_head(hk, e)) continue;
+    const uint32_t m = x[e];
+    mh[m] = hk[e];
+    msub[m] = uint32_t(e);
+    mfirst[m] = kInvalid;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) msub[x[n]] = uint32_t(n);
+}
+
+// first_row of every run = min row id in the run (segmented wave min + one atomicMin per
+// wave-segment; a hot key's long run costs one atomic per wave, not per tuple).
+__global__ __launch_bounds__(kBlock) void k_run_min(const uint32_t* __restrict__ hk, const uint32_t* __restrict__ rv,
+                                                    uint64_t n, const uint32_t* __restrict__ x,
+                                                    uint32_t* __restrict__ mfirst) {
+  const int lane = threadIdx.x & 63;
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock;
+  for (uint64_t base = uint64_t(blockIdx.x) * kBlock; base < n; base += stride) {
+    const uint64_t e = base + threadIdx.x;
+    const bool valid = e < n;
+    const uint32_t m = valid ? (is_head(hk, e) ? x[e] : x[e] - 1u) : kInvalid;
+    uint32_t v = valid ? rv[e] : kInvalid;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_down(v, o, kWave);
+      const uint32_t my = __shfl_down(m, o, kWave);
+      if (lane + o < 64 && my == m) v = min(v, y);
+    }
+    const uint32_t mp = __shfl_up(m, 1, kWave);
+    if (valid && (lane == 0 || mp != m)) atomicMin(&mfirst[m], v);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_main_count(const uint32_t* __restrict__ mh, const uint32_t* __restrict__ x,
+                                                       uint64_t n, FastMod fm, uint32_t lo, uint32_t nbl,
+                                                       uint32_t* __restrict__ off, uint32_t* __restrict__ mslot) {
+  const uint32_t d = x[n];
+  for (uint64_t m = uint64_t(blockIdx.x) * kBlock + threadIdx.x; m < d; m += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t b = fm.mod(mh[m]) - lo;
+    mslot[m] = b < nbl ? atomicAdd(&off[b], 1u) : kInvalid;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_main_scatter(const uint32_t* __restrict__ mh,
+                                                         const uint32_t* __restrict__ mfirst,
+                                                         const uint32_t* __restrict__ msub,
+                                                         const uint32_t* __restrict__ mslot,
+                                                         const uint32_t* __restrict__ x, uint64_t n, FastMod fm,
+                                                         uint32_t lo, const uint32_t* __restrict__ off,
+                                                         uint4* __restrict__ mains, uint64_t* __restrict__ counts) {
+  const uint32_t d = x[n];
+  uint64_t nd = 0, mx = 0;
+  for (uint64_t m = uint64_t(blockIdx.x) * kBlock + threadIdx.x; m < d; m += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t sl = mslot[m];
+    if (sl == kInvalid) continue;
+    const uint32_t b = fm.mod(mh[m]) - lo;
+    const uint32_t len = msub[m + 1] - msub[m];
+    mains[off[b] + sl] = make_uint4(mh[m], mfirst[m], msub[m], len);
+    ++nd;
+    mx = len > mx ? len : mx;
+  }
+  uint64_t v[1] = {nd};
+  block_flush<1, 0>(v, counts + 1);  // distinct keys
+  const uint64_t wm = wave_max(mx);
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(reinterpret_cast<unsigned long long*>(counts + 2), wm);
+}
+
+enum NMode { kAggNU = 0, kDenseNU = 1, kAggUN = 2, kCountUN = 3 };
+
+struct Heavy {
+  uint32_t probe_row;
+  uint32_t main_idx;
+};
+
+// Probe strand over the nested table. kAggNU / kDenseNU: AlgNestJoinProbe -> AlgTop (nested
+// tuples). kAggUN: AlgNestJoinProbe -> AlgUnnestHt -> AlgTop. kCountUN: like kAggUN but
+// records per probe tuple its output count (cnt) and matched main (mid) for a scan + expand.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_nested_probe(RelView r, FastMod fm, uint32_t lo, uint32_t nbl,
+                                                         const uint32_t* __restrict__ off,
+                                                         const uint4* __restrict__ mains,
+                                                         const uint32_t* __restrict__ sub,
+                                                         uint2* __restrict__ out, uint64_t out_cap,
+                                                         uint64_t* __restrict__ cnt, uint32_t* __restrict__ mid,
+                                                         Heavy* __restrict__ heavy, uint64_t* __restrict__ nheavy,
+                                                         uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t stride = uint64_t(gridDim.x) * kBlock * kItems;
+  for (uint64_t base = uint64_t(blockIdx.x) * kBlock * kItems; base < r.n; base += stride) {
+    uint32_t h[kItems], b[kItems], pr[kItems], s[kItems], e[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+      const bool v = i < r.n;
+      h[j] = murmur32(v ? r.key(i) : 0u);
+      pr[j] = v ? r.row(i) : 0u;
+      b[j] = v ? fm.mod(h[j]) - lo : kInvalid;
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      s[j] = 0;
+      e[j] = 0;
+      if (b[j] < nbl) {
+        s[j] = off[b[j]];
+        e[j] = off[b[j] + 1];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+      if (i >= r.n) continue;
+      acc[0] += 1;
+      uint32_t found = kInvalid;
+      uint4 M = make_uint4(0, 0, 0, 0);
+      for (uint32_t k = s[j]; k < e[j]; ++k) {
+        const uint4 c = mains[k];
+        if (c.x == h[j]) {
+          found = k;
+          M = c;
+          break;
+        }
+      }
+      if (found == kInvalid) {
+        acc[3] += e[j] - s[j];
+      } else {
+        uint32_t before = 0;  // mains of this bucket inserted before the matching one
+        for (uint32_t k = s[j]; k < e[j]; ++k) before += mains[k].y < M.y;
+        acc[3] += 1 + before;
+        acc[1] += 1;
+      }
+      if (MODE == kAggNU || MODE == kDenseNU) {
+        if (found != kInvalid) {
+          acc[2] += 1;
+          acc[4] += pr[j];
+          acc[5] += M.y;
+          const uint64_t ph = pair_hash(pr[j], M.y);
+          acc[7] += ph;
+          acc[8] ^= ph;
+        }
+        if (MODE == kDenseNU && i < out_cap) out[i] = make_uint2(pr[j], found == kInvalid ? kInvalid : M.y);
+      } else if (MODE == kAggUN) {
+        if (found != kInvalid) {
+          acc[2] += M.w;
+          if (M.w <= kInline) {
+            for (uint32_t q = 0; q < M.w; ++q) {
+              const uint32_t br = sub[M.z + q];
+              acc[4] += pr[j];
+              acc[5] += br;
+              const uint64_t ph = pair_hash(pr[j], br);
+              acc[7] += ph;
+              acc[8] ^= ph;
+            }
+          } else {
+            const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
+            heavy[slot] = Heavy{pr[j], found};
+          }
+        }
+      } else {  // kCountUN
+        acc[2] += found != kInvalid ? M.w : 0u;
+        cnt[i] = found != kInvalid ? M.w : 0u;
+        mid[i] = found;
+      }
+    }
+  }
+  block_flush<kProbeFields, 1>(acc, res);
+}
+
+// Heavy matches: one workgroup expands one (probe row, main) pair at a time.
+__global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict__ heavy,
+                                                         const uint64_t* __restrict__ nheavy,
+                                                         const uint4* __restrict__ mains,
+                                                         const uint32_t* __restrict__ sub, uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t nh = *nheavy;
+  for (uint64_t q = blockIdx.x; q < nh; q += gridDim.x) {
+    const Heavy hv = heavy[q];
+    const uint4 M = mains[hv.main_idx];
+    for (uint32_t k = threadIdx.x; k < M.w; k += kBlock) {
+      const uint32_t br = sub[M.z + k];
+      acc[4] += hv.probe_row;
+      acc[5] += br;
+      const uint64_t ph = pair_hash(hv.probe_row, br);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+  }
+  block_flush<kProbeFields, 1>(acc, res);
+}
+
+// Load-balanced unnest with materialisation: output position p belongs to the probe tuple i
+// with ooff[i] <= p < ooff[i+1]; each thread takes a run of kSpan consecutive positions and
+// binary-searches its first probe tuple once.
+constexpr int kSpan = 8;
+__global__ __launch_bounds__(kBlock) void k_expand_write(RelView r, const uint64_t* __restrict__ ooff,
+                                                         const uint32_t* __restrict__ mid,
+                                                         const uint4* __restrict__ mains,
+                                                         const uint32_t* __restrict__ sub, uint2* __restrict__ out,
+                                                         uint64_t out_cap, uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t total = ooff[r.n];
+  const uint64_t lim = total < out_cap ? total : out_cap;
+  for (uint64_t p0 = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) * kSpan; p0 < lim;
+       p0 += uint64_t(gridDim.x) * kBlock * kSpan) {
+    uint64_t lo = 0, hi = r.n;  // largest i with ooff[i] <= p0
+    while (hi - lo > 1) {
+      const uint64_t md = (lo + hi) >> 1;
+      if (ooff[md] <= p0) lo = md; else hi = md;
+    }
+    uint64_t i = lo;
+    for (uint64_t p = p0; p < p0 + kSpan && p < lim; ++p) {
+      while (ooff[i + 1] <= p) ++i;
+      const uint4 M = mains[mid[i]];
+      const uint32_t pr = r.row(i), br = sub[M.z + uint32_t(p - ooff[i])];
+      out[p] = make_uint2(pr, br);
+      acc[4] += pr;
+      acc[5] += br;
+      const uint64_t ph = pair_hash(pr, br);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+  }
+  block_flush<kProbeFields, 1>(acc, res);
+}
+
+}  // namespace
+
+hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+  hipError_t e;
+  const uint64_t n = r.n;
+  const uint64_t nn = n ? n : 1;
+  const uint32_t lo = uint32_t(t->desc.bucket_lo), nbl = t->nb_local;
+  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->main.ensure(nn * sizeof(uint4))) != hipSuccess) return e;
+  if ((e = t->sub.ensure(nn * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
+  // scratch: hk | k1 | v1 | x(n+1) | mh | msub(n+1) | mfirst | mslot
+  if ((e = ctx->scratch[kScrSortK].ensure(3 * nn * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrB].ensure((5 * nn + 2) * sizeof(uint32_t))) != hipSuccess) return e;
+  uint32_t* hk = ctx->scratch[kScrSortK].as<uint32_t>();
+  uint32_t* k1 = hk + nn;
+  uint32_t* v1 = k1 + nn;
+  uint32_t* x = ctx->scratch[kScrB].as<uint32_t>();
+  uint32_t* mh = x + nn + 1;
+  uint32_t* msub = mh + nn;
+  uint32_t* mfirst = msub + nn + 1;
+  uint32_t* mslot = mfirst + nn;
+  uint32_t* rows = t->sub.as<uint32_t>();
+  uint32_t* off = t->off.as<uint32_t>();
+  uint64_t* counts = t->counts.as<uint64_t>();
+  if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(off, 0, (uint64_t(nbl) + 1) * sizeof(uint32_t), s)) != hipSuccess) return e;
+  const RelView v = view_of(r);
+  const unsigned g = grid_for(ctx, nn, kBlock * 4);
+  if (n) {
+    hipLaunchKernelGGL(k_extract, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, hk, rows, counts);
+    if ((e = radix_sort_pairs(ctx, hk, rows, k1, v1, n, 32, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, s, hk, n, x);
+    if ((e = exclusive_scan_u32(ctx, x, x, n, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_runs, dim3(g), dim3(kBlock), 0, s, hk, n, x, mh, msub, mfirst);
+    hipLaunchKernelGGL(k_run_min, dim3(g), dim3(kBlock), 0, s, hk, rows, n, x, mfirst);
+    hipLaunchKernelGGL(k_main_count, dim3(g), dim3(kBlock), 0, s, mh, x, n, t->fm, lo, nbl, off, mslot);
+  }
+  if ((e = exclusive_scan_u32(ctx, off, off, nbl, s)) != hipSuccess) return e;
+  if (n) {
+    hipLaunchKernelGGL(k_main_scatter, dim3(g), dim3(kBlock), 0, s, mh, mfirst, msub, mslot, x, n, t->fm, lo, off,
+                       t->main.as<uint4>(), counts);
+  }
+  t->n_build = n;
+  return hipGetLastError();
+}
+
+hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                        uint64_t out_cap, uint64_t* res, hipStream_t s) {
+  if (r.n == 0) return hipSuccess;
+  const RelView v = view_of(r);
+  const bool unnest = flags & HJ3D_PROBE_UNNEST;
+  const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
+  const uint32_t lo = uint32_t(t->desc.bucket_lo), nbl = t->nb_local;
+  const uint32_t* off = t->off.as<const uint32_t>();
+  const uint4* mains = t->main.as<const uint4>();
+  const uint32_t* sub = t->sub.as<const uint32_t>();
+  uint2* o = static_cast<uint2*>(out);
+  const unsigned g = grid_for(ctx, r.n, kBlock * kItems);
+  hipError_t e;
+  if (!unnest) {
+    if (emit)
+      hipLaunchKernelGGL(k_nested_probe<kDenseNU>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub, o,
+                         out_cap, nullptr, nullptr, nullptr, nullptr, res);
+    else
+      hipLaunchKernelGGL(k_nested_probe<kAggNU>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub,
+                         nullptr, 0, nullptr, nullptr, nullptr, nullptr, res);
+    return hipGetLastError();
+  }
+  if (!emit) {
+    if ((e = ctx->scratch[kScrC].ensure(r.n * sizeof(Heavy) + 16)) != hipSuccess) return e;
+    uint64_t* nheavy = ctx->scratch[kScrC].as<uint64_t>();
+    Heavy* heavy = reinterpret_cast<Heavy*>(nheavy + 2);
+    if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint64_t), s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nested_probe<kAggUN>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub,
+                       nullptr, 0, nullptr, nullptr, heavy, nheavy, res);
+    hipLaunchKernelGGL(k_expand_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, heavy, nheavy, mains, sub, res);
+    return hipGetLastError();
+  }
+  // materialised unnest: count -> scan -> load-balanced expansion
+  if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrC].ensure(r.n * sizeof(uint32_t) + 16)) != hipSuccess) return e;
+  uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
+  uint32_t* mid = ctx->scratch[kScrC].as<uint32_t>();
+  hipLaunchKernelGGL(k_nested_probe<kCountUN>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub,
+                     nullptr, 0, cnt, mid, nullptr, nullptr, res);
+  if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_expand_write, dim3(ctx->num_cus * 8), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, o, out_cap,
+                     res);
+  return hipGetLastError();
+}
+
+}  // namespace hj3d

@@ -1,0 +1,260 @@
+// part.hip — multi-GPU exchange helpers and on-device synthetic relations.
+//
+// Bucket-range partition: owner(bucket) = bucket * P / NB, so every GPU owns a
+// contiguous range of the global directory and its statistics / comparison counts are those of
+// the single-table reference. Tuples leave as 8-B (key, global row) pairs, grouped by owner,
+// stable (input order kept within an owner). Same tile/ballot machinery as sort.hip.
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kRounds = 16;
+constexpr int kTile = kBlock * kRounds;
+constexpr int kWaves = kBlock / kWave;
+constexpr int kMaxParts = 256;
+
+__device__ __forceinline__ uint32_t owner_of(uint32_t key, FastMod fm, uint64_t nb, uint32_t parts) {
+  const uint64_t b = fm.mod(murmur32(key));
+  return uint32_t((b * parts) / nb);
+}
+
+__global__ __launch_bounds__(kBlock) void k_part_hist(RelView r, FastMod fm, uint64_t nb, uint32_t parts,
+                                                      uint32_t ntiles, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t h[kMaxParts];
+  h[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t base = uint64_t(blockIdx.x) * kTile;
+  for (int j = 0; j < kRounds; ++j) {
+    const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+    if (i < r.n) atomicAdd(&h[owner_of(r.key(i), fm, nb, parts)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < parts) hist[uint64_t(threadIdx.x) * ntiles + blockIdx.x] = h[threadIdx.x];
+}
+
+__global__ __launch_bounds__(kBlock) void k_part_scatter(RelView r, FastMod fm, uint64_t nb, uint32_t parts,
+                                                         uint32_t ntiles, const uint32_t* __restrict__ offs,
+                                                         uint2* __restrict__ out) {
+  __shared__ uint32_t run[kMaxParts];
+  __shared__ uint32_t wcnt[kWaves][kMaxParts];
+  __shared__ uint32_t tbase[kMaxParts];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  run[threadIdx.x] = 0;
+  tbase[threadIdx.x] = threadIdx.x < parts ? offs[uint64_t(threadIdx.x) * ntiles + blockIdx.x] : 0u;
+  const uint64_t base = uint64_t(blockIdx.x) * kTile;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (int j = 0; j < kRounds; ++j) {
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+    const bool valid = i < r.n;
+    const uint32_t key = valid ? r.key(i) : 0u;
+    const uint32_t row = valid ? r.row(i) : 0u;
+    const uint32_t d = valid ? owner_of(key, fm, nb, parts) : 0u;
+    uint64_t peer = __ballot(valid);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const bool set = (d >> bit) & 1u;
+      const uint64_t bb = __ballot(set);
+      peer &= set ? bb : ~bb;
+    }
+    const uint32_t wrank = uint32_t(__popcll(peer & lt));
+    if (valid && wrank == 0) wcnt[wid][d] = uint32_t(__popcll(peer));
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[d] + wrank;
+      for (int w = 0; w < wid; ++w) pos += wcnt[w][d];
+      out[uint64_t(tbase[d]) + pos] = make_uint2(key, row);
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) add += wcnt[w][threadIdx.x];
+    run[threadIdx.x] += add;
+  }
+}
+
+__global__ void k_part_counts(const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t parts,
+                              uint64_t* __restrict__ counts) {
+  const uint32_t p = threadIdx.x;
+  if (p < parts) counts[p] = uint64_t(offs[uint64_t(p + 1) * ntiles]) - offs[uint64_t(p) * ntiles];
+}
+
+// Bijective permutation of [0, n): 4-round Feistel network on the smallest even-bit domain
+// >= n, with cycle walking back into [0, n).
+struct Feistel {
+  uint64_t n, seed;
+  uint32_t half;
+  uint64_t mask;
+  __host__ __device__ static Feistel make(uint64_t n, uint64_t seed) {
+    Feistel f;
+    f.n = n;
+    f.seed = seed;
+    uint32_t bits = 0;
+    while (bits < 64 && (1ull << bits) < n) ++bits;
+    f.half = (bits + 1) / 2;
+    if (f.half == 0) f.half = 1;
+    f.mask = (1ull << f.half) - 1;
+    return f;
+  }
+  __host__ __device__ uint64_t round_fn(uint64_t x, int k) const {
+    return mix64(x ^ (seed + 0x9e3779b97f4a7c15ull * uint64_t(k + 1))) & mask;
+  }
+  __host__ __device__ uint64_t enc1(uint64_t x) const {
+    uint64_t L = x >> half, R = x & mask;
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t t = L ^ round_fn(R, k);
+      L = R;
+      R = t;
+    }
+    return (L << half) | R;
+  }
+  __host__ __device__ uint64_t dec1(uint64_t x) const {
+    uint64_t L = x >> half, R = x & mask;
+    for (int k = 3; k >= 0; --k) {
+      const uint64_t t = R ^ round_fn(L, k);
+      R = L;
+      L = t;
+    }
+    return (L << half) | R;
+  }
+  __host__ __device__ uint64_t perm(uint64_t x) const {
+    if (n <= 1) return 0;
+    uint64_t y = enc1(x);
+    while (y >= n) y = enc1(y);
+    return y;
+  }
+  __host__ __device__ uint64_t inv(uint64_t y) const {
+    if (n <= 1) return 0;
+    uint64_t x = dec1(y);
+    while (x >= n) x = dec1(x);
+    return x;
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void k_gen_keys(char* __restrict__ t, uint64_t n, uint32_t stride,
+                                                     uint32_t key_off, uint64_t row_base, Feistel f, bool identity) {
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint64_t g = row_base + i;
+    *reinterpret_cast<uint32_t*>(t + i * stride + key_off) = uint32_t(identity ? g : f.perm(g));
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_gen_fk(char* __restrict__ t, uint64_t n, uint32_t stride,
+                                                   uint32_t key_off, uint64_t row_base, uint32_t fk_max,
+                                                   uint64_t seed) {
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint64_t x = mix64((row_base + i) ^ seed);
+    *reinterpret_cast<uint32_t*>(t + i * stride + key_off) = uint32_t(((x >> 32) * uint64_t(fk_max)) >> 32);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_inv(RelView b, uint64_t n_keys, uint32_t* __restrict__ inv) {
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t k = b.key(i);
+    if (k < n_keys) inv[k] = b.row(i);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void k_expect(RelView p, uint64_t n_keys, const uint32_t* __restrict__ inv,
+                                                   bool swap, uint64_t* __restrict__ res) {
+  uint64_t a[5] = {0, 0, 0, 0, 0};
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t k = p.key(i);
+    if (k >= n_keys) continue;
+    const uint32_t x = swap ? inv[k] : p.row(i), y = swap ? p.row(i) : inv[k];
+    const uint64_t h = pair_hash(x, y);
+    a[0] += 1;
+    a[1] += x;
+    a[2] += y;
+    a[3] += h;
+    a[4] ^= h;
+  }
+  block_flush<5, 1>(a, res);
+}
+
+// Expected key/FK pairs when the build keys came from k_gen_keys(n_keys, seed): the partner
+// of FK k is the build row perm^-1(k) (no table, no inverse array: works per rank).
+__global__ __launch_bounds__(kBlock) void k_expect_gen(RelView p, Feistel f, bool swap, uint64_t* __restrict__ res) {
+  uint64_t a[5] = {0, 0, 0, 0, 0};
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < p.n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t k = p.key(i);
+    if (k >= f.n) continue;
+    const uint32_t br = uint32_t(f.inv(k)), pr = p.row(i);
+    const uint32_t x = swap ? br : pr, y = swap ? pr : br;
+    const uint64_t h = pair_hash(x, y);
+    a[0] += 1;
+    a[1] += x;
+    a[2] += y;
+    a[3] += h;
+    a[4] ^= h;
+  }
+  block_flush<5, 1>(a, res);
+}
+
+}  // namespace
+
+hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n_keys, uint64_t seed, bool swap,
+                                void* res, hipStream_t s) {
+  if (probe.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_expect_gen, dim3(grid_for(ctx, probe.n, kBlock * 4)), dim3(kBlock), 0, s, view_of(probe),
+                     Feistel::make(n_keys, seed), swap, static_cast<uint64_t*>(res));
+  return hipGetLastError();
+}
+
+hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t parts, void* out_pairs, void* counts,
+                     hipStream_t s) {
+  if (parts == 0 || parts > kMaxParts || nb == 0 || nb >= (1ull << 32)) return hipErrorInvalidValue;
+  hipError_t e;
+  const uint64_t ntiles = (r.n + kTile - 1) / kTile;
+  if (r.n == 0) return hipMemsetAsync(counts, 0, parts * sizeof(uint64_t), s);
+  if ((e = ctx->scratch[kScrD].ensure((uint64_t(parts) * ntiles + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  uint32_t* hist = ctx->scratch[kScrD].as<uint32_t>();
+  const FastMod fm = FastMod::make(uint32_t(nb));
+  const RelView v = view_of(r);
+  hipLaunchKernelGGL(k_part_hist, dim3(unsigned(ntiles)), dim3(kBlock), 0, s, v, fm, nb, parts, uint32_t(ntiles), hist);
+  if ((e = exclusive_scan_u32(ctx, hist, hist, uint64_t(parts) * ntiles, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_part_scatter, dim3(unsigned(ntiles)), dim3(kBlock), 0, s, v, fm, nb, parts, uint32_t(ntiles),
+                     hist, static_cast<uint2*>(out_pairs));
+  hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(kMaxParts), 0, s, hist, uint32_t(ntiles), parts,
+                     static_cast<uint64_t*>(counts));
+  return hipGetLastError();
+}
+
+hipError_t gen_keys(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint64_t n_keys,
+                    uint64_t seed, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const Feistel f = Feistel::make(n_keys, seed);
+  const unsigned g = unsigned(n / kBlock + 1 < 4096 ? n / kBlock + 1 : 4096);
+  hipLaunchKernelGGL(k_gen_keys, dim3(g), dim3(kBlock), 0, s, static_cast<char*>(tuples), n, stride, key_off, row_base,
+                     f, n_keys == 0);
+  return hipGetLastError();
+}
+
+hipError_t gen_fk(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,
+                  uint64_t seed, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const unsigned g = unsigned(n / kBlock + 1 < 4096 ? n / kBlock + 1 : 4096);
+  hipLaunchKernelGGL(k_gen_fk, dim3(g), dim3(kBlock), 0, s, static_cast<char*>(tuples), n, stride, key_off, row_base,
+                     fk_max, seed);
+  return hipGetLastError();
+}
+
+hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel& probe, uint64_t n_keys, bool swap,
+                            void* res, hipStream_t s) {
+  hipError_t e = ctx->scratch[kScrD].ensure((n_keys ? n_keys : 1) * sizeof(uint32_t));
+  if (e != hipSuccess) return e;
+  uint32_t* inv = ctx->scratch[kScrD].as<uint32_t>();
+  if ((e = hipMemsetAsync(inv, 0xFF, (n_keys ? n_keys : 1) * sizeof(uint32_t), s)) != hipSuccess) return e;
+  const RelView b = view_of(build), p = view_of(probe);
+  if (build.n)
+    hipLaunchKernelGGL(k_inv, dim3(grid_for(ctx, build.n, kBlock * 4)), dim3(kBlock), 0, s, b, n_keys, inv);
+  if (probe.n)
+    hipLaunchKernelGGL(k_expect, dim3(grid_for(ctx, probe.n, kBlock * 4)), dim3(kBlock), 0, s, p, n_keys, inv,
+                       swap, static_cast<uint64_t*>(res));
+  return hipGetLastError();
+}
+
+}  // namespace hj3d

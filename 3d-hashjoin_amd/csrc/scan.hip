@@ -1,0 +1,145 @@
+// scan.hip — exclusive prefix sums (CSR directory offsets, output offsets).
+//
+// Reduce-then-scan in three launches over 4096-element tiles: (1) per-tile sums,
+// (2) one workgroup scans the tile sums, (3) per-tile scan with the tile's offset.
+// HBM traffic: 2 reads + 1 write of the array. Used for bucket offsets (NB+1 u32)
+// and per-probe output offsets (u64).
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kScanItems = 16;
+constexpr int kTile = kBlock * kScanItems;  // 4096
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* lds) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, kWave);
+  if (lane == 0) lds[wid] = v;
+  __syncthreads();
+  T r = 0;
+  for (int w = 0; w < kBlock / kWave; ++w) r += lds[w];
+  return r;
+}
+
+// Block-wide exclusive scan of one value per thread; returns the exclusive prefix and the total.
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T v, T* lds, T* total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  T x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const T y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) lds[wid] = x;
+  __syncthreads();
+  T wpre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    const T s = lds[w];
+    if (w < wid) wpre += s;
+    tot += s;
+  }
+  *total = tot;
+  return wpre + x - v;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_tile_sums(const T* __restrict__ in, uint64_t n, T* __restrict__ sums) {
+  __shared__ T lds[kBlock / kWave];
+  const uint64_t base = uint64_t(blockIdx.x) * kTile;
+  T acc = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
+    if (i < n) acc += in[i];
+  }
+  const T s = block_sum(acc, lds);
+  if (threadIdx.x == 0) sums[blockIdx.x] = s;
+}
+
+// One workgroup (1024 threads) scans `m` tile sums in place (exclusive); sums[m] = total.
+template <typename T>
+__global__ __launch_bounds__(1024) void k_scan_sums(T* sums, uint64_t m) {
+  __shared__ T lds[1024 / kWave];
+  __shared__ T carry_s;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  for (uint64_t base = 0; base < m; base += 1024) {
+    const uint64_t i = base + threadIdx.x;
+    const T v = i < m ? sums[i] : T(0);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    T x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const T y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) lds[wid] = x;
+    __syncthreads();
+    T wpre = 0, tot = 0;
+    for (int w = 0; w < 1024 / kWave; ++w) {
+      const T s = lds[w];
+      if (w < wid) wpre += s;
+      tot += s;
+    }
+    const T carry = carry_s;
+    if (i < m) sums[i] = carry + wpre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s = carry + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) sums[m] = carry_s;
+}
+
+// Per-tile exclusive scan. Thread t owns the kScanItems consecutive elements
+// [base + t*kScanItems, ...) so the scan order is the element order.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scan_tiles(const T* in, T* out, uint64_t n, const T* __restrict__ sums) {
+  __shared__ T lds[kBlock / kWave];
+  const uint64_t base = uint64_t(blockIdx.x) * kTile + uint64_t(threadIdx.x) * kScanItems;
+  T v[kScanItems];
+  T local = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint64_t i = base + j;
+    v[j] = i < n ? in[i] : T(0);
+    local += v[j];
+  }
+  T total;
+  T pre = block_excl_scan(local, lds, &total) + sums[blockIdx.x];
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint64_t i = base + j;
+    if (i < n) out[i] = pre;
+    pre += v[j];
+  }
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = sums[gridDim.x];
+}
+
+template <typename T>
+hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t s) {
+  if (n == 0) return hipMemsetAsync(out, 0, sizeof(T), s);
+  const uint64_t tiles = (n + kTile - 1) / kTile;
+  hipError_t e = ctx->scratch[kScrScan].ensure((tiles + 1) * sizeof(T));
+  if (e != hipSuccess) return e;
+  T* sums = ctx->scratch[kScrScan].as<T>();
+  hipLaunchKernelGGL(k_tile_sums<T>, dim3(unsigned(tiles)), dim3(kBlock), 0, s, in, n, sums);
+  hipLaunchKernelGGL(k_scan_sums<T>, dim3(1), dim3(1024), 0, s, sums, tiles);
+  hipLaunchKernelGGL(k_scan_tiles<T>, dim3(unsigned(tiles)), dim3(kBlock), 0, s, in, out, n, sums);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
+  return excl_scan<uint32_t>(ctx, in, out, n, s);
+}
+hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
+  return excl_scan<uint64_t>(ctx, in, out, n, s);
+}
+
+}  // namespace hj3d

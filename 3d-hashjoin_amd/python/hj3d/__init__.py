@@ -1,0 +1,330 @@
+"""hj3d — Python plumbing over the C ABI of libhj3d.so (include/hj3d.h).
+
+The product is the HIP library; this module only marshals torch device tensors (plain
+device pointers and sizes) into the C ABI for tests, the benchmark and the multi-GPU
+driver. There is no CPU fallback anywhere: if libhj3d.so is missing or no GPU is
+present, every compute entry point raises.
+
+Relations are torch tensors in device memory holding array-of-structs u32 tuples, e.g.
+the experiment-1 tuple {k, a, b} (main_experiment1.cc:86) is an (n, 3) int32 tensor.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(os.path.dirname(HERE))  # 3d-hashjoin_amd/
+LIB_PATH = os.environ.get("HJ3D_LIB", os.path.join(PKG_ROOT, "lib", "libhj3d.so"))
+HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "hj3d.h")
+
+HJ3D_OK, HJ3D_EINVAL, HJ3D_ENOMEM, HJ3D_EDEVICE, HJ3D_EUNSUPPORTED, HJ3D_EOVERFLOW = range(6)
+HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
+HJ3D_CHAIN, HJ3D_NESTED = 0, 1
+PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT = 0x1, 0x2, 0x4
+T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION = range(4)
+
+MASK64 = (1 << 64) - 1
+
+
+class Hj3dError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"hj3d status {status}: {msg}")
+        self.status = status
+
+
+class _Rel(C.Structure):
+    _fields_ = [("base", C.c_void_p), ("n", C.c_uint64), ("stride", C.c_uint32), ("key_off", C.c_uint32),
+                ("row_off", C.c_uint32), ("reserved", C.c_uint32), ("row_base", C.c_uint64)]
+
+
+class _Desc(C.Structure):
+    _fields_ = [("num_buckets", C.c_uint64), ("bucket_lo", C.c_uint64), ("bucket_hi", C.c_uint64),
+                ("kind", C.c_uint32), ("reserved", C.c_uint32)]
+
+
+class _ProbeRes(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("n_probe", "n_matched", "n_out", "n_cmps", "sum_a", "sum_b", "sum_c",
+                                          "sum_h", "xor_h")]
+
+
+class _Probe2Res(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp",
+                                          "c_unnest_1", "c_unnest_2", "c_top", "sum_a", "sum_b", "sum_c", "sum_h",
+                                          "xor_h")]
+
+
+class _Stats(C.Structure):
+    _fields_ = [(f, C.c_uint64) for f in ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum",
+                                          "cc0_cnt", "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")]
+
+
+_lib = None
+
+
+def lib():
+    """Load libhj3d.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libhj3d.so not found at {LIB_PATH}; build it with `make -C 3d-hashjoin_amd` "
+                          "or __graft_entry__.build()")
+    L = C.CDLL(LIB_PATH)
+    p, u64, u32, i32, st = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_int
+    R, D = C.POINTER(_Rel), C.POINTER(_Desc)
+    sig = {
+        "hj3d_mix64": (u64, [u64]),
+        "hj3d_ctx_create": (st, [i32, p, C.POINTER(p)]),
+        "hj3d_ctx_destroy": (None, [p]),
+        "hj3d_ctx_set_stream": (st, [p, p]),
+        "hj3d_ctx_stream": (p, [p]),
+        "hj3d_ctx_sync": (st, [p]),
+        "hj3d_last_error": (C.c_char_p, [p]),
+        "hj3d_ctx_timing": (st, [p, i32]),
+        "hj3d_ctx_timer": (st, [p, i32, C.POINTER(C.c_double), C.POINTER(u64)]),
+        "hj3d_ctx_timer_reset": (st, [p]),
+        "hj3d_table_create": (st, [p, D, C.POINTER(p)]),
+        "hj3d_table_destroy": (None, [p]),
+        "hj3d_table_reserve": (st, [p, p, u64]),
+        "hj3d_table_clear": (st, [p, p]),
+        "hj3d_build": (st, [p, p, R]),
+        "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
+        "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
+        "hj3d_probe": (st, [p, p, R, u32, p, u64]),
+        "hj3d_probe_result": (st, [p, C.POINTER(_ProbeRes)]),
+        "hj3d_probe2": (st, [p, p, p, R, u32, p, u64]),
+        "hj3d_probe2_result": (st, [p, C.POINTER(_Probe2Res)]),
+        "hj3d_partition": (st, [p, R, u64, u32, p, p]),
+        "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
+        "hj3d_gen_keys": (st, [p, p, u64, u32, u32, u64, u64, u64]),
+        "hj3d_gen_fk": (st, [p, p, u64, u32, u32, u64, u32, u64]),
+        "hj3d_expected_fk_join": (st, [p, R, R, u64, i32, p]),
+        "hj3d_expected_fk_join_gen": (st, [p, R, u64, u64, i32, p]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def declared_symbols() -> list[str]:
+    """Function names declared in include/hj3d.h (the ABI contract)."""
+    import re
+    text = open(HEADER_PATH).read()
+    return sorted(set(re.findall(r"\b(hj3d_[a-z0-9_]+)\s*\(", text)))
+
+
+def mix64(z: int) -> int:
+    z &= MASK64
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & MASK64
+    return z ^ (z >> 31)
+
+
+def pair_hash(a: int, b: int) -> int:
+    return mix64(((a & 0xFFFFFFFF) << 32) | (b & 0xFFFFFFFF))
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Rel:
+    """A device relation: AoS u32 tuples in a torch tensor (no copy)."""
+
+    def __init__(self, tensor, key_word: int, row_word: Optional[int] = None, row_base: int = 0, n: Optional[int] = None):
+        torch = _torch()
+        if not tensor.is_cuda:
+            raise ValueError("relations must live in device memory")
+        if tensor.dtype not in (torch.int32, torch.uint32) or tensor.dim() != 2 or not tensor.is_contiguous():
+            raise ValueError("relation tensor must be a contiguous (n, words) int32 tensor")
+        self.tensor = tensor
+        words = tensor.shape[1]
+        self.c = _Rel(tensor.data_ptr() if tensor.numel() else None, tensor.shape[0] if n is None else n,
+                      4 * words, 4 * key_word,
+                      HJ3D_ROW_IMPLICIT if row_word is None else 4 * row_word, 0, row_base)
+
+    @property
+    def n(self) -> int:
+        return self.c.n
+
+
+@dataclass
+class ProbeResult:
+    n_probe: int
+    n_matched: int
+    n_out: int
+    n_cmps: int
+    sum_a: int
+    sum_b: int
+    sum_c: int
+    sum_h: int
+    xor_h: int
+    overflow: bool = False
+
+
+class Context:
+    """hj3d_ctx: a device, the stream every call is enqueued on, scratch, event timers."""
+
+    def __init__(self, device: int = 0, stream=None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise RuntimeError("hj3d needs a GPU (torch.cuda.is_available() is False)")
+        L = lib()
+        torch.cuda.set_device(device)
+        if stream is None:
+            stream = torch.cuda.current_stream(device)
+        self.stream = stream
+        h = C.c_void_p()
+        self._check(L.hj3d_ctx_create(device, C.c_void_p(stream.cuda_stream), C.byref(h)), "hj3d_ctx_create", None)
+        self.h = h
+        self.device = device
+
+    def _check(self, status: int, what: str, h=-1):
+        if status != HJ3D_OK:
+            msg = lib().hj3d_last_error(self.h if h == -1 else h)
+            raise Hj3dError(status, f"{what}: {msg.decode() if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().hj3d_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        self._check(lib().hj3d_ctx_sync(self.h), "sync")
+
+    def timing(self, enable: bool = True):
+        self._check(lib().hj3d_ctx_timing(self.h, int(enable)), "timing")
+
+    def timer(self, phase: int):
+        ms, cnt = C.c_double(), C.c_uint64()
+        self._check(lib().hj3d_ctx_timer(self.h, phase, C.byref(ms), C.byref(cnt)), "timer")
+        return ms.value, cnt.value
+
+    def timer_reset(self):
+        self._check(lib().hj3d_ctx_timer_reset(self.h), "timer_reset")
+
+    # ---- probes ----
+    def probe(self, table: "Table", rel: Rel, unique: bool = False, unnest: bool = False, out=None,
+              fetch: bool = True) -> Optional[ProbeResult]:
+        flags = (PROBE_UNIQUE if unique else 0) | (PROBE_UNNEST if unnest else 0)
+        ptr, cap = None, 0
+        if out is not None:
+            flags |= PROBE_EMIT
+            ptr, cap = out.data_ptr(), out.numel() * out.element_size() // 8
+        self._check(lib().hj3d_probe(self.h, table.h, C.byref(rel.c), flags, ptr, cap), "hj3d_probe")
+        return self.probe_result() if fetch else None
+
+    def probe_result(self) -> ProbeResult:
+        r = _ProbeRes()
+        st = lib().hj3d_probe_result(self.h, C.byref(r))
+        if st not in (HJ3D_OK, HJ3D_EOVERFLOW):
+            self._check(st, "hj3d_probe_result")
+        return ProbeResult(*(getattr(r, f) for f, _ in _ProbeRes._fields_), overflow=st == HJ3D_EOVERFLOW)
+
+    def probe2(self, ts: "Table", tt: "Table", rel: Rel, fetch: bool = True) -> Optional[dict]:
+        self._check(lib().hj3d_probe2(self.h, ts.h, tt.h, C.byref(rel.c), 0, None, 0), "hj3d_probe2")
+        return self.probe2_result() if fetch else None
+
+    def probe2_result(self) -> dict:
+        r = _Probe2Res()
+        self._check(lib().hj3d_probe2_result(self.h, C.byref(r)), "hj3d_probe2_result")
+        return {f: getattr(r, f) for f, _ in _Probe2Res._fields_}
+
+    # ---- exchange / synthetic data ----
+    def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts):
+        self._check(lib().hj3d_partition(self.h, C.byref(rel.c), num_buckets, parts, out_pairs.data_ptr(),
+                                         counts.data_ptr()), "hj3d_partition")
+
+    def gen_keys(self, tensor, key_word: int, row_base: int, n_keys: int, seed: int):
+        """n_keys == 0: identity (k = global row id); else a seeded permutation of [0, n_keys)."""
+        self._check(lib().hj3d_gen_keys(self.h, tensor.data_ptr(), tensor.shape[0], 4 * tensor.shape[1],
+                                        4 * key_word, row_base, n_keys, seed), "hj3d_gen_keys")
+
+    def gen_fk(self, tensor, key_word: int, row_base: int, fk_max: int, seed: int):
+        self._check(lib().hj3d_gen_fk(self.h, tensor.data_ptr(), tensor.shape[0], 4 * tensor.shape[1],
+                                      4 * key_word, row_base, fk_max, seed), "hj3d_gen_fk")
+
+    def expected_fk_join(self, build: Rel, probe: Rel, n_keys: int, swap: bool = False) -> dict:
+        torch = _torch()
+        res = torch.zeros(8, dtype=torch.int64, device=f"cuda:{self.device}")
+        self._check(lib().hj3d_expected_fk_join(self.h, C.byref(build.c), C.byref(probe.c), n_keys, int(swap),
+                                                res.data_ptr()), "hj3d_expected_fk_join")
+        self.sync()
+        return _res5(res.cpu().tolist())
+
+    def expected_fk_join_gen(self, probe: Rel, n_keys: int, key_seed: int, swap: bool = False, res=None):
+        """Expected key/FK aggregates for build keys made by gen_keys(n_keys, key_seed); accumulates
+        into the device int64[8] tensor `res` when given (multi-GPU), else returns a dict."""
+        torch = _torch()
+        r = res if res is not None else torch.zeros(8, dtype=torch.int64, device=f"cuda:{self.device}")
+        self._check(lib().hj3d_expected_fk_join_gen(self.h, C.byref(probe.c), n_keys, key_seed, int(swap),
+                                                    r.data_ptr()), "hj3d_expected_fk_join_gen")
+        if res is not None:
+            return None
+        self.sync()
+        return _res5(r.cpu().tolist())
+
+
+def _res5(v):
+    v = [int(x) & MASK64 for x in v]
+    return {"n": v[0], "sum_a": v[1], "sum_b": v[2], "sum_h": v[3], "xor_h": v[4]}
+
+
+def part_range(num_buckets: int, parts: int, part: int):
+    lo, hi = C.c_uint64(), C.c_uint64()
+    lib().hj3d_part_range(num_buckets, parts, part, C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
+
+
+class Table:
+    """hj3d_table: a device-resident chaining (HtChaining1) or nested (HtNested1) hash table."""
+
+    def __init__(self, ctx: Context, kind: int, num_buckets: int, bucket_lo: int = 0, bucket_hi: Optional[int] = None):
+        self.ctx = ctx
+        desc = _Desc(num_buckets, bucket_lo, num_buckets if bucket_hi is None else bucket_hi, kind, 0)
+        h = C.c_void_p()
+        ctx._check(lib().hj3d_table_create(ctx.h, C.byref(desc), C.byref(h)), "hj3d_table_create")
+        self.h = h
+        self.kind = kind
+        self.num_buckets = num_buckets
+
+    def reserve(self, n: int):
+        self.ctx._check(lib().hj3d_table_reserve(self.ctx.h, self.h, n), "hj3d_table_reserve")
+
+    def build(self, rel: Rel):
+        self.ctx._check(lib().hj3d_build(self.ctx.h, self.h, C.byref(rel.c)), "hj3d_build")
+
+    def clear(self):
+        self.ctx._check(lib().hj3d_table_clear(self.ctx.h, self.h), "hj3d_table_clear")
+
+    def stats(self) -> dict:
+        s = _Stats()
+        self.ctx._check(lib().hj3d_table_stats(self.ctx.h, self.h, C.byref(s)), "hj3d_table_stats")
+        return {f: getattr(s, f) for f, _ in _Stats._fields_}
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().hj3d_table_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+from .plans import EXP1_PLANS, exp1_plan, exp4_plan, num_buckets_exp1  # noqa: E402,F401

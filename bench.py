@@ -1,0 +1,285 @@
+#!/usr/bin/env python3
+"""Benchmark of the experiment-1 key/FK join (BASELINE.json metric) on the hj3d engine.
+
+A "step" = one execution of the Csr plan (main_experiment1.cc:623-744): build the chaining
+table on R.k, then probe it with every S tuple (unique-key early exit) and materialise the
+output row-id pairs in HBM. Inputs are resident in HBM before timing. Per GPU:
+|R| = 1e7, |S| = 1e8 (BASELINE config B); with --gpus N (one process per GPU, torchrun) the
+relations are N times larger and bucket-range partitioned with an RCCL all-to-all per step
+(weak scaling).
+
+value = probe tuples/s (all ranks' probe tuples / max over ranks of the probe-phase time, the
+reference's t_probeStr); build_ms is reported beside it. ms_per_step = build + probe.
+"""
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
+
+METRIC = "probe tuples/s + build ms, exp1 key/FK |R|=1e7 |S|=1e8, 1/2/4/8 GPU"
+SEED_R, SEED_S = 0x5eed0001, 0x5eed0002
+PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--nR", type=int, default=10_000_000, help="|R| per GPU")
+    p.add_argument("--nS", type=int, default=100_000_000, help="|S| per GPU")
+    p.add_argument("--b", type=int, default=1, help="bucket scale-down (#buckets = |R| / b)")
+    p.add_argument("--no-emit", action="store_true", help="aggregate-only probe (no pair materialisation)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=20_000_000, help="S tuples probed by the CPU baseline")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_probe.json"))
+    p.add_argument("--json-out", default=None)
+    return p.parse_args()
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(R_host, S_host, nb, reps):
+    """The oracle's single-thread port of the reference Csr plan on a bounded sample, pinned
+    to one core (reported baseline, not the target)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as O  # CPU baseline leg only
+
+    out = {}
+
+    def run():
+        try:
+            core = sorted(os.sched_getaffinity(0))[-1]
+            os.sched_setaffinity(0, {core})  # this thread only
+            out["core"] = core
+        except (AttributeError, OSError):
+            pass
+        out["res"] = O.chain_plan(R_host, 0, S_host, 1, nb, True, agg=False, min_ms=0.0, min_reps=reps)
+
+    th = threading.Thread(target=run)
+    th.start()
+    th.join()
+    r = out["res"]
+    cpu_model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu_model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": len(S_host) / (r.probe_ns * 1e-9),
+        "unit": "probe tuples/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"Csr plan of the oracle (oracle/hj3d_oracle.c, pointer-chained reference layout): build all "
+                   f"{len(R_host)} R tuples, probe the first {len(S_host)} S tuples, {r.reps} reps, 1 pinned core"),
+        "build_ms": r.build_ns * 1e-6,
+        "probe_ms": r.probe_ns * 1e-6,
+        "host_cpu": cpu_model,
+        "nproc": os.cpu_count(),
+    }
+
+
+def main():
+    args = parse()
+    import torch
+    import hj3d
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+        from hj3d import dist as hdist
+        dist.init_process_group("nccl", device_id=dev)
+
+    def barrier():
+        if world > 1:
+            torch.distributed.barrier()
+
+    nR, nS = args.nR, args.nS
+    nR_tot = nR * world
+    nb = max(nR_tot // args.b, 1)
+    emit = not args.no_emit
+    ctx = hj3d.Context(local)
+    ctx.timing(True)
+
+    # ---- inputs (HBM-resident before timing): rank r holds global rows [r*n, (r+1)*n) ----
+    R = torch.zeros((nR, 3), dtype=torch.int32, device=dev)
+    S = torch.zeros((nS, 3), dtype=torch.int32, device=dev)
+    ctx.gen_keys(R, 0, rank * nR, nR_tot, SEED_R)     # R.k: permutation of [0, |R|)
+    ctx.gen_keys(S, 0, rank * nS, 0, 0)               # S.k: global row id
+    ctx.gen_fk(S, 1, rank * nS, nR_tot, SEED_S)       # S.a ~ U[0, |R|)
+    relR = hj3d.Rel(R, key_word=0, row_base=rank * nR)
+    relS = hj3d.Rel(S, key_word=1, row_base=rank * nS)
+
+    if world == 1:
+        table = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nb)
+        table.reserve(nR)
+        out = torch.empty((nS, 2), dtype=torch.int32, device=dev) if emit else None
+    else:
+        lo, hi = hj3d.part_range(nb, world, rank)
+        table = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nb, lo, hi)
+        slack = 1.05
+        table.reserve(int(nR * slack) + 4096)
+        sendR = torch.empty((nR, 2), dtype=torch.int32, device=dev)
+        sendS = torch.empty((nS, 2), dtype=torch.int32, device=dev)
+        cntR = torch.zeros(world, dtype=torch.int64, device=dev)
+        cntS = torch.zeros(world, dtype=torch.int64, device=dev)
+        recvR = torch.empty((int(nR * slack) + 4096, 2), dtype=torch.int32, device=dev)
+        recvS = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev)
+        out = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev) if emit else None
+    torch.cuda.synchronize()
+
+    state = {}
+
+    def step(ev):
+        ev[0].record()
+        if world == 1:
+            table.build(relR)
+            ev[1].record()
+            ctx.probe(table, relS, unique=True, out=out, fetch=False)
+        else:
+            ctx.partition(relR, nb, world, sendR, cntR)
+            rR = hdist.exchange(sendR, cntR, recvR)
+            table.build(hj3d.Rel(rR, key_word=0, row_word=1))
+            ev[1].record()
+            ctx.partition(relS, nb, world, sendS, cntS)
+            rS = hdist.exchange(sendS, cntS, recvS)
+            state["probe_n"] = rS.shape[0]
+            ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True, out=out, fetch=False)
+        ev[2].record()
+
+    def events():
+        return [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+
+    for _ in range(args.warmup):
+        step(events())
+    torch.cuda.synchronize()
+    barrier()
+    ctx.timer_reset()
+    evs = [events() for _ in range(args.steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        step(e)
+    torch.cuda.synchronize()
+    barrier()
+    wall = time.perf_counter() - t0
+
+    build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    kern_ms, kern_n = ctx.timer(hj3d.T_PROBE_KERNEL)
+    kern_avg = kern_ms / max(kern_n, 1)
+    res = ctx.probe_result()
+    wall_ms = wall * 1e3 / args.steps
+    probe_n_local = state.get("probe_n", nS)
+
+    # ---- verification of the last step (bit-exact, size-independent) ----
+    expd = torch.zeros(8, dtype=torch.int64, device=dev)
+    ctx.expected_fk_join_gen(relS, nR_tot, SEED_R, swap=False, res=expd)
+    torch.cuda.synchronize()
+    exp_local = [int(x) & hj3d.MASK64 for x in expd.cpu().tolist()[:5]]
+    got_local = [res.n_out, res.sum_a, res.sum_b, res.sum_h]
+    if world > 1:
+        exp_sum = hdist.allreduce_sum_u64(exp_local[:4], dev)
+        exp_xor = hdist.allreduce_xor_u64(exp_local[4], dev)
+        got_sum = hdist.allreduce_sum_u64(got_local, dev)
+        got_xor = hdist.allreduce_xor_u64(res.xor_h, dev)
+        cmps = hdist.allreduce_sum_u64([res.n_cmps], dev)[0]
+        build_ms = hdist.allreduce_max(build_ms, dev)
+        probe_ms = hdist.allreduce_max(probe_ms, dev)
+        wall_ms = hdist.allreduce_max(wall_ms, dev)
+        kern_avg = hdist.allreduce_max(kern_avg, dev)
+    else:
+        exp_sum, exp_xor = exp_local[:4], exp_local[4]
+        got_sum, got_xor = got_local, res.xor_h
+        cmps = res.n_cmps
+    verified = exp_sum == got_sum and exp_xor == got_xor and got_sum[0] == nS * world
+
+    if rank != 0:
+        if world > 1:
+            torch.distributed.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel (the probe kernel) ----
+    # algorithmic bytes per launch: probe tuple read + one 8-B table entry + 8-B output pair
+    tuple_bytes = 12 if world == 1 else 8
+    bytes_per_probe = tuple_bytes + 8 + (8 if emit else 0)
+    alg_bytes = probe_n_local * bytes_per_probe
+    achieved = alg_bytes / (kern_avg * 1e-3) / 1e9
+    traffic = None
+    if world == 1 and os.path.exists(args.pmc_json):
+        try:
+            with open(args.pmc_json) as f:
+                pm = json.load(f)
+            if pm.get("nS") == nS and pm.get("emit") == emit:
+                traffic = pm.get("traffic_bytes_per_launch")
+        except (OSError, ValueError):
+            traffic = None
+
+    line = {
+        "metric": METRIC,
+        "value": nS * world / (probe_ms * 1e-3),
+        "unit": "probe tuples/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall_ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (device-generated: R.k = seeded permutation of [0,|R|), S.a ~ U[0,|R|))",
+        "config": {
+            "workload": f"exp1 key/FK plan Csr, |R|={nR} |S|={nS} per GPU, uniform FKs, b={args.b}",
+            "plan": "Csr", "R_per_gpu": nR, "S_per_gpu": nS, "num_buckets": nb,
+            "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if world > 1 else "single GPU",
+        },
+        "build_ms": build_ms,
+        "probe_ms": probe_ms,
+        "join_tuples_per_s": nS * world / ((build_ms + probe_ms) * 1e-3),
+        "roofline": {
+            "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+            "kernel": "k_chain_probe", "kernel_avg_ms": kern_avg, "alg_bytes_per_launch": alg_bytes,
+        },
+        "counters": {"c_top": got_sum[0], "c_htProbeCmp": cmps},
+        "verified_bit_exact": verified,
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        m = min(args.cpu_sample, nS)
+        R_host = R.cpu().numpy().view("uint32")
+        S_host = S[:m].cpu().numpy().view("uint32")
+        line["cpu_baseline"] = cpu_baseline(R_host, S_host, nb, args.cpu_reps)
+    else:
+        line["cpu_baseline"] = None
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(s + "\n")
+    if world > 1:
+        torch.distributed.destroy_process_group()
+    if not verified:
+        raise SystemExit("verification failed: join output differs from the expected key/FK pair set")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,196 @@
+/* hj3d.h — C ABI of the MI355X-native 3D hash-join engine (libhj3d.so).
+ *
+ * The reference (dflaxx/3d-hashjoin) has no FFI: its boundary is the compile-time
+ * template surface of algebra.hh / ht_chaining.hh / ht_nested.hh. This ABI is what
+ * that surface binds to. Each entry point replaces one reference interface:
+ *
+ *   hj3d_build  (HJ3D_CHAIN)   HtChaining1::insert            ht_chaining.hh:181-196
+ *                              driven by AlgScan -> AlgHashJoinBuild::step  algebra.hh:259-269, 574-577
+ *   hj3d_build  (HJ3D_NESTED)  HtNested1::insert              ht_nested.hh:287-311, 386-436
+ *                              driven by AlgNestJoinBuild::step            algebra.hh:386-389
+ *   hj3d_probe  (chain table)  AlgHashJoinProbe::step         algebra.hh:625-659
+ *                              (+ HtChaining1::findDirEntryByOther ht_chaining.hh:236-248)
+ *   hj3d_probe  (nested table) AlgNestJoinProbe::step         algebra.hh:435-459
+ *                              (+ HtNested1::findMainNodeByOther ht_nested.hh:354-382)
+ *                              and with HJ3D_PROBE_UNNEST also AlgUnnestHt::step  algebra.hh:510-541
+ *   hj3d_probe2                the experiment-4 probe strand: two probes keyed on the same
+ *                              probe attribute + deferred unnesting   main_experiment4.cc:831-1043
+ *   hj3d_table_stats           HtChaining1/HtNested1::makeStatistics  ht_chaining.hh:260-292,
+ *                                                                     ht_nested.hh:450-482
+ *   hj3d_table_clear           HtChaining1/HtNested1::clear           ht_chaining.hh:250-258,
+ *                                                                     ht_nested.hh:438-447
+ *
+ * Semantics kept bit-exact with the reference: hash = murmur3 fmix32 (util/hasht.hh:52-61),
+ * bucket = hash % num_buckets, and every counter the reference reports (match counts,
+ * collision-chain comparisons c_htProbeCmp, unnest counts, HT statistics). The physical
+ * layout is NOT the reference's pointer chains: tables are CSR-bucketized arrays, and the
+ * reference's chain order (chaining: directory entry first, then newest-first; nested:
+ * main nodes in first-occurrence order) is reproduced arithmetically from row ids.
+ *
+ * Conventions: all relation/pair pointers are DEVICE pointers; every call is enqueued on the
+ * context's stream (asynchronous) unless documented as synchronous. Calls return hj3d_status;
+ * nothing throws. One host thread per context.
+ */
+#ifndef HJ3D_H
+#define HJ3D_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  HJ3D_OK = 0,
+  HJ3D_EINVAL = 1,       /* bad argument (null pointer, misaligned stride, ...)          */
+  HJ3D_ENOMEM = 2,       /* device allocation failed                                      */
+  HJ3D_EDEVICE = 3,      /* a HIP runtime call failed (see hj3d_last_error)               */
+  HJ3D_EUNSUPPORTED = 4, /* a request outside what the engine implements                 */
+  HJ3D_EOVERFLOW = 5     /* output buffer too small (counters are still complete)         */
+} hj3d_status;
+
+typedef struct hj3d_ctx hj3d_ctx;     /* device, stream, scratch arena, event timers        */
+typedef struct hj3d_table hj3d_table; /* a device-resident hash table (chaining or nested)  */
+
+#define HJ3D_ROW_IMPLICIT 0xFFFFFFFFu
+
+/* A relation in device memory: array of structs. The join attribute is the u32 at
+ * key_off of every tuple (main_experiment1.cc:86 tuple {k,a,b} -> stride 12, key_off 0 for
+ * R.k, 4 for S.a). Row id of tuple i: row_base + i, or the u32 at row_off when
+ * row_off != HJ3D_ROW_IMPLICIT (exchanged (key,row) pairs on multi-GPU). Row ids are the
+ * identity of tuples: they are what the reference's tuple pointers become. */
+typedef struct {
+  const void* base;
+  uint64_t n;
+  uint32_t stride;  /* bytes between consecutive tuples, multiple of 4, > 0 */
+  uint32_t key_off; /* byte offset of the u32 join attribute, multiple of 4  */
+  uint32_t row_off; /* byte offset of a u32 row id, or HJ3D_ROW_IMPLICIT     */
+  uint32_t reserved;
+  uint64_t row_base;
+} hj3d_rel;
+
+enum { HJ3D_CHAIN = 0, HJ3D_NESTED = 1 };
+
+typedef struct {
+  uint64_t num_buckets; /* global NB: bucket(key) = murmur32(key) % NB, 1 <= NB < 2^32     */
+  uint64_t bucket_lo;   /* this table holds buckets [bucket_lo, bucket_hi) (a multi-GPU    */
+  uint64_t bucket_hi;   /* shard); 0 / num_buckets on one GPU. Keys of other buckets are  */
+                        /* ignored by build and never match in probe.                      */
+  uint32_t kind;        /* HJ3D_CHAIN or HJ3D_NESTED                                        */
+  uint32_t reserved;
+} hj3d_table_desc;
+
+/* probe flags */
+#define HJ3D_PROBE_UNIQUE 0x1u /* IsBuildKeyUnique: stop at the first match (algebra.hh:653-655) */
+#define HJ3D_PROBE_UNNEST 0x2u /* nested table: expand main + sub-chain (AlgUnnestHt)           */
+#define HJ3D_PROBE_EMIT   0x4u /* write output tuples to out_dev (else aggregate only)          */
+
+/* Result of one probe strand. Orientation follows the reference's concat functors:
+ * a = probe-side row, b = build-side row (for a nested probe without unnest, b = the row of
+ * the matched key's first build tuple, i.e. MainNode::data()). */
+typedef struct {
+  uint64_t n_probe;   /* probe tuples scanned                    (c_scanProbe)             */
+  uint64_t n_matched; /* probe tuples with >= 1 match            (nested c_htProbe)         */
+  uint64_t n_out;     /* output tuples: chaining c_htProbe, nested c_unnest / c_top         */
+  uint64_t n_cmps;    /* collision-chain comparisons             (c_htProbeCmp, bit-exact)  */
+  uint64_t sum_a, sum_b, sum_c; /* sum of row ids over output tuples (c only for triples)   */
+  uint64_t sum_h, xor_h;        /* sum / xor of HJ3D pair (triple) hashes over output tuples */
+} hj3d_probe_res;
+
+/* Result of the experiment-4 probe strand (main_experiment4.cc:831-1043 counter columns).
+ * Output triples (r, s, t) rows; a = r, b = s, c = t in the checksums. */
+typedef struct {
+  uint64_t c_probe_rs, c_probe_rs_cmp, c_probe_rt, c_probe_rt_cmp;
+  uint64_t c_unnest_1, c_unnest_2, c_top;
+  uint64_t sum_a, sum_b, sum_c, sum_h, xor_h;
+} hj3d_probe2_res;
+
+/* HtStatistics (ht_statistics.hh:18-54): cc0 over all buckets, cc1 over non-empty ones.
+ * Chain length = #entries (chaining) or #main nodes = distinct keys (nested) per bucket. */
+typedef struct {
+  uint64_t nb, empty, entries, distinct;
+  uint64_t cc0_min, cc0_max, cc0_sum, cc0_cnt;
+  uint64_t cc1_min, cc1_max, cc1_sum, cc1_cnt;
+} hj3d_stats;
+
+/* ---- checksums (definitions shared with oracle/ and tests) ----
+ * mix64 = splitmix64 finalizer; pair(a,b) = mix64(a<<32 | b); triple(a,b,c) = mix64(pair(a,b) ^ c) */
+uint64_t hj3d_mix64(uint64_t z);
+
+/* ---- context ---- */
+hj3d_status hj3d_ctx_create(int device, void* hip_stream /* NULL: a new non-blocking stream */, hj3d_ctx** out);
+void        hj3d_ctx_destroy(hj3d_ctx* ctx);
+hj3d_status hj3d_ctx_set_stream(hj3d_ctx* ctx, void* hip_stream);
+void*       hj3d_ctx_stream(const hj3d_ctx* ctx);
+hj3d_status hj3d_ctx_sync(hj3d_ctx* ctx); /* synchronous: waits for the stream */
+const char* hj3d_last_error(const hj3d_ctx* ctx);
+/* Kernel-phase timers: HIP events recorded on the context stream around every phase
+ * (phase ids below). hj3d_ctx_timer reads (synchronously) the summed milliseconds and the
+ * number of recorded intervals since the last reset. */
+enum { HJ3D_T_BUILD = 0, HJ3D_T_PROBE = 1, HJ3D_T_PROBE_KERNEL = 2, HJ3D_T_PARTITION = 3, HJ3D_T_NTIMERS = 4 };
+hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
+hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count);
+hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx);
+
+/* ---- tables ---- */
+hj3d_status hj3d_table_create(hj3d_ctx* ctx, const hj3d_table_desc* desc, hj3d_table** out);
+void        hj3d_table_destroy(hj3d_table* t);
+/* Pre-size device storage for builds of up to max_build tuples (allocation outside timed loops). */
+hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build);
+hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t);
+/* Build: replaces the table content with the tuples of `build` (asynchronous). */
+hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
+/* Synchronous statistics (makeStatistics). */
+hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out);
+/* Number of tuples / distinct keys currently stored (synchronous). */
+hj3d_status hj3d_table_size(hj3d_ctx* ctx, const hj3d_table* t, uint64_t* n_entries, uint64_t* n_distinct);
+
+/* ---- probe ----
+ * Asynchronous: counters accumulate in a device-side result slot; hj3d_probe_result reads it
+ * (synchronous). With HJ3D_PROBE_EMIT, output pairs {u32 a, u32 b} are written to out_dev
+ * (at most out_cap pairs; n_out still counts all and HJ3D_EOVERFLOW is reported by
+ * hj3d_probe_result if n_out > out_cap). Pair order in out_dev is unspecified. */
+hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe, uint32_t flags,
+                       void* out_dev, uint64_t out_cap);
+hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out);
+
+/* Experiment-4 probe strand over two tables built on S and T (both HJ3D_NESTED: Ndu with deferred
+ * unnesting; both HJ3D_CHAIN: Chj). With HJ3D_PROBE_EMIT, triples {u32 r, s, t} go to out_dev. */
+hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel* probe,
+                        uint32_t flags, void* out_dev, uint64_t out_cap);
+hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out);
+
+/* ---- multi-GPU exchange helpers (bucket-range radix partition) ----
+ * Destination of a tuple: owner(bucket) = bucket * nparts / num_buckets. Writes (key,row)
+ * pairs grouped by destination into out_pairs_dev (capacity rel->n pairs) and the per
+ * destination counts into counts_dev[nparts] (device u64). Order within a destination
+ * follows input order (stable). */
+hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t num_buckets, uint32_t nparts,
+                           void* out_pairs_dev, void* counts_dev);
+/* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
+void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
+
+/* ---- synthetic key/FK relations generated on the device (bench / full-size checks) ----
+ * R.k = a seeded bijective permutation of [0, n_keys) (keys for global rows
+ * [row_base, row_base+n)), written into tuple word key_off of an AoS buffer;
+ * S.a = uniform in [0, fk_max) from a counter-based RNG of the global row id. */
+hj3d_status hj3d_gen_keys(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t stride, uint32_t key_off,
+                          uint64_t row_base, uint64_t n_keys, uint64_t seed);
+hj3d_status hj3d_gen_fk(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t stride, uint32_t key_off,
+                        uint64_t row_base, uint32_t fk_max, uint64_t seed);
+/* Expected key/FK join aggregates WITHOUT a hash table (full-size verification of the
+ * key/FK plans): `build` holds unique keys in [0, n_keys); every probe tuple's partner row is
+ * inv[key], inv being the inverse of the build key column. Accumulates {n_out, sum_a, sum_b,
+ * sum_h, xor_h} (u64 each) into res_dev (zero it first). Orientation: a = probe row,
+ * b = build row; with swap != 0, a = build row, b = probe row (plans that build on the FK side). */
+hj3d_status hj3d_expected_fk_join(hj3d_ctx* ctx, const hj3d_rel* build, const hj3d_rel* probe, uint64_t n_keys,
+                                  int swap, void* res_dev);
+/* The same expectation when the build keys were made by hj3d_gen_keys(n_keys, key_seed): the
+ * partner row of key k is the inverse permutation of k (per-rank verification on multi-GPU). */
+hj3d_status hj3d_expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel* probe, uint64_t n_keys, uint64_t key_seed,
+                                      int swap, void* res_dev);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* HJ3D_H */

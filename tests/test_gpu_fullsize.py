@@ -1,0 +1,93 @@
+"""Full-size (BASELINE config B: |R| = 1e7, |S| = 1e8) parity through size-independent
+properties, on relations generated on the device (hj3d_gen_keys / hj3d_gen_fk).
+
+For a key/FK join every S tuple has exactly one partner, the R row whose key equals S.a.
+hj3d_expected_fk_join computes that pair set WITHOUT a hash table (inverse permutation of
+R.k), so the join's cardinality and its order-independent pair checksums are checked
+bit-exactly at full size. Comparison counts are checked against the oracle at 1e6 / 1e7
+on the same generator."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+SEED_R, SEED_S = 0x5eed0001, 0x5eed0002
+
+
+def make_rel(ctx, nR, nS, fk_max=None):
+    import torch
+    R = torch.zeros((nR, 3), dtype=torch.int32, device="cuda")
+    S = torch.zeros((nS, 3), dtype=torch.int32, device="cuda")
+    ctx.gen_keys(R, 0, 0, nR, SEED_R)          # R.k = permutation of [0, |R|)
+    ctx.gen_keys(S, 0, 0, 0, 0)                # S.k = row id
+    ctx.gen_fk(S, 1, 0, fk_max or nR, SEED_S)  # S.a ~ U[0, |R|)
+    return R, S
+
+
+def test_config_b_csr_full_size(ctx):
+    import torch
+    import hj3d
+    nR, nS = 10_000_000, 100_000_000
+    R, S = make_rel(ctx, nR, nS)
+    exp = ctx.expected_fk_join(hj3d.Rel(R, 0), hj3d.Rel(S, 1), nR)
+    assert exp["n"] == nS
+    out = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    got = hj3d.exp1_plan(ctx, "Csr", R, S, nR, out=out)
+    assert got["c_top"] == nS and got["c_probe"] == nS
+    assert {k: got["out"][k] for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h")} == exp
+    assert got["stats"]["entries"] == nR and got["stats"]["distinct"] == nR
+    assert got["stats"]["cc0_sum"] == nR
+    # the materialised pairs: slot i holds (i, partner of S[i])
+    head = out[:1000].cpu().numpy().view(np.uint32)
+    assert (head[:, 0] == np.arange(1000)).all()
+    Rk = R[:, 0].cpu().numpy().view(np.uint32)
+    inv = np.empty(nR, np.uint32)
+    inv[Rk] = np.arange(nR, dtype=np.uint32)
+    Sa = S[:1000, 1].cpu().numpy().view(np.uint32)
+    assert (head[:, 1] == inv[Sa]).all()
+    # aggregate-only probe gives identical counters
+    agg = hj3d.exp1_plan(ctx, "Csr", R, S, nR, stats=False)
+    assert agg["out"] == got["out"] and agg["c_cmp"] == got["c_cmp"]
+
+
+def test_config_b_nested_full_size(ctx):
+    """Nrs (3D table on the non-unique S.a, 1e8 inserts) and Nsr at full size."""
+    import hj3d
+    nR, nS = 10_000_000, 100_000_000
+    R, S = make_rel(ctx, nR, nS)
+    exp_sr = ctx.expected_fk_join(hj3d.Rel(R, 0), hj3d.Rel(S, 1), nR)
+    exp_rs = ctx.expected_fk_join(hj3d.Rel(R, 0), hj3d.Rel(S, 1), nR, swap=True)
+    got = hj3d.exp1_plan(ctx, "Nsr", R, S, nR, stats=False)
+    assert got["c_top"] == nS
+    assert {k: got["out"][k] for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h")} == exp_sr
+    # #dv(S.a) from the nested table itself (one main record per distinct key)
+    t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nR)
+    t.build(hj3d.Rel(S, 1))
+    dv = t.stats()["distinct"]
+    assert 0.99 * nR * (1 - np.exp(-10)) < dv <= nR
+    got = hj3d.exp1_plan(ctx, "Nrs", R, S, dv)
+    assert got["c_unnest"] == nS and got["c_probe"] == dv
+    assert {k: got["out"][k] for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h")} == exp_rs
+    assert got["stats"]["entries"] == nS and got["stats"]["distinct"] == dv
+
+
+@pytest.mark.parametrize("nR,nS", [(1_000_000, 10_000_000)])
+def test_device_generator_cmps_vs_oracle(ctx, nR, nS):
+    """Config A sizes (1e6 / 1e7) on the device generator: the C oracle (reference semantics)
+    reproduces every counter of the GPU plans, comparison counts included."""
+    import hj3d
+    R, S = make_rel(ctx, nR, nS)
+    Rh = R.cpu().numpy().view(np.uint32)
+    Sh = S.cpu().numpy().view(np.uint32)
+    dv = O.num_distinct(Sh[:, 1])
+    for plan, fn in (("Csr", lambda: O.chain_plan(Rh, 0, Sh, 1, nR, True)),
+                     ("Crs", lambda: O.chain_plan(Sh, 1, Rh, 0, dv, False)),
+                     ("Nrs", lambda: O.nested_plan(Sh, 1, Rh, 0, dv, True))):
+        e = fn()
+        nb = nR if plan == "Csr" else dv
+        got = hj3d.exp1_plan(ctx, plan, R, S, nb)
+        assert (got["c_probe"], got["c_cmp"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_top), plan
+        assert got["out"] == e.out, plan
+        assert got["stats"]["cc0_max"] == e.stats["cc0_max"] and got["stats"]["empty"] == e.stats["empty"]

@@ -1,0 +1,208 @@
+"""GPU parity: libhj3d.so on the MI355X against the reference's golden fixtures and the oracle.
+
+Inputs are produced by the oracle's bit-exact generator restatement (itself pinned to the
+reference by test_oracle_golden.py) and uploaded; every counter the reference reports
+(c_htProbe, c_htProbeCmp, c_unnest, c_top), every HtStatistics field and the order-independent
+output checksums must match EXACTLY (integer work: bit-exact bar).
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+EXP1 = load_golden("exp1_*.json")
+EXP4 = load_golden("exp4_*.json")
+STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
+             "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
+PLANS = ("Csr", "CsrUU", "Crs", "Nsr", "Nrs", "NrsNU")
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).cuda()
+
+
+def exp1_rel(g):
+    _, nR, nS, skew, theta, t, b = g["generator_args"][:7]
+    Rk, Sa, _ = O.gen_exp1(nR, nS, bool(skew), theta, t)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    return R, S, b
+
+
+def host_checksums(pairs: np.ndarray) -> dict:
+    """Order-independent checksums of emitted (a, b) pairs, computed on the host."""
+    a = pairs[:, 0].astype(np.uint64)
+    b = pairs[:, 1].astype(np.uint64)
+    z = (a << np.uint64(32)) | b
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xbf58476d1ce4e5b9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94d049bb133111eb)
+    z = z ^ (z >> np.uint64(31))
+    with np.errstate(over="ignore"):
+        return {"n": len(pairs), "sum_a": int(a.sum(dtype=np.uint64)), "sum_b": int(b.sum(dtype=np.uint64)),
+                "sum_c": 0, "sum_h": int(z.sum(dtype=np.uint64)), "xor_h": int(np.bitwise_xor.reduce(z)) if len(z) else 0}
+
+
+@pytest.mark.parametrize("name,g", EXP1, ids=[n for n, _ in EXP1])
+def test_exp1_plans_bit_exact(ctx, name, g):
+    import hj3d
+    R, S, b = exp1_rel(g)
+    dR, dS = dev(R), dev(S)
+    for plan in PLANS:
+        nb = hj3d.num_buckets_exp1(plan, len(R), g["numDvSa"], b)
+        ref = g["plans"][plan]
+        got = hj3d.exp1_plan(ctx, plan, dR, dS, nb)
+        assert got["nb"] == ref["nb"], plan
+        for k in ("c_probe", "c_cmp", "c_top"):
+            assert got[k] == ref[k], (plan, k, got[k], ref[k])
+        assert got["c_unnest"] == ref.get("c_unnest", 0), plan
+        assert {k: got["stats"][k] for k in STAT_KEYS} == {k: ref["stats"][k] for k in STAT_KEYS}, plan
+        assert got["out"] == ref["out"], plan
+
+
+@pytest.mark.parametrize("name,g", [x for x in EXP1 if x[1]["nS"] <= 1_100_000], ids=lambda v: v if isinstance(v, str) else "")
+def test_exp1_materialised_output(ctx, name, g):
+    """HJ3D_PROBE_EMIT: the pairs written to HBM are exactly the reference's output tuples."""
+    import torch
+    import hj3d
+    R, S, b = exp1_rel(g)
+    dR, dS = dev(R), dev(S)
+    for plan in PLANS:
+        nb = hj3d.num_buckets_exp1(plan, len(R), g["numDvSa"], b)
+        ref = g["plans"][plan]
+        cap = max(ref["out"]["n"], len(S), len(R), 1)
+        out = torch.zeros((cap, 2), dtype=torch.int32, device="cuda")
+        got = hj3d.exp1_plan(ctx, plan, dR, dS, nb, out=out, stats=False)
+        assert not got["overflow"]
+        host = out.cpu().numpy().view(np.uint32)
+        kind, _, _, _, unique, unnest = hj3d.EXP1_PLANS[plan]
+        dense = (kind == hj3d.HJ3D_CHAIN and unique) or (kind == hj3d.HJ3D_NESTED and not unnest)
+        if dense:  # one slot per probe tuple, unmatched slots carry 0xFFFFFFFF
+            nprobe = len(S) if hj3d.EXP1_PLANS[plan][1] == "R" else len(R)
+            host = host[:nprobe]
+            assert (host[:, 0] == np.arange(nprobe, dtype=np.uint32)).all()
+            host = host[host[:, 1] != 0xFFFFFFFF]
+        else:
+            host = host[: ref["out"]["n"]]
+        assert host_checksums(host) == ref["out"], plan
+        assert got["out"]["n"] == ref["out"]["n"]
+
+
+@pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
+def test_exp4_plans_bit_exact(ctx, name, g):
+    import hj3d
+    log2R, a, A, b, B = g["generator_args"][1:6]
+    Sa, Ta = O.gen_exp4(log2R, a, A, b, B)
+    n, cardR = len(Sa), 1 << log2R
+    R = dev(O.tuples2(np.arange(cardR, dtype=np.uint32), np.zeros(cardR, np.uint32)))
+    S = dev(O.tuples2(np.arange(n, dtype=np.uint32), Sa))
+    T = dev(O.tuples2(np.arange(n, dtype=np.uint32), Ta))
+    for plan in ("Ndu", "Chj"):
+        got = hj3d.exp4_plan(ctx, plan, R, S, T, g["nb"])
+        ref = g["plans"][plan]
+        for k in ("c_probe_RS", "c_probe_RS_cmp", "c_probe_RT", "c_probe_RT_cmp", "c_top"):
+            assert got[k.lower()] == ref[k], (plan, k, got[k.lower()], ref[k])
+        if plan == "Ndu":
+            assert got["c_unnest_1"] == ref["c_unnest_1"] and got["c_unnest_2"] == ref["c_unnest_2"]
+        assert {k: got[k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")} == \
+               {k: ref["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")}, plan
+
+
+def _oracle_plans(R, S, nbR, nbS):
+    return {
+        "Csr": O.chain_plan(R, 0, S, 1, nbR, True), "CsrUU": O.chain_plan(R, 0, S, 1, nbR, False),
+        "Crs": O.chain_plan(S, 1, R, 0, nbS, False), "Nsr": O.nested_plan(R, 0, S, 1, nbR, True),
+        "Nrs": O.nested_plan(S, 1, R, 0, nbS, True), "NrsNU": O.nested_plan(S, 1, R, 0, nbS, False),
+    }
+
+
+def _compare(ctx, R, S, nbR, nbS):
+    import hj3d
+    exp = _oracle_plans(R, S, nbR, nbS)
+    dR, dS = dev(R), dev(S)
+    for plan in PLANS:
+        e = exp[plan]
+        nb = nbR if hj3d.EXP1_PLANS[plan][1] == "R" else nbS
+        got = hj3d.exp1_plan(ctx, plan, dR, dS, nb)
+        assert (got["c_probe"], got["c_cmp"], got["c_top"], got["c_unnest"]) == \
+               (e.c_probe, e.c_cmp, e.c_top, e.c_unnest), plan
+        assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, plan
+        assert got["out"] == e.out, plan
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_relations_vs_oracle(ctx, seed):
+    """Non-key build sides, dangling FKs, duplicate R keys, tiny and odd bucket counts."""
+    rng = np.random.default_rng(seed)
+    nR, nS = int(rng.integers(1, 5000)), int(rng.integers(1, 20000))
+    Rk = rng.integers(0, nR * 2, nR).astype(np.uint32)  # duplicates + keys without partners
+    Sa = rng.integers(0, nR * 2, nS).astype(np.uint32)
+    R = O.tuples3(Rk, np.zeros(nR, np.uint32))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    for nbR, nbS in ((max(nR // 3, 1), 7), (1, 1), (nR + 13, O.num_distinct(Sa))):
+        _compare(ctx, R, S, nbR, nbS)
+
+
+def test_empty_relations(ctx):
+    R = O.tuples3(np.array([5, 9], np.uint32), np.zeros(2, np.uint32))
+    S0 = O.tuples3(np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+    _compare(ctx, R, S0, 2, 1)   # empty probe side / empty build side
+    _compare(ctx, S0, R, 1, 2)
+
+
+def test_skewed_hot_key_heavy_unnest(ctx):
+    """One key owns most of S: the nested build groups ~200k duplicates and the unnest of the hot
+    key goes through the workgroup-wide (heavy) expansion path; counters must not change."""
+    rng = np.random.default_rng(7)
+    nR, nS = 1000, 300_000
+    Rk = rng.permutation(nR).astype(np.uint32)
+    Sa = rng.integers(0, nR, nS).astype(np.uint32)
+    Sa[rng.random(nS) < 0.7] = 17
+    R = O.tuples3(Rk, np.zeros(nR, np.uint32))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    _compare(ctx, R, S, nR, O.num_distinct(Sa))
+
+
+def test_bucket_shards_sum_to_single_table(ctx):
+    """Multi-GPU building block: tables that own disjoint bucket ranges, probed by the tuples of
+    their range (hj3d_partition), add up to the single-table reference counters exactly."""
+    import torch
+    import hj3d
+    g = dict(load_golden("exp1_R1024_S4096_zipf.json"))["exp1_R1024_S4096_zipf"]
+    R, S, b = exp1_rel(g)
+    dR, dS = dev(R), dev(S)
+    for plan in ("Csr", "Crs", "Nrs", "Nsr"):
+        kind, bside, bkey, pkey, unique, unnest = hj3d.EXP1_PLANS[plan]
+        nb = hj3d.num_buckets_exp1(plan, len(R), g["numDvSa"], b)
+        build = hj3d.Rel(dR if bside == "R" else dS, key_word=bkey)
+        probe = hj3d.Rel(dS if bside == "R" else dR, key_word=pkey)
+        parts = 3
+        bp = torch.zeros((build.n, 2), dtype=torch.int32, device="cuda")
+        pp = torch.zeros((probe.n, 2), dtype=torch.int32, device="cuda")
+        bc = torch.zeros(parts, dtype=torch.int64, device="cuda")
+        pc = torch.zeros(parts, dtype=torch.int64, device="cuda")
+        ctx.partition(build, nb, parts, bp, bc)
+        ctx.partition(probe, nb, parts, pp, pc)
+        bcs, pcs = [0] + np.cumsum(bc.cpu().numpy()).tolist(), [0] + np.cumsum(pc.cpu().numpy()).tolist()
+        tot = {"c_cmp": 0, "n_out": 0, "n_matched": 0, "sum_h": 0, "xor_h": 0, "empty": 0, "cc0_max": 0}
+        for p in range(parts):
+            lo, hi = hj3d.part_range(nb, parts, p)
+            t = hj3d.Table(ctx, kind, nb, lo, hi)
+            t.build(hj3d.Rel(bp[bcs[p]:bcs[p + 1]], key_word=0, row_word=1))
+            r = ctx.probe(t, hj3d.Rel(pp[pcs[p]:pcs[p + 1]], key_word=0, row_word=1), unique=unique, unnest=unnest)
+            st = t.stats()
+            tot["c_cmp"] += r.n_cmps
+            tot["n_out"] += r.n_out
+            tot["n_matched"] += r.n_matched
+            tot["sum_h"] = (tot["sum_h"] + r.sum_h) % (1 << 64)
+            tot["xor_h"] ^= r.xor_h
+            tot["empty"] += st["empty"]
+            tot["cc0_max"] = max(tot["cc0_max"], st["cc0_max"])
+        ref = g["plans"][plan]
+        assert tot["c_cmp"] == ref["c_cmp"], plan
+        assert tot["n_out"] == ref["out"]["n"], plan
+        assert (tot["sum_h"], tot["xor_h"]) == (ref["out"]["sum_h"], ref["out"]["xor_h"]), plan
+        assert tot["empty"] == ref["stats"]["empty"] and tot["cc0_max"] == ref["stats"]["cc0_max"], plan

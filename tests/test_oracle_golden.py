@@ -1,0 +1,105 @@
+"""The oracle (oracle/hj3d_oracle.c) against the golden fixtures made by the REAL reference.
+
+Pins: the bit-exact input generators (mt19937 + libstdc++ shuffle / uniform_int /
+generate_canonical + the reference's Zipf sampler and vec_permute), and every counter,
+statistic and output checksum of the six experiment-1 plans and the two experiment-4 plans.
+CPU only.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+from conftest import load_golden
+
+EXP1 = load_golden("exp1_*.json")
+EXP4 = load_golden("exp4_*.json")
+STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
+             "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
+
+
+def exp1_inputs(g):
+    _, nR, nS, skew, theta, t, b = g["generator_args"][:7]
+    Rk, Sa, fk = O.gen_exp1(nR, nS, bool(skew), theta, t)
+    return Rk, Sa, fk, b
+
+
+@pytest.mark.parametrize("name,g", EXP1, ids=[n for n, _ in EXP1])
+def test_exp1_generator_bit_exact(name, g):
+    Rk, Sa, fk, _ = exp1_inputs(g)
+    assert fk == g["fkMax"]
+    assert Rk[:16].tolist() == g["head_Rk"]
+    assert Sa[:16].tolist() == g["head_Sa"]
+    assert O.colsum(Rk) == g["colsum_Rk"]
+    assert O.colsum(Sa) == g["colsum_Sa"]
+    if "Rk" in g:
+        assert Rk.tolist() == g["Rk"] and Sa.tolist() == g["Sa"]
+    assert O.num_distinct(Sa) == g["numDvSa"]
+
+
+@pytest.mark.parametrize("name,g", EXP1, ids=[n for n, _ in EXP1])
+def test_exp1_plans_match_reference(name, g):
+    if g["nS"] > 2_000_000:
+        pytest.skip("large fixture covered by the GPU parity suite")
+    Rk, Sa, _, b = exp1_inputs(g)
+    nR, nS = len(Rk), len(Sa)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    nbR, nbS = max(nR // b, 1), max(g["numDvSa"] // b, 1)
+    runs = {
+        "Csr": O.chain_plan(R, 0, S, 1, nbR, True), "CsrUU": O.chain_plan(R, 0, S, 1, nbR, False),
+        "Crs": O.chain_plan(S, 1, R, 0, nbS, False), "Nsr": O.nested_plan(R, 0, S, 1, nbR, True),
+        "Nrs": O.nested_plan(S, 1, R, 0, nbS, True), "NrsNU": O.nested_plan(S, 1, R, 0, nbS, False),
+    }
+    for plan, r in runs.items():
+        ref = g["plans"][plan]
+        assert r.c_probe == ref["c_probe"], plan
+        assert r.c_cmp == ref["c_cmp"], plan
+        assert r.c_top == ref["c_top"], plan
+        assert r.c_unnest == ref.get("c_unnest", 0), plan
+        assert {k: r.stats[k] for k in STAT_KEYS} == {k: ref["stats"][k] for k in STAT_KEYS}, plan
+        assert r.out == ref["out"], plan
+
+
+@pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
+def test_exp4_generator_and_plans(name, g):
+    log2R, a, A, b, B = g["generator_args"][1:6]
+    Sa, Ta = O.gen_exp4(log2R, a, A, b, B)
+    assert O.colsum(Sa) == g["colsum_Sa"] and O.colsum(Ta) == g["colsum_Ta"]
+    if "Sa" in g:
+        assert Sa.tolist() == g["Sa"] and Ta.tolist() == g["Ta"]
+    n, cardR = len(Sa), 1 << log2R
+    R = O.tuples2(np.arange(cardR, dtype=np.uint32), np.zeros(cardR, np.uint32))
+    S = O.tuples2(np.arange(n, dtype=np.uint32), Sa)
+    T = O.tuples2(np.arange(n, dtype=np.uint32), Ta)
+    for plan, nested in (("Ndu", True), ("Chj", False)):
+        r = O.exp4_plan(R, S, T, g["nb"], nested)
+        ref = g["plans"][plan]
+        for k in ("c_probe_RS", "c_probe_RS_cmp", "c_probe_RT", "c_probe_RT_cmp", "c_top"):
+            assert r[k.lower()] == ref[k], (plan, k)
+        if nested:
+            assert r["c_unnest_1"] == ref["c_unnest_1"] and r["c_unnest_2"] == ref["c_unnest_2"]
+        assert r["out"] == ref["out"], plan
+    assert g["plans"]["Ndu"]["c_top"] == g["join_card2"]  # calcJoinCard2 (main_experiment4.cc:593-597)
+
+
+def test_survey_known_answers():
+    """the reference's own printed relations for -R 3 -S 4."""
+    Rk, Sa, _ = O.gen_exp1(8, 16, False)
+    assert Rk.tolist() == [2, 3, 0, 5, 4, 6, 7, 1]
+    assert Sa.tolist() == [7, 4, 1, 5, 2, 1, 2, 7, 7, 7, 7, 0, 4, 7, 1, 7]
+    _, Sz, _ = O.gen_exp1(8, 16, True, 1.0)
+    assert Sz.tolist() == [1, 0, 7, 0, 4, 7, 3, 0, 0, 0, 7, 7, 7, 0, 2, 0]
+    Sa4, Ta4 = O.gen_exp4(3, 2, 2, 2, 1)
+    assert Sa4.tolist() == [0, 0, 1, 1, 2, 3]
+    assert Ta4.tolist() == [0, 0, 1, 1, 5, 4]
+
+
+def test_empty_and_tiny_relations():
+    """Edge cases the reference cannot run (its vec_permute underflows on an empty FK vector):
+    the oracle treats empty inputs as empty joins."""
+    R = O.tuples3(np.array([3, 1, 2], np.uint32), np.zeros(3, np.uint32))
+    S = O.tuples3(np.zeros(0, np.uint32), np.zeros(0, np.uint32))
+    r = O.chain_plan(R, 0, S, 1, 3, True)
+    assert (r.c_probe, r.c_cmp, r.c_top) == (0, 0, 0)
+    r = O.nested_plan(S, 1, R, 0, 1, True)
+    assert (r.c_probe, r.c_cmp, r.c_top, r.stats["empty"]) == (0, 0, 0, 1)
