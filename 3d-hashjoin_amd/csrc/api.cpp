@@ -89,15 +89,8 @@ hj3d_status hj3d_ctx_create(int device, void* stream, hj3d_ctx** out) {
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     ctx->num_cus = prop.multiProcessorCount;
-  if (stream) {
-    ctx->stream = static_cast<hipStream_t>(stream);
-  } else {
-    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-      delete ctx;
-      return HJ3D_EDEVICE;
-    }
-    ctx->own_stream = true;
-  }
+  ctx->stream = static_cast<hipStream_t>(stream);  // NULL: the null stream
+  ctx->own_stream = false;
   if (ctx->res.ensure(kResFields * sizeof(uint64_t)) != hipSuccess) {
     delete ctx;
     return HJ3D_ENOMEM;
@@ -119,7 +112,7 @@ void hj3d_ctx_destroy(hj3d_ctx* ctx) {
 }
 
 hj3d_status hj3d_ctx_set_stream(hj3d_ctx* ctx, void* stream) {
-  if (!ctx || !stream) return HJ3D_EINVAL;
+  if (!ctx) return HJ3D_EINVAL;
   if (ctx->own_stream) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipStreamDestroy(ctx->stream);
@@ -137,6 +130,15 @@ hj3d_status hj3d_ctx_sync(hj3d_ctx* ctx) {
 }
 
 const char* hj3d_last_error(const hj3d_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+
+hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
+  if (!ctx) return HJ3D_EINVAL;
+  switch (option) {
+    case HJ3D_OPT_FORCE_DIRECT: ctx->force_direct = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_RADIX_MIN: ctx->radix_min = value < 0 ? 0 : uint64_t(value); return HJ3D_OK;
+    default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
+  }
+}
 
 hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable) {
   if (!ctx) return HJ3D_EINVAL;
@@ -232,8 +234,13 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   if (!rel_ok(build)) return fail(ctx, HJ3D_EINVAL, "hj3d_build: invalid relation");
   if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
-  const hipError_t e = t->desc.kind == HJ3D_CHAIN ? chain_build(ctx, t, *build, ctx->stream)
-                                                  : nested_build(ctx, t, *build, ctx->stream);
+  hipError_t e;
+  if (t->desc.kind == HJ3D_CHAIN)
+    e = (!ctx->force_direct && build->n >= (ctx->radix_min >> 4) && build->n > 0 && t->nb_local >= 64)
+            ? radix_build(ctx, t, *build, ctx->stream)
+            : chain_build(ctx, t, *build, ctx->stream);
+  else
+    e = nested_build(ctx, t, *build, ctx->stream);
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");
 }
@@ -266,8 +273,12 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
-    e = t->desc.kind == HJ3D_CHAIN ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
-                                   : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    if (t->desc.kind == HJ3D_CHAIN)
+      e = radix_probe_applicable(ctx, t, probe->n)
+              ? radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
+              : chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    else
+      e = nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
   }
   // remember what an overflow check needs
   ctx->res_flags = flags;

@@ -97,11 +97,17 @@ __global__ __launch_bounds__(kBlock) void k_chain_scatter(RelView r, FastMod fm,
 
 enum ProbeMode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
 
+constexpr int kRegEnt = 4;  // bucket entries held in registers per probe item (covers ~98% of
+                            // probes at #buckets = |R|; longer buckets take the loop below)
+
 // One probe strand over a chaining table.
 //   kAgg   : counters + output checksums only (what the reference's AlgTop observes)
 //   kDense : kAgg + out[i] = {probe row, build row | 0xFFFFFFFF} per probe tuple (UNIQUE only)
 //   kCount : kAgg + cnt[i] = #output pairs of probe tuple i (u64)
 //   kWrite : out[ooff[i] + k] = k-th output pair of probe tuple i (after a scan of kCount)
+// Memory-level parallelism: every item's key, bucket range and first kRegEnt entries are issued
+// as independent loads (three dependent rounds per kProbeItems tuples), then evaluated from
+// registers.
 template <bool UNIQUE, int MODE>
 __global__ __launch_bounds__(kBlock) void k_chain_probe(RelView r, FastMod fm, uint32_t lo, uint32_t nbl,
                                                         const uint32_t* __restrict__ off,
@@ -111,9 +117,9 @@ __global__ __launch_bounds__(kBlock) void k_chain_probe(RelView r, FastMod fm, u
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t stride = uint64_t(gridDim.x) * kBlock * kProbeItems;
   for (uint64_t base = uint64_t(blockIdx.x) * kBlock * kProbeItems; base < r.n; base += stride) {
-    uint32_t h[kProbeItems], b[kProbeItems], pr[kProbeItems];
-    uint32_t s[kProbeItems], e[kProbeItems];
-    // phase 1: stream the probe keys (independent loads, all in flight together)
+    uint32_t h[kProbeItems], b[kProbeItems], pr[kProbeItems], s[kProbeItems], n[kProbeItems];
+    uint2 E[kProbeItems][kRegEnt];
+    // round 1: stream the probe keys (non-temporal: S is read once)
 #pragma unroll
     for (int j = 0; j < kProbeItems; ++j) {
       const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
@@ -122,46 +128,68 @@ __global__ __launch_bounds__(kBlock) void k_chain_probe(RelView r, FastMod fm, u
       pr[j] = v ? r.row(i) : 0u;
       b[j] = v ? fm.mod(h[j]) - lo : kInvalid;
     }
-    // phase 2: bucket ranges (random, Infinity-Cache resident directory)
+    // round 2: bucket ranges (random; the directory is Infinity-Cache resident)
 #pragma unroll
     for (int j = 0; j < kProbeItems; ++j) {
       s[j] = 0;
-      e[j] = 0;
+      n[j] = 0;
       if (b[j] < nbl) {
         s[j] = off[b[j]];
-        e[j] = off[b[j] + 1];
+        n[j] = off[b[j] + 1] - s[j];
       }
     }
-    // phase 3: bucket entries
+    // round 3: the first kRegEnt entries of every bucket, all in flight together
+#pragma unroll
+    for (int k = 0; k < kRegEnt; ++k) {
+#pragma unroll
+      for (int j = 0; j < kProbeItems; ++j) {
+        E[j][k] = make_uint2(~h[j], kInvalid);  // never matches
+        if (uint32_t(k) < n[j]) E[j][k] = ent[s[j] + k];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < kProbeItems; ++j) {
       const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
       if (i >= r.n) continue;
       if (MODE != kWrite) acc[0] += 1;  // n_probe
-      const uint32_t n = e[j] - s[j];
+      const uint32_t nj = n[j];
       uint32_t nout = 0;
       if (UNIQUE) {
+        // the reference walks [first insert, newest, ..., second]: the first match it meets is
+        // the minimum-row entry if that matches, else the largest matching row
         uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
-        for (uint32_t k = s[j]; k < e[j]; ++k) {
-          const uint2 E = ent[k];
-          minrow = min(minrow, E.y);
-          if (E.x == h[j]) {
+#pragma unroll
+        for (int k = 0; k < kRegEnt; ++k) {
+          if (uint32_t(k) < nj) {
+            minrow = min(minrow, E[j][k].y);
+            if (E[j][k].x == h[j]) {
+              ++nm;
+              lo_m = min(lo_m, E[j][k].y);
+              hi_m = max(hi_m, E[j][k].y);
+            }
+          }
+        }
+        for (uint32_t k = kRegEnt; k < nj; ++k) {  // long buckets
+          const uint2 e2 = ent[s[j] + k];
+          minrow = min(minrow, e2.y);
+          if (e2.x == h[j]) {
             ++nm;
-            lo_m = min(lo_m, E.y);
-            hi_m = max(hi_m, E.y);
+            lo_m = min(lo_m, e2.y);
+            hi_m = max(hi_m, e2.y);
           }
         }
         uint32_t match = kInvalid;
-        if (n != 0) {
+        if (nj != 0) {
           if (nm == 0) {
-            acc[3] += n;  // no match: the whole chain is compared
+            acc[3] += nj;  // no match: the whole chain is compared
           } else if (lo_m == minrow) {
             acc[3] += 1;  // the directory entry (first insert) matches
             match = lo_m;
           } else {
-            // first match met while walking newest-first = the largest matching row
             uint32_t gt = 0;
-            for (uint32_t k = s[j]; k < e[j]; ++k) gt += ent[k].y > hi_m;
+#pragma unroll
+            for (int k = 0; k < kRegEnt; ++k) gt += (uint32_t(k) < nj) && E[j][k].y > hi_m;
+            for (uint32_t k = kRegEnt; k < nj; ++k) gt += ent[s[j] + k].y > hi_m;
             acc[3] += 2 + gt;
             match = hi_m;
           }
@@ -182,21 +210,29 @@ __global__ __launch_bounds__(kBlock) void k_chain_probe(RelView r, FastMod fm, u
             if (o < out_cap) out[o] = make_uint2(pr[j], match);
           }
         }
-        if (MODE == kDense && i < out_cap) out[i] = make_uint2(pr[j], match);
+        if (MODE == kDense && i < out_cap)
+          __builtin_nontemporal_store((uint64_t(match) << 32) | pr[j], reinterpret_cast<uint64_t*>(out + i));
       } else {
-        if (MODE != kWrite) acc[3] += n;
+        if (MODE != kWrite) acc[3] += nj;
         uint64_t o = (MODE == kWrite) ? cnt[i] : 0;
-        for (uint32_t k = s[j]; k < e[j]; ++k) {
-          const uint2 E = ent[k];
-          if (E.x != h[j]) continue;
+        for (uint32_t k = 0; k < nj; ++k) {
+          uint2 e2;
+          if (k < kRegEnt) {
+            e2 = E[j][0];
+#pragma unroll
+            for (int q = 1; q < kRegEnt; ++q) e2 = (k == uint32_t(q)) ? E[j][q] : e2;
+          } else {
+            e2 = ent[s[j] + k];
+          }
+          if (e2.x != h[j]) continue;
           ++nout;
           if (MODE == kWrite) {
-            if (o < out_cap) out[o] = make_uint2(pr[j], E.y);
+            if (o < out_cap) out[o] = make_uint2(pr[j], e2.y);
             ++o;
           } else {
             acc[4] += pr[j];
-            acc[5] += E.y;
-            const uint64_t ph = pair_hash(pr[j], E.y);
+            acc[5] += e2.y;
+            const uint64_t ph = pair_hash(pr[j], e2.y);
             acc[7] += ph;
             acc[8] ^= ph;
           }

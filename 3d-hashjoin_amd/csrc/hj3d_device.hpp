@@ -128,6 +128,29 @@ __device__ __forceinline__ void block_flush(const uint64_t (&v)[NF], uint64_t* d
   }
 }
 
+// Block-reduce NF u64 fields (last NXOR with xor) and store the block's totals to
+// dst_row[0..NF) without atomics (per-block partials, summed by reduce_partials: deterministic
+// and free of same-address atomic serialisation, ~12 ns per same-line atomic on MI355X).
+template <int NF, int NXOR>
+__device__ __forceinline__ void block_store(const uint64_t (&v)[NF], uint64_t* dst_row) {
+  __shared__ uint64_t red[16][NF];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  uint64_t w[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) w[f] = (f >= NF - NXOR) ? wave_xor(v[f]) : wave_sum(v[f]);
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) red[wid][f] = w[f];
+  }
+  __syncthreads();
+  if (threadIdx.x < NF) {
+    const int f = threadIdx.x;
+    uint64_t acc = 0;
+    for (int k = 0; k < nw; ++k) acc = (f >= NF - NXOR) ? (acc ^ red[k][f]) : (acc + red[k][f]);
+    dst_row[f] = acc;
+  }
+}
+
 // Exclusive prefix sum over a wave (64 lanes) of u32 values; returns the wave total in *total.
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t* total) {
   const int lane = threadIdx.x & 63;

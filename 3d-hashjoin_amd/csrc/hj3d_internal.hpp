@@ -53,7 +53,7 @@ struct hj3d_ctx {
   int num_cus = 256;
   std::string last_error;
   // scratch arena slots (see api for their use)
-  hj3d::DevBuf scratch[8];
+  hj3d::DevBuf scratch[12];
   hj3d::DevBuf res;       // device result slot (u64 fields) for probe / probe2
   hj3d::DevBuf misc;      // small device reductions (statistics)
   uint32_t res_flags = 0;     // flags of the last probe (overflow check in hj3d_probe_result)
@@ -62,6 +62,8 @@ struct hj3d_ctx {
   uint64_t res_nprobe = 0;    // probe tuples of the last probe
   // phase timers
   bool timing = false;
+  bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
+  uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;
@@ -91,6 +93,11 @@ hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, 
 // (k0,v0); (k1,v1) is a same-size scratch double buffer.
 hipError_t radix_sort_pairs(hj3d_ctx* ctx, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n,
                             int bits, hipStream_t s);
+// radix.hip: partitioned (LDS-slice) build / probe of the chaining table
+bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
+hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                       uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
@@ -117,7 +124,19 @@ hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n
                                 void* res, hipStream_t s);
 
 // Scratch slot ids in hj3d_ctx::scratch.
-enum ScratchSlot { kScrScan = 0, kScrSlot = 1, kScrSortK = 2, kScrSortV = 3, kScrA = 4, kScrB = 5, kScrC = 6, kScrD = 7 };
+enum ScratchSlot {
+  kScrScan = 0, kScrSlot = 1, kScrSortK = 2, kScrSortV = 3, kScrA = 4, kScrB = 5, kScrC = 6, kScrD = 7,
+  kScrPairs = 8,    // radix-partitioned (hash, row) pairs
+  kScrPHist = 9,    // radix partition histograms / offsets
+  kScrPartial = 10, // per-block result partials
+  kScrPStart = 11   // partition starts of the probe side
+};
+
+// Per-block result partials: kernels store their block totals (block_store) to
+// partials[block * nf ...]; reduce_partials adds the column sums into res (stream-ordered).
+// set0 != ~0: res[0] is set to set0 instead of accumulated (scanned-tuple count known on the host).
+hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
+                           uint64_t set0 = ~0ull);
 
 inline RelView view_of(const hj3d_rel& r) {
   RelView v;

@@ -1,0 +1,405 @@
+// radix.hip — radix-partitioned build and probe of the chaining table (the hot path).
+//
+// Why: a probe of the CSR table costs two dependent random reads (directory, entries). On
+// MI355X such small random reads are served at ~55 G/s from the Infinity Cache (~250 G/s from
+// L2), so a 1e8-probe strand against a 1e7 table is bound by random-access throughput at
+// ~4 ms while streaming S itself takes 0.17 ms (micro/micro_probe.hip). The fix is the classic
+// radix join, sized for CDNA4's 160 KB LDS:
+//   partition: stream the tuples once to count, once to scatter (hash, row) pairs into P
+//              partitions by bucket range (partition p owns local buckets [p*W, (p+1)*W));
+//   probe:     one 1024-thread workgroup per partition copies its table slice (off + entries,
+//              <= 144 KB, coalesced) into LDS and probes all of the partition's pairs against
+//              LDS; results are written densely in partition order.
+//   build:     same partitioning of R, then one workgroup per partition counts, scans and
+//              scatters its slice of the global CSR directory in LDS: the table is the plain
+//              CSR layout of chain.hip (probe-side partitioning is independent of the build).
+// Bucket ranges keep the reference's per-bucket semantics (chain order, comparison counts,
+// statistics) untouched: every counter is computed per bucket exactly as in chain.hip.
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kPBlock = 256;                     // partition kernels
+constexpr int kPRounds = 32;
+constexpr int kPTile = kPBlock * kPRounds;       // 8192 tuples per partition tile
+constexpr uint32_t kMaxParts = 8192;
+constexpr int kJBlock = 1024;                    // build / probe workgroups (16 waves, 1 per CU)
+constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
+constexpr uint32_t kProbeLdsWords = 36864;       // 144 KB LDS table slice per probe workgroup
+constexpr int kItems = 4;
+
+struct FastDiv {  // exact floor(a / d) for u32 a, 1 <= d < 2^32
+  uint64_t m;
+  static FastDiv make(uint32_t d) {
+    FastDiv f;
+    f.m = ~uint64_t(0) / d + 1;
+    return f;
+  }
+  __device__ __forceinline__ uint32_t div(uint32_t a) const { return d1 ? a : uint32_t(__umul64hi(m, uint64_t(a))); }
+  bool d1 = false;
+};
+inline FastDiv make_div(uint32_t d) {
+  FastDiv f = FastDiv::make(d);
+  f.d1 = d == 1;
+  return f;
+}
+
+__global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                     uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist) {
+  __shared__ uint32_t cnt[kMaxParts];
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
+  __syncthreads();
+  const uint64_t base = uint64_t(blockIdx.x) * kPTile;
+#pragma unroll 4
+  for (int j = 0; j < kPRounds; ++j) {
+    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    if (i < r.n) {
+      const uint32_t bl = fm.mod(murmur32(r.key(i))) - lo;
+      if (bl < nbl) atomicAdd(&cnt[fw.div(bl)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * ntiles + blockIdx.x] = cnt[p];
+}
+
+// Scatter (hash, row) pairs to their partitions. Positions inside a partition come from LDS
+// cursors (order inside a partition is irrelevant to every counter). A tile's elements of one
+// partition land contiguously, so the 8-B stores of a workgroup merge into whole lines in L2.
+__global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                        uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
+                                                        uint2* __restrict__ out) {
+  __shared__ uint32_t cur[kMaxParts];
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] = offs[uint64_t(p) * ntiles + blockIdx.x];
+  __syncthreads();
+  const uint64_t base = uint64_t(blockIdx.x) * kPTile;
+#pragma unroll 4
+  for (int j = 0; j < kPRounds; ++j) {
+    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    if (i < r.n) {
+      const uint32_t h = murmur32(r.key(i));
+      const uint32_t bl = fm.mod(h) - lo;
+      if (bl < nbl) {
+        const uint32_t pos = atomicAdd(&cur[fw.div(bl)], 1u);
+        out[pos] = make_uint2(h, r.row(i));
+      }
+    }
+  }
+}
+
+__global__ void k_rp_starts(const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t P, uint32_t* __restrict__ ps) {
+  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p <= P; p += gridDim.x * blockDim.x)
+    ps[p] = offs[uint64_t(p) * ntiles];
+}
+
+// Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. 1024 threads.
+__device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
+  const uint32_t per = (n + kJBlock - 1) / kJBlock;
+  const uint32_t beg = threadIdx.x * per;
+  const uint32_t end = min(beg + per, n);
+  uint32_t local = 0;
+  for (uint32_t k = beg; k < end; ++k) local += a[k];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t x = local;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t y = __shfl_up(x, o, kWave);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[wid] = x;
+  __syncthreads();
+  uint32_t wpre = 0, tot = 0;
+  for (int w = 0; w < kJBlock / kWave; ++w) {
+    const uint32_t v = wsum[w];
+    if (w < wid) wpre += v;
+    tot += v;
+  }
+  uint32_t run = wpre + x - local;
+  for (uint32_t k = beg; k < end; ++k) {
+    const uint32_t v = a[k];
+    a[k] = run;
+    run += v;
+  }
+  __syncthreads();
+  return tot;
+}
+
+// One workgroup per build partition: local count -> scan -> scatter of the CSR slice.
+__global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                      FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
+                                                      uint32_t* __restrict__ off, uint2* __restrict__ ent) {
+  __shared__ uint32_t cnt[kBuildSlice];
+  __shared__ uint32_t wsum[kJBlock / kWave];
+  const uint32_t p = blockIdx.x;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, nbl - b0);
+  const uint32_t s0 = ps[p], s1 = ps[p + 1];
+  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
+  __syncthreads();
+  for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) atomicAdd(&cnt[fm.mod(pairs[i].x) - lo - b0], 1u);
+  __syncthreads();
+  lds_excl_scan(cnt, nbs, wsum);
+  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+  if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
+  __syncthreads();
+  for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) {
+    const uint2 e = pairs[i];
+    const uint32_t pos = atomicAdd(&cnt[fm.mod(e.x) - lo - b0], 1u);
+    ent[s0 + pos] = e;
+  }
+}
+
+enum Mode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
+
+// Reference comparison count and match of one probe against bucket entries [s, s+n) of `E`
+// (LDS or global): see chain.hip for the derivation of the chain-order arithmetic.
+template <bool UNIQUE, int MODE, typename EntT>
+__device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT* E, uint32_t s, uint32_t n,
+                                             uint64_t (&acc)[kProbeFields], uint64_t i, uint2* __restrict__ out,
+                                             uint64_t out_cap, uint64_t* __restrict__ cnt) {
+  if (MODE != kWrite) acc[0] += 1;
+  if (UNIQUE) {
+    uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
+    for (uint32_t k = s; k < s + n; ++k) {
+      const uint2 e = E[k];
+      minrow = min(minrow, e.y);
+      if (e.x == h) {
+        ++nm;
+        lo_m = min(lo_m, e.y);
+        hi_m = max(hi_m, e.y);
+      }
+    }
+    uint32_t match = kInvalid;
+    if (n != 0) {
+      if (nm == 0) {
+        acc[3] += n;
+      } else if (lo_m == minrow) {
+        acc[3] += 1;
+        match = lo_m;
+      } else {
+        uint32_t gt = 0;
+        for (uint32_t k = s; k < s + n; ++k) gt += E[k].y > hi_m;
+        acc[3] += 2 + gt;
+        match = hi_m;
+      }
+    }
+    if (MODE == kDense) {
+      if (i < out_cap)
+        __builtin_nontemporal_store((uint64_t(match) << 32) | pr, reinterpret_cast<uint64_t*>(out + i));
+    }
+    if (match != kInvalid) {
+      if (MODE == kWrite) {
+        const uint64_t o = cnt[i];
+        if (o < out_cap) out[o] = make_uint2(pr, match);
+      } else {
+        acc[1] += 1;
+        acc[2] += 1;
+        acc[4] += pr;
+        acc[5] += match;
+        const uint64_t ph = pair_hash(pr, match);
+        acc[7] += ph;
+        acc[8] ^= ph;
+      }
+    }
+    if (MODE == kCount) cnt[i] = match != kInvalid;
+  } else {
+    if (MODE != kWrite) acc[3] += n;
+    uint64_t o = (MODE == kWrite) ? cnt[i] : 0;
+    uint32_t nout = 0;
+    for (uint32_t k = s; k < s + n; ++k) {
+      const uint2 e = E[k];
+      if (e.x != h) continue;
+      ++nout;
+      if (MODE == kWrite) {
+        if (o < out_cap) out[o] = make_uint2(pr, e.y);
+        ++o;
+      } else {
+        acc[4] += pr;
+        acc[5] += e.y;
+        const uint64_t ph = pair_hash(pr, e.y);
+        acc[7] += ph;
+        acc[8] ^= ph;
+      }
+    }
+    if (MODE != kWrite) {
+      acc[1] += nout != 0;
+      acc[2] += nout;
+    }
+    if (MODE == kCount) cnt[i] = nout;
+  }
+}
+
+// One workgroup per (partition, split): the partition's table slice is staged in LDS when it
+// fits (always, for key builds of uniform size), else the workgroup reads it through L2.
+template <bool UNIQUE, int MODE>
+__global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                      const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
+                                                      FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
+                                                      uint32_t splits, uint2* __restrict__ out, uint64_t out_cap,
+                                                      uint64_t* __restrict__ cnt, uint64_t* __restrict__ partials) {
+  __shared__ uint32_t lds[kProbeLdsWords];
+  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, nbl - b0);
+  const uint32_t e0 = off[b0], e1 = off[b0 + nbs];
+  const uint32_t ne = e1 - e0;
+  const bool fits = (nbs + 1) + 2ull * ne + 1 <= kProbeLdsWords;  // +1 word: 8-B alignment of entries
+  uint32_t* loff = lds;
+  const uint32_t ent_word = (nbs + 2) & ~1u;
+  uint2* lent = reinterpret_cast<uint2*>(lds + ent_word);
+  if (fits) {
+    for (uint32_t k = threadIdx.x; k <= nbs; k += kJBlock) loff[k] = off[b0 + k] - e0;
+    for (uint32_t k = threadIdx.x; k < ne; k += kJBlock) lent[k] = ent[e0 + k];
+  }
+  __syncthreads();
+  const uint32_t s0 = ps[p], s1 = ps[p + 1];
+  const uint32_t len = s1 - s0;
+  const uint32_t q0 = s0 + uint32_t(uint64_t(len) * sp / splits);
+  const uint32_t q1 = s0 + uint32_t(uint64_t(len) * (sp + 1) / splits);
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t base = q0; base < q1; base += kJBlock * kItems) {
+    uint2 pr[kItems];
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      const uint32_t i = base + j * kJBlock + threadIdx.x;
+      const uint64_t v = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
+      pr[j] = make_uint2(uint32_t(v), uint32_t(v >> 32));
+    }
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      const uint32_t i = base + j * kJBlock + threadIdx.x;
+      if (i >= q1) continue;
+      const uint32_t h = pr[j].x;
+      const uint32_t bl = fm.mod(h) - lo - b0;
+      if (fits) {
+        const uint32_t s = loff[bl];
+        probe_bucket<UNIQUE, MODE>(h, pr[j].y, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+      } else {
+        const uint32_t s = off[b0 + bl];
+        probe_bucket<UNIQUE, MODE>(h, pr[j].y, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
+      }
+    }
+  }
+  if (MODE != kWrite) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+}
+
+struct Plan {
+  uint32_t W = 1, P = 1, ntiles = 0;
+  FastDiv fw;
+};
+
+Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
+  Plan pl;
+  pl.W = W < 1 ? 1 : W;
+  pl.P = uint32_t((uint64_t(nbl) + pl.W - 1) / pl.W);
+  if (pl.P == 0) pl.P = 1;
+  pl.ntiles = uint32_t((n + kPTile - 1) / kPTile);
+  pl.fw = make_div(pl.W);
+  return pl;
+}
+
+// Partition `r` into (hash, row) pairs by bucket range; ps[0..P] = partition starts.
+hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
+                           uint32_t* ps, hipStream_t s) {
+  hipError_t e;
+  const uint64_t hn = uint64_t(pl.P) * pl.ntiles + 1;
+  if ((e = ctx->scratch[kScrPHist].ensure(hn * sizeof(uint32_t))) != hipSuccess) return e;
+  uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
+  const RelView v = view_of(r);
+  const uint32_t lo = uint32_t(t->desc.bucket_lo);
+  if (r.n) {
+    hipLaunchKernelGGL(k_rp_hist, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
+                       pl.ntiles, hist);
+  }
+  if ((e = exclusive_scan_u32(ctx, hist, hist, hn - 1, s)) != hipSuccess) return e;
+  if (r.n) {
+    hipLaunchKernelGGL(k_rp_scatter, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
+                       pl.ntiles, hist, out);
+  }
+  if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
+  hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, pl.ntiles, pl.P, ps);
+  return hipGetLastError();
+}
+
+template <bool UNIQUE, int MODE>
+void launch_probe(const hj3d_table* t, const Plan& pl, uint32_t splits, const uint2* pairs, const uint32_t* ps,
+                  uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, hipStream_t s) {
+  hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
+                     t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
+                     t->nb_local, pl.W, splits, out, cap, cnt, partials);
+}
+
+}  // namespace
+
+bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe) {
+  // worth the partition passes once the probe side is large (HJ3D_OPT_RADIX_MIN, default 2^20)
+  return t->desc.kind == HJ3D_CHAIN && !ctx->force_direct && n_probe >= ctx->radix_min && n_probe > 0 &&
+         t->nb_local >= 64 && n_probe < (1ull << 32);
+}
+
+hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+  hipError_t e;
+  const uint32_t nbl = t->nb_local;
+  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->ent.ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
+  const Plan pl = plan_for(nbl, kBuildSlice, r.n);
+  if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
+  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
+  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
+  if (nbl) {
+    hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
+                       pl.W, t->off.as<uint32_t>(), t->ent.as<uint2>());
+  } else {
+    if ((e = hipMemsetAsync(t->off.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+  }
+  t->n_build = r.n;
+  return hipGetLastError();
+}
+
+hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                       uint64_t out_cap, uint64_t* res, hipStream_t s) {
+  hipError_t e;
+  const uint32_t nbl = t->nb_local;
+  // slice width: 80% of the LDS slice budget at the table's mean bucket fill
+  const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
+  uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
+  if (W < 64) W = 64;
+  const Plan pl = plan_for(nbl, W, r.n);
+  if (pl.P > kMaxParts) return hipErrorNotSupported;
+  uint32_t splits = 1;
+  const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
+  if (pl.P < want_blocks) splits = (want_blocks + pl.P - 1) / pl.P;
+  if ((e = ctx->scratch[kScrPairs].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  const uint32_t nblocks = pl.P * splits;
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+    return e;
+  uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
+  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
+  uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
+  const bool unique = flags & HJ3D_PROBE_UNIQUE;
+  const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
+  uint2* o = static_cast<uint2*>(out);
+  if (!emit) {
+    if (unique) launch_probe<true, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, s);
+    else launch_probe<false, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, s);
+  } else if (unique) {
+    launch_probe<true, kDense>(t, pl, splits, pairs, ps, o, out_cap, nullptr, partials, s);
+  } else {
+    if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+    uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
+    if ((e = hipMemsetAsync(cnt, 0, (r.n + 1) * sizeof(uint64_t), s)) != hipSuccess) return e;
+    launch_probe<false, kCount>(t, pl, splits, pairs, ps, nullptr, 0, cnt, partials, s);
+    // only the probes that landed in owned buckets are counted; unowned pairs were dropped
+    if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
+    launch_probe<false, kWrite>(t, pl, splits, pairs, ps, o, out_cap, cnt, nullptr, s);
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
+  return reduce_partials(partials, nblocks, kProbeFields, 1, res, s, r.n);
+}
+
+}  // namespace hj3d

@@ -133,7 +133,36 @@ hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t
   return hipGetLastError();
 }
 
+// Column sums of per-block partials: one wave per field (nf <= 16), xor for the last nxor.
+__global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __restrict__ part, uint32_t nblocks, int nf,
+                                                          int nxor, uint64_t* __restrict__ res, uint64_t set0) {
+  const int f = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  if (f >= nf) return;
+  const bool x = f >= nf - nxor;
+  uint64_t acc = 0;
+  for (uint32_t b = lane; b < nblocks; b += 64) {
+    const uint64_t v = part[uint64_t(b) * nf + f];
+    acc = x ? (acc ^ v) : (acc + v);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint64_t w = __shfl_xor(acc, o, kWave);
+    acc = x ? (acc ^ w) : (acc + w);
+  }
+  if (lane == 0) {
+    if (f == 0 && set0 != ~0ull) res[0] = set0;
+    else res[f] = x ? (res[f] ^ acc) : (res[f] + acc);
+  }
+}
+
 }  // namespace
+
+hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
+                           uint64_t set0) {
+  if (nf > 16) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(1024), 0, s, partials, nblocks, nf, nxor, res, set0);
+  return hipGetLastError();
+}
 
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
   return excl_scan<uint32_t>(ctx, in, out, n, s);

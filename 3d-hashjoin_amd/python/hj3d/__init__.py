@@ -25,6 +25,7 @@ HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT = 0x1, 0x2, 0x4
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION = range(4)
+OPT_FORCE_DIRECT, OPT_RADIX_MIN = 1, 2
 
 MASK64 = (1 << 64) - 1
 
@@ -84,6 +85,7 @@ def lib():
         "hj3d_ctx_sync": (st, [p]),
         "hj3d_last_error": (C.c_char_p, [p]),
         "hj3d_ctx_timing": (st, [p, i32]),
+        "hj3d_ctx_set_option": (st, [p, i32, C.c_int64]),
         "hj3d_ctx_timer": (st, [p, i32, C.POINTER(C.c_double), C.POINTER(u64)]),
         "hj3d_ctx_timer_reset": (st, [p]),
         "hj3d_table_create": (st, [p, D, C.POINTER(p)]),
@@ -204,6 +206,17 @@ class Context:
 
     def sync(self):
         self._check(lib().hj3d_ctx_sync(self.h), "sync")
+
+    def set_option(self, option: int, value: int):
+        self._check(lib().hj3d_ctx_set_option(self.h, option, value), "set_option")
+
+    def force_direct(self, on: bool = True):
+        """A/B switch: chaining build/probe without the radix-partitioned kernels."""
+        self.set_option(OPT_FORCE_DIRECT, int(on))
+
+    def radix_min(self, n: int):
+        """Smallest probe side (tuples) that takes the radix-partitioned chaining kernels."""
+        self.set_option(OPT_RADIX_MIN, int(n))
 
     def timing(self, enable: bool = True):
         self._check(lib().hj3d_ctx_timing(self.h, int(enable)), "timing")

@@ -118,12 +118,24 @@ typedef struct {
 uint64_t hj3d_mix64(uint64_t z);
 
 /* ---- context ---- */
-hj3d_status hj3d_ctx_create(int device, void* hip_stream /* NULL: a new non-blocking stream */, hj3d_ctx** out);
+/* hip_stream: the stream every call of this context is enqueued on; NULL = the device's null
+ * (default) stream, i.e. the stream torch uses unless told otherwise. */
+hj3d_status hj3d_ctx_create(int device, void* hip_stream, hj3d_ctx** out);
 void        hj3d_ctx_destroy(hj3d_ctx* ctx);
 hj3d_status hj3d_ctx_set_stream(hj3d_ctx* ctx, void* hip_stream);
 void*       hj3d_ctx_stream(const hj3d_ctx* ctx);
 hj3d_status hj3d_ctx_sync(hj3d_ctx* ctx); /* synchronous: waits for the stream */
 const char* hj3d_last_error(const hj3d_ctx* ctx);
+/* Engine options. HJ3D_OPT_FORCE_DIRECT (0/1): probe / build the chaining table without the
+ * radix-partitioned (LDS-slice) kernels, i.e. with one random table access chain per tuple
+ * (kept for small inputs and for A/B measurements). */
+enum {
+  HJ3D_OPT_FORCE_DIRECT = 1,
+  /* HJ3D_OPT_RADIX_MIN (tuples): probes of at least this many tuples (builds of at least 1/16 of
+   * it) use the radix-partitioned kernels; default 2^20. */
+  HJ3D_OPT_RADIX_MIN = 2
+};
+hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
  * (phase ids below). hj3d_ctx_timer reads (synchronously) the summed milliseconds and the
  * number of recorded intervals since the last reset. */
