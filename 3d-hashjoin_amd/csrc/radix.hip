@@ -20,14 +20,14 @@
 namespace hj3d {
 namespace {
 
-constexpr int kPBlock = 256;                     // partition kernels
-constexpr int kPRounds = 32;
-constexpr int kPTile = kPBlock * kPRounds;       // 8192 tuples per partition tile
-constexpr uint32_t kMaxParts = 8192;
+constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
+constexpr int kPRounds = 16;
+constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
+constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr int kJBlock = 1024;                    // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
 constexpr uint32_t kProbeLdsWords = 36864;       // 144 KB LDS table slice per probe workgroup
-constexpr int kItems = 4;
+constexpr int kItems = 12;
 
 struct FastDiv {  // exact floor(a / d) for u32 a, 1 <= d < 2^32
   uint64_t m;
@@ -51,11 +51,17 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
   __syncthreads();
   const uint64_t base = uint64_t(blockIdx.x) * kPTile;
-#pragma unroll 4
+  uint32_t key[kPRounds];
+#pragma unroll
+  for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
+    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    key[j] = i < r.n ? r.key(i) : 0u;
+  }
+#pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
     const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
     if (i < r.n) {
-      const uint32_t bl = fm.mod(murmur32(r.key(i))) - lo;
+      const uint32_t bl = fm.mod(murmur32(key[j])) - lo;
       if (bl < nbl) atomicAdd(&cnt[fw.div(bl)], 1u);
     }
   }
@@ -63,27 +69,52 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * ntiles + blockIdx.x] = cnt[p];
 }
 
-// Scatter (hash, row) pairs to their partitions. Positions inside a partition come from LDS
-// cursors (order inside a partition is irrelevant to every counter). A tile's elements of one
-// partition land contiguously, so the 8-B stores of a workgroup merge into whole lines in L2.
+__device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
+
+// Scatter (hash, row) pairs to their partitions. The tile is first ranked per partition with
+// LDS atomics (order inside a partition is irrelevant to every counter), staged in LDS in
+// partition order (128 KB), then written out so that consecutive lanes store consecutive
+// addresses of one partition's run: ~16 elements = one 128-B line per partition and tile at
+// the probe's fan-out, instead of one scattered 8-B store per tuple.
 __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
                                                         uint2* __restrict__ out) {
-  __shared__ uint32_t cur[kMaxParts];
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] = offs[uint64_t(p) * ntiles + blockIdx.x];
-  __syncthreads();
+  __shared__ uint2 stage[kPTile];
+  __shared__ uint32_t loc[kMaxParts];   // local counts, then local run starts
+  __shared__ uint32_t gb[kMaxParts];    // global run start of each partition for this tile
+  __shared__ uint32_t wsum[kPBlock / kWave];
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
+    loc[p] = 0;
+    gb[p] = offs[uint64_t(p) * ntiles + blockIdx.x];
+  }
   const uint64_t base = uint64_t(blockIdx.x) * kPTile;
-#pragma unroll 4
+  uint32_t h[kPRounds], rk[kPRounds];
+#pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
     const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-    if (i < r.n) {
-      const uint32_t h = murmur32(r.key(i));
-      const uint32_t bl = fm.mod(h) - lo;
-      if (bl < nbl) {
-        const uint32_t pos = atomicAdd(&cur[fw.div(bl)], 1u);
-        out[pos] = make_uint2(h, r.row(i));
-      }
-    }
+    h[j] = i < r.n ? r.key(i) : 0u;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kPRounds; ++j) {
+    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    h[j] = murmur32(h[j]);
+    const uint32_t bl = fm.mod(h[j]) - lo;
+    rk[j] = (i < r.n && bl < nbl) ? atomicAdd(&loc[fw.div(bl)], 1u) : kInvalid;
+  }
+  __syncthreads();
+  const uint32_t m = lds_excl_scan(loc, P, wsum);  // staged tuples of this tile
+#pragma unroll
+  for (int j = 0; j < kPRounds; ++j) {
+    if (rk[j] == kInvalid) continue;
+    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    stage[loc[fw.div(fm.mod(h[j]) - lo)] + rk[j]] = make_uint2(h[j], r.row(i));
+  }
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
+    const uint2 e = stage[k];
+    const uint32_t p = fw.div(fm.mod(e.x) - lo);
+    out[gb[p] + (k - loc[p])] = e;
   }
 }
 
@@ -247,9 +278,36 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ 
   uint32_t* loff = lds;
   const uint32_t ent_word = (nbs + 2) & ~1u;
   uint2* lent = reinterpret_cast<uint2*>(lds + ent_word);
-  if (fits) {
-    for (uint32_t k = threadIdx.x; k <= nbs; k += kJBlock) loff[k] = off[b0 + k] - e0;
-    for (uint32_t k = threadIdx.x; k < ne; k += kJBlock) lent[k] = ent[e0 + k];
+  if (fits) {  // stage the slice: every thread keeps kStage loads in flight before writing LDS
+    constexpr int kStage = 8;
+    for (uint32_t k0 = threadIdx.x; k0 <= nbs; k0 += kJBlock * kStage) {
+      uint32_t v[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const uint32_t k = k0 + u * kJBlock;
+        v[u] = k <= nbs ? off[b0 + k] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const uint32_t k = k0 + u * kJBlock;
+        if (k <= nbs) loff[k] = v[u] - e0;
+      }
+    }
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
+    uint64_t* dst = reinterpret_cast<uint64_t*>(lent);
+    for (uint32_t k0 = threadIdx.x; k0 < ne; k0 += kJBlock * kStage) {
+      uint64_t v[kStage];
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const uint32_t k = k0 + u * kJBlock;
+        v[u] = k < ne ? src[k] : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kStage; ++u) {
+        const uint32_t k = k0 + u * kJBlock;
+        if (k < ne) dst[k] = v[u];
+      }
+    }
   }
   __syncthreads();
   const uint32_t s0 = ps[p], s1 = ps[p + 1];
