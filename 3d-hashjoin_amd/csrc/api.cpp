@@ -235,11 +235,12 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
-  if (t->desc.kind == HJ3D_CHAIN)
+  if (t->desc.kind == HJ3D_CHAIN) {
     e = (!ctx->force_direct && build->n >= (ctx->radix_min >> 4) && build->n > 0 && t->nb_local >= 64)
             ? radix_build(ctx, t, *build, ctx->stream)
             : chain_build(ctx, t, *build, ctx->stream);
-  else
+    if (e == hipSuccess) e = sort_small_buckets(ctx, t, ctx->stream);
+  } else
     e = nested_build(ctx, t, *build, ctx->stream);
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");

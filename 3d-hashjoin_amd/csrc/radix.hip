@@ -28,6 +28,7 @@ constexpr int kJBlock = 1024;                    // build / probe workgroups (16
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
 constexpr uint32_t kProbeLdsWords = 36864;       // 144 KB LDS table slice per probe workgroup
 constexpr int kItems = 12;
+constexpr uint32_t kSortedMax = 32;             // buckets up to this size are kept sorted by row
 
 struct FastDiv {  // exact floor(a / d) for u32 a, 1 <= d < 2^32
   uint64_t m;
@@ -183,37 +184,55 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
 enum Mode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
 
 // Reference comparison count and match of one probe against bucket entries [s, s+n) of `E`
-// (LDS or global): see chain.hip for the derivation of the chain-order arithmetic.
-template <bool UNIQUE, int MODE, typename EntT>
+// (LDS or global). Buckets of <= kSortedMax entries are sorted by row (k_sort_small_buckets), so
+// the reference's walk [first insert, newest, ..., second insert] visits sorted index j at
+// position 1 (j == 0) or n - j + 1: one pass finds the first match of that walk. Longer
+// buckets use the order-free two-pass form of chain.hip. CK: fold output checksums.
+template <bool UNIQUE, int MODE, bool CK, typename EntT>
 __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT* E, uint32_t s, uint32_t n,
                                              uint64_t (&acc)[kProbeFields], uint64_t i, uint2* __restrict__ out,
                                              uint64_t out_cap, uint64_t* __restrict__ cnt) {
   if (MODE != kWrite) acc[0] += 1;
   if (UNIQUE) {
-    uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
-    for (uint32_t k = s; k < s + n; ++k) {
-      const uint2 e = E[k];
-      minrow = min(minrow, e.y);
-      if (e.x == h) {
-        ++nm;
-        lo_m = min(lo_m, e.y);
-        hi_m = max(hi_m, e.y);
+    uint32_t match = kInvalid, cmps = 0;
+    if (n <= kSortedMax) {
+      uint32_t jm = kInvalid, rowm = 0;
+      bool m0 = false;
+      for (uint32_t k = 0; k < n; ++k) {
+        const uint2 e = E[s + k];
+        if (e.x == h) {
+          m0 = m0 || k == 0;
+          if (k == 0) rowm = e.y;
+          if (!m0) { jm = k; rowm = e.y; }
+        }
       }
-    }
-    uint32_t match = kInvalid;
-    if (n != 0) {
+      if (m0) { cmps = 1; match = rowm; }
+      else if (jm != kInvalid) { cmps = n - jm + 1; match = rowm; }
+      else cmps = n;
+    } else {
+      uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
+      for (uint32_t k = s; k < s + n; ++k) {
+        const uint2 e = E[k];
+        minrow = min(minrow, e.y);
+        if (e.x == h) {
+          ++nm;
+          lo_m = min(lo_m, e.y);
+          hi_m = max(hi_m, e.y);
+        }
+      }
       if (nm == 0) {
-        acc[3] += n;
+        cmps = n;
       } else if (lo_m == minrow) {
-        acc[3] += 1;
+        cmps = 1;
         match = lo_m;
       } else {
         uint32_t gt = 0;
         for (uint32_t k = s; k < s + n; ++k) gt += E[k].y > hi_m;
-        acc[3] += 2 + gt;
+        cmps = 2 + gt;
         match = hi_m;
       }
     }
+    if (MODE != kWrite) acc[3] += cmps;
     if (MODE == kDense) {
       if (i < out_cap)
         __builtin_nontemporal_store((uint64_t(match) << 32) | pr, reinterpret_cast<uint64_t*>(out + i));
@@ -225,11 +244,13 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
       } else {
         acc[1] += 1;
         acc[2] += 1;
-        acc[4] += pr;
-        acc[5] += match;
-        const uint64_t ph = pair_hash(pr, match);
-        acc[7] += ph;
-        acc[8] ^= ph;
+        if (CK) {
+          acc[4] += pr;
+          acc[5] += match;
+          const uint64_t ph = pair_hash(pr, match);
+          acc[7] += ph;
+          acc[8] ^= ph;
+        }
       }
     }
     if (MODE == kCount) cnt[i] = match != kInvalid;
@@ -244,7 +265,7 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
       if (MODE == kWrite) {
         if (o < out_cap) out[o] = make_uint2(pr, e.y);
         ++o;
-      } else {
+      } else if (CK) {
         acc[4] += pr;
         acc[5] += e.y;
         const uint64_t ph = pair_hash(pr, e.y);
@@ -262,7 +283,7 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
 
 // One workgroup per (partition, split): the partition's table slice is staged in LDS when it
 // fits (always, for key builds of uniform size), else the workgroup reads it through L2.
-template <bool UNIQUE, int MODE>
+template <bool UNIQUE, int MODE, bool CK>
 __global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                       const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
                                                       FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
@@ -331,10 +352,10 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ 
       const uint32_t bl = fm.mod(h) - lo - b0;
       if (fits) {
         const uint32_t s = loff[bl];
-        probe_bucket<UNIQUE, MODE>(h, pr[j].y, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(h, pr[j].y, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
       } else {
         const uint32_t s = off[b0 + bl];
-        probe_bucket<UNIQUE, MODE>(h, pr[j].y, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(h, pr[j].y, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
       }
     }
   }
@@ -381,13 +402,44 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
 
 template <bool UNIQUE, int MODE>
 void launch_probe(const hj3d_table* t, const Plan& pl, uint32_t splits, const uint2* pairs, const uint32_t* ps,
-                  uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, hipStream_t s) {
-  hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
-                     t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
-                     t->nb_local, pl.W, splits, out, cap, cnt, partials);
+                  uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, bool ck, hipStream_t s) {
+  if (ck)
+    hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE, true>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
+                       t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
+                       t->nb_local, pl.W, splits, out, cap, cnt, partials);
+  else
+    hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE, false>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
+                       t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
+                       t->nb_local, pl.W, splits, out, cap, cnt, partials);
+}
+
+// Sort every bucket of 2..kSortedMax entries by row (insertion sort, one thread per bucket; the
+// bucket was just written and is L2-resident). Longer buckets stay in arrival order.
+__global__ __launch_bounds__(256) void k_sort_small_buckets(const uint32_t* __restrict__ off, uint32_t nbl,
+                                                            uint2* __restrict__ ent) {
+  for (uint32_t b = blockIdx.x * 256 + threadIdx.x; b < nbl; b += gridDim.x * 256) {
+    const uint32_t s = off[b], n = off[b + 1] - s;
+    if (n < 2 || n > kSortedMax) continue;
+    for (uint32_t k = 1; k < n; ++k) {
+      const uint2 x = ent[s + k];
+      uint32_t j = k;
+      while (j > 0 && ent[s + j - 1].y > x.y) {
+        ent[s + j] = ent[s + j - 1];
+        --j;
+      }
+      ent[s + j] = x;
+    }
+  }
 }
 
 }  // namespace
+
+hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s) {
+  if (t->nb_local == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_sort_small_buckets, dim3(grid_for(ctx, t->nb_local, 256 * 4)), dim3(256), 0, s,
+                     t->off.as<const uint32_t>(), t->nb_local, t->ent.as<uint2>());
+  return hipGetLastError();
+}
 
 bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe) {
   // worth the partition passes once the probe side is large (HJ3D_OPT_RADIX_MIN, default 2^20)
@@ -440,20 +492,21 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   const bool unique = flags & HJ3D_PROBE_UNIQUE;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
+  const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   uint2* o = static_cast<uint2*>(out);
   if (!emit) {
-    if (unique) launch_probe<true, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, s);
-    else launch_probe<false, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, s);
+    if (unique) launch_probe<true, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);
+    else launch_probe<false, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);
   } else if (unique) {
-    launch_probe<true, kDense>(t, pl, splits, pairs, ps, o, out_cap, nullptr, partials, s);
+    launch_probe<true, kDense>(t, pl, splits, pairs, ps, o, out_cap, nullptr, partials, ck, s);
   } else {
     if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
     uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
     if ((e = hipMemsetAsync(cnt, 0, (r.n + 1) * sizeof(uint64_t), s)) != hipSuccess) return e;
-    launch_probe<false, kCount>(t, pl, splits, pairs, ps, nullptr, 0, cnt, partials, s);
+    launch_probe<false, kCount>(t, pl, splits, pairs, ps, nullptr, 0, cnt, partials, ck, s);
     // only the probes that landed in owned buckets are counted; unowned pairs were dropped
     if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
-    launch_probe<false, kWrite>(t, pl, splits, pairs, ps, o, out_cap, cnt, nullptr, s);
+    launch_probe<false, kWrite>(t, pl, splits, pairs, ps, o, out_cap, cnt, nullptr, ck, s);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)

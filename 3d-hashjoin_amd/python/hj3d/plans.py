@@ -33,7 +33,7 @@ def num_buckets_exp1(plan: str, card_r: int, num_dv_sa: int, b: int = 1) -> int:
 
 
 def exp1_plan(ctx: Context, plan: str, R, S, nb: int, out=None, table: Table | None = None,
-              stats: bool = True) -> dict:
+              stats: bool = True, checksum: bool = True) -> dict:
     """Run one experiment-1 plan on device relations R, S ((n,3) int32 tensors {k,a,b}).
 
     Returns {nb, c_build, c_probe, c_cmp, c_unnest, c_top, stats, out} with the reference's
@@ -43,7 +43,7 @@ def exp1_plan(ctx: Context, plan: str, R, S, nb: int, out=None, table: Table | N
     probe = Rel(S if bside == "R" else R, key_word=pkey)
     t = table if table is not None else Table(ctx, kind, nb)
     t.build(build)
-    r = ctx.probe(t, probe, unique=unique, unnest=unnest, out=out)
+    r = ctx.probe(t, probe, unique=unique, unnest=unnest, out=out, checksum=checksum)
     if kind == HJ3D_CHAIN:
         c_probe, c_unnest, c_top = r.n_out, 0, r.n_out
     else:

@@ -153,7 +153,7 @@ def main():
         if world == 1:
             table.build(relR)
             ev[1].record()
-            ctx.probe(table, relS, unique=True, out=out, fetch=False)
+            ctx.probe(table, relS, unique=True, out=out, fetch=False, checksum=state.get("ck", False))
         else:
             ctx.partition(relR, nb, world, sendR, cntR)
             rR = hdist.exchange(sendR, cntR, recvR)
@@ -162,7 +162,8 @@ def main():
             ctx.partition(relS, nb, world, sendS, cntS)
             rS = hdist.exchange(sendS, cntS, recvS)
             state["probe_n"] = rS.shape[0]
-            ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True, out=out, fetch=False)
+            ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True, out=out, fetch=False,
+                      checksum=state.get("ck", False))
         ev[2].record()
 
     def events():
@@ -187,6 +188,11 @@ def main():
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     kern_ms, kern_n = ctx.timer(hj3d.T_PROBE_KERNEL)
     kern_avg = kern_ms / max(kern_n, 1)
+    # verification step (outside the timed region): the same step once more with the
+    # order-independent output checksums folded in, compared below with the expected pair set
+    state["ck"] = True
+    step(events())
+    torch.cuda.synchronize()
     res = ctx.probe_result()
     wall_ms = wall * 1e3 / args.steps
     probe_n_local = state.get("probe_n", nS)
