@@ -169,6 +169,35 @@ hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx) {
   return HJ3D_OK;
 }
 
+hj3d_status hj3d_dev_alloc(hj3d_ctx* ctx, uint64_t bytes, void** dev) {
+  if (!ctx || !dev) return HJ3D_EINVAL;
+  *dev = nullptr;
+  return from_hip(ctx, hipMalloc(dev, bytes ? bytes : 1), "hj3d_dev_alloc");
+}
+
+hj3d_status hj3d_dev_free(hj3d_ctx* ctx, void* dev) {
+  if (!ctx) return HJ3D_EINVAL;
+  if (!dev) return HJ3D_OK;
+  (void)hipStreamSynchronize(ctx->stream);
+  return from_hip(ctx, hipFree(dev), "hj3d_dev_free");
+}
+
+hj3d_status hj3d_upload(hj3d_ctx* ctx, void* dev, const void* host, uint64_t bytes) {
+  if (!ctx || (bytes && (!dev || !host))) return HJ3D_EINVAL;
+  if (!bytes) return HJ3D_OK;
+  hipError_t e = hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  return from_hip(ctx, e, "hj3d_upload");
+}
+
+hj3d_status hj3d_download(hj3d_ctx* ctx, void* host, const void* dev, uint64_t bytes) {
+  if (!ctx || (bytes && (!dev || !host))) return HJ3D_EINVAL;
+  if (!bytes) return HJ3D_OK;
+  hipError_t e = hipMemcpyAsync(host, dev, bytes, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  return from_hip(ctx, e, "hj3d_download");
+}
+
 hj3d_status hj3d_table_create(hj3d_ctx* ctx, const hj3d_table_desc* desc, hj3d_table** out) {
   if (!ctx || !desc || !out) return HJ3D_EINVAL;
   *out = nullptr;

@@ -88,6 +88,10 @@ def lib():
         "hj3d_ctx_set_option": (st, [p, i32, C.c_int64]),
         "hj3d_ctx_timer": (st, [p, i32, C.POINTER(C.c_double), C.POINTER(u64)]),
         "hj3d_ctx_timer_reset": (st, [p]),
+        "hj3d_dev_alloc": (st, [p, u64, C.POINTER(p)]),
+        "hj3d_dev_free": (st, [p, p]),
+        "hj3d_upload": (st, [p, p, p, u64]),
+        "hj3d_download": (st, [p, p, p, u64]),
         "hj3d_table_create": (st, [p, D, C.POINTER(p)]),
         "hj3d_table_destroy": (None, [p]),
         "hj3d_table_reserve": (st, [p, p, u64]),

@@ -146,6 +146,13 @@ hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
 hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count);
 hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx);
 
+/* ---- device memory for hosts that link only this ABI (the C++ drop-in layer) ---- */
+hj3d_status hj3d_dev_alloc(hj3d_ctx* ctx, uint64_t bytes, void** dev);
+hj3d_status hj3d_dev_free(hj3d_ctx* ctx, void* dev);
+/* synchronous copies (host <-> device) on the context stream */
+hj3d_status hj3d_upload(hj3d_ctx* ctx, void* dev, const void* host, uint64_t bytes);
+hj3d_status hj3d_download(hj3d_ctx* ctx, void* host, const void* dev, uint64_t bytes);
+
 /* ---- tables ---- */
 hj3d_status hj3d_table_create(hj3d_ctx* ctx, const hj3d_table_desc* desc, hj3d_table** out);
 void        hj3d_table_destroy(hj3d_table* t);
