@@ -44,31 +44,6 @@ bool rel_ok(const hj3d_rel* r) {
   return true;
 }
 
-hipEvent_t take_event(hj3d_ctx* ctx) {
-  if (ctx->pool_used == ctx->event_pool.size()) {
-    hipEvent_t ev;
-    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
-    ctx->event_pool.push_back(ev);
-  }
-  return ctx->event_pool[ctx->pool_used++];
-}
-
-struct PhaseTimer {  // records [a, b) on the context stream when timing is enabled
-  hj3d_ctx* ctx;
-  int phase;
-  hipEvent_t a = nullptr;
-  PhaseTimer(hj3d_ctx* c, int p) : ctx(c), phase(p) {
-    if (ctx->timing && (a = take_event(ctx))) (void)hipEventRecord(a, ctx->stream);
-  }
-  ~PhaseTimer() {
-    if (!a) return;
-    hipEvent_t b = take_event(ctx);
-    if (!b) return;
-    (void)hipEventRecord(b, ctx->stream);
-    ctx->spans[phase].push_back({a, b});
-  }
-};
-
 constexpr int kResFields = 16;
 
 }  // namespace
@@ -302,13 +277,13 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   uint64_t* res = ctx->res.as<uint64_t>();
   hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) {
-    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
-    if (t->desc.kind == HJ3D_CHAIN)
-      e = radix_probe_applicable(ctx, t, probe->n)
-              ? radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
-              : chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
-    else
-      e = nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n)) {
+      e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);  // times its own kernels
+    } else {
+      PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+      e = (t->desc.kind == HJ3D_CHAIN) ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
+                                       : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    }
   }
   // remember what an overflow check needs
   ctx->res_flags = flags;

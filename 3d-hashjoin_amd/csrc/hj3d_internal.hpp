@@ -140,6 +140,33 @@ enum ScratchSlot {
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
                            uint64_t set0 = ~0ull);
 
+// Event spans on the context stream when timing is enabled (hj3d_ctx_timer): a PhaseTimer
+// brackets whatever is enqueued during its lifetime.
+inline hipEvent_t take_event(hj3d_ctx* ctx) {
+  if (ctx->pool_used == ctx->event_pool.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    ctx->event_pool.push_back(ev);
+  }
+  return ctx->event_pool[ctx->pool_used++];
+}
+
+struct PhaseTimer {
+  hj3d_ctx* ctx;
+  int phase;
+  hipEvent_t a = nullptr;
+  PhaseTimer(hj3d_ctx* c, int p) : ctx(c), phase(p) {
+    if (ctx->timing && p >= 0 && (a = take_event(ctx))) (void)hipEventRecord(a, ctx->stream);
+  }
+  ~PhaseTimer() {
+    if (!a) return;
+    hipEvent_t b = take_event(ctx);
+    if (!b) return;
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->spans[phase].push_back({a, b});
+  }
+};
+
 inline RelView view_of(const hj3d_rel& r) {
   RelView v;
   v.base = static_cast<const char*>(r.base);

@@ -378,8 +378,9 @@ Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
 }
 
 // Partition `r` into (hash, row) pairs by bucket range; ps[0..P] = partition starts.
+// t_hist / t_scatter: timer phases of the two streaming kernels (-1: untimed).
 hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
-                           uint32_t* ps, hipStream_t s) {
+                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1) {
   hipError_t e;
   const uint64_t hn = uint64_t(pl.P) * pl.ntiles + 1;
   if ((e = ctx->scratch[kScrPHist].ensure(hn * sizeof(uint32_t))) != hipSuccess) return e;
@@ -387,11 +388,13 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   const RelView v = view_of(r);
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
   if (r.n) {
+    PhaseTimer tm(ctx, t_hist);
     hipLaunchKernelGGL(k_rp_hist, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
                        pl.ntiles, hist);
   }
   if ((e = exclusive_scan_u32(ctx, hist, hist, hn - 1, s)) != hipSuccess) return e;
   if (r.n) {
+    PhaseTimer tm(ctx, t_scatter);
     hipLaunchKernelGGL(k_rp_scatter, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
                        pl.ntiles, hist, out);
   }
@@ -489,11 +492,12 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
-  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
+  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s, HJ3D_T_HIST, HJ3D_T_SCATTER)) != hipSuccess) return e;
   const bool unique = flags & HJ3D_PROBE_UNIQUE;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   uint2* o = static_cast<uint2*>(out);
+  PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);  // for the non-unique EMIT form this includes the offset scan
   if (!emit) {
     if (unique) launch_probe<true, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);
     else launch_probe<false, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);

@@ -24,7 +24,7 @@ HJ3D_OK, HJ3D_EINVAL, HJ3D_ENOMEM, HJ3D_EDEVICE, HJ3D_EUNSUPPORTED, HJ3D_EOVERFL
 HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM = 0x1, 0x2, 0x4, 0x8
-T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION = range(4)
+T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN = 1, 2
 
 MASK64 = (1 << 64) - 1

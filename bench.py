@@ -26,6 +26,12 @@ SEED_R, SEED_S = 0x5eed0001, 0x5eed0002
 PEAK_HBM_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def latest_pmc():
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
+    return files[-1] if files else ""
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -38,7 +44,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=20_000_000, help="S tuples probed by the CPU baseline")
     p.add_argument("--cpu-reps", type=int, default=3)
-    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_probe.json"))
+    p.add_argument("--pmc-json", default=latest_pmc(), help="PMC summary (scripts/pmc_summary.py) for roofline.traffic")
     p.add_argument("--json-out", default=None)
     return p.parse_args()
 
@@ -186,8 +192,12 @@ def main():
 
     build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    kern_ms, kern_n = ctx.timer(hj3d.T_PROBE_KERNEL)
-    kern_avg = kern_ms / max(kern_n, 1)
+    # per-kernel averages over the timed steps (HIP events on the engine's stream)
+    kern_avg = {}
+    for name, ph in (("k_rp_probe", hj3d.T_PROBE_KERNEL), ("k_rp_scatter", hj3d.T_SCATTER),
+                     ("k_rp_hist", hj3d.T_HIST)):
+        ms, cnt = ctx.timer(ph)
+        kern_avg[name] = ms / cnt if cnt else None
     # verification step (outside the timed region): the same step once more with the
     # order-independent output checksums folded in, compared below with the expected pair set
     state["ck"] = True
@@ -212,7 +222,7 @@ def main():
         build_ms = hdist.allreduce_max(build_ms, dev)
         probe_ms = hdist.allreduce_max(probe_ms, dev)
         wall_ms = hdist.allreduce_max(wall_ms, dev)
-        kern_avg = hdist.allreduce_max(kern_avg, dev)
+        kern_avg = {k: (hdist.allreduce_max(v, dev) if v is not None else None) for k, v in kern_avg.items()}
     else:
         exp_sum, exp_xor = exp_local[:4], exp_local[4]
         got_sum, got_xor = got_local, res.xor_h
@@ -224,21 +234,44 @@ def main():
             torch.distributed.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel (the probe kernel) ----
-    # algorithmic bytes per launch: probe tuple read + one 8-B table entry + 8-B output pair
+    # ---- roofline of the dominant kernel ----
+    # Algorithmic bytes per launch (DESIGN.md "Kernels"), n = probe tuples of this rank:
+    #   k_rp_hist     n * 12                      read the S tuple (AoS {k,a,b}; the key's line)
+    #   k_rp_scatter  n * (12 + 8)                read the S tuple, write the (hash,row) pair
+    #   k_rp_probe    n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
+    #                                                  the table slices (entries + directory) once
+    # (N > 1: the probe side is the received pair array, 8 B per tuple, and has no hist/scatter
+    # tuple read beyond it.)
+    n = probe_n_local
     tuple_bytes = 12 if world == 1 else 8
-    bytes_per_probe = tuple_bytes + 8 + (8 if emit else 0)
-    alg_bytes = probe_n_local * bytes_per_probe
-    achieved = alg_bytes / (kern_avg * 1e-3) / 1e9
+    alg = {
+        "k_rp_hist": n * tuple_bytes,
+        "k_rp_scatter": n * (tuple_bytes + 8),
+        "k_rp_probe": n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4,
+    }
+    kernels = {}
+    for k, ms in kern_avg.items():
+        if ms:
+            kernels[k] = {"avg_ms": ms, "alg_bytes": alg[k], "achieved_GBs": alg[k] / (ms * 1e-3) / 1e9,
+                          "frac": alg[k] / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
+    dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     traffic = None
-    if world == 1 and os.path.exists(args.pmc_json):
+    pmc = None
+    if world == 1 and args.pmc_json and os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("nS") == nS and pm.get("emit") == emit:
-                traffic = pm.get("traffic_bytes_per_launch")
+            if pm.get("nS") == nS and pm.get("nR") == nR and pm.get("emit") == emit:
+                pmc = pm.get("kernels", {})
+                traffic = (pmc.get(dom) or {}).get("traffic_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    if pmc:
+        for k in kernels:
+            if k in pmc:
+                kernels[k]["traffic"] = pmc[k].get("traffic_bytes_per_launch")
+    # the whole probe phase (hist + scan + scatter + probe) against the plan's 28 B per probe
+    phase_alg = n * (tuple_bytes + 8 + (8 if emit else 0))
 
     line = {
         "metric": METRIC,
@@ -262,9 +295,13 @@ def main():
         "probe_ms": probe_ms,
         "join_tuples_per_s": nS * world / ((build_ms + probe_ms) * 1e-3),
         "roofline": {
-            "bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-            "kernel": "k_chain_probe", "kernel_avg_ms": kern_avg, "alg_bytes_per_launch": alg_bytes,
+            "bound": "hbm", "achieved": kernels[dom]["achieved_GBs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+            "frac": kernels[dom]["frac"], "traffic": traffic,
+            "kernel": dom, "kernel_avg_ms": kernels[dom]["avg_ms"], "alg_bytes_per_launch": kernels[dom]["alg_bytes"],
+            "kernels": kernels,
+            "probe_phase": {"ms": probe_ms, "alg_bytes": phase_alg,
+                            "achieved_GBs": phase_alg / (probe_ms * 1e-3) / 1e9,
+                            "frac": phase_alg / (probe_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
         },
         "counters": {"c_top": got_sum[0], "c_htProbeCmp": cmps},
         "verified_bit_exact": verified,

@@ -141,7 +141,15 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
  * (phase ids below). hj3d_ctx_timer reads (synchronously) the summed milliseconds and the
  * number of recorded intervals since the last reset. */
-enum { HJ3D_T_BUILD = 0, HJ3D_T_PROBE = 1, HJ3D_T_PROBE_KERNEL = 2, HJ3D_T_PARTITION = 3, HJ3D_T_NTIMERS = 4 };
+enum {
+  HJ3D_T_BUILD = 0,         /* hj3d_build, whole call */
+  HJ3D_T_PROBE = 1,         /* hj3d_probe / hj3d_probe2, whole call */
+  HJ3D_T_PROBE_KERNEL = 2,  /* the join-probe kernel launches only (radix path: k_rp_probe) */
+  HJ3D_T_PARTITION = 3,     /* hj3d_partition (multi-GPU exchange partitioner) */
+  HJ3D_T_SCATTER = 4,       /* radix probe path: probe-side partition scatter kernel */
+  HJ3D_T_HIST = 5,          /* radix probe path: probe-side partition histogram kernel */
+  HJ3D_T_NTIMERS = 6
+};
 hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
 hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count);
 hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx);
