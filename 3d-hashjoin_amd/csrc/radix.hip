@@ -23,6 +23,7 @@ namespace {
 constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
 constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
+static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr int kJBlock = 1024;                    // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
@@ -77,6 +78,8 @@ __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
 // partition order (128 KB), then written out so that consecutive lanes store consecutive
 // addresses of one partition's run: ~16 elements = one 128-B line per partition and tile at
 // the probe's fan-out, instead of one scattered 8-B store per tuple.
+// Persistent over tiles (one workgroup per CU, LDS-bound): the next tile's keys are loaded
+// before the current tile's write-out, so the CU's reads and writes overlap.
 __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
                                                         uint2* __restrict__ out) {
@@ -84,38 +87,53 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
   __shared__ uint32_t loc[kMaxParts];   // local counts, then local run starts
   __shared__ uint32_t gb[kMaxParts];    // global run start of each partition for this tile
   __shared__ uint32_t wsum[kPBlock / kWave];
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
-    loc[p] = 0;
-    gb[p] = offs[uint64_t(p) * ntiles + blockIdx.x];
-  }
-  const uint64_t base = uint64_t(blockIdx.x) * kPTile;
-  uint32_t h[kPRounds], rk[kPRounds];
+  uint32_t h[kPRounds];
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
   }
-  __syncthreads();
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
+      loc[p] = 0;
+      gb[p] = offs[uint64_t(p) * ntiles + tile];
+    }
+    const uint64_t base = uint64_t(tile) * kPTile;
+    uint32_t rk[kPRounds];
+    __syncthreads();
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-    h[j] = murmur32(h[j]);
-    const uint32_t bl = fm.mod(h[j]) - lo;
-    rk[j] = (i < r.n && bl < nbl) ? atomicAdd(&loc[fw.div(bl)], 1u) : kInvalid;
-  }
-  __syncthreads();
-  const uint32_t m = lds_excl_scan(loc, P, wsum);  // staged tuples of this tile
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+      h[j] = murmur32(h[j]);
+      const uint32_t bl = fm.mod(h[j]) - lo;
+      if (i < r.n && bl < nbl) {  // rk = partition << 14 | rank in the tile's run (kPTile = 2^14)
+        const uint32_t part = fw.div(bl);
+        rk[j] = (part << 14) | atomicAdd(&loc[part], 1u);
+      } else {
+        rk[j] = kInvalid;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = lds_excl_scan(loc, P, wsum);  // staged tuples of this tile
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    if (rk[j] == kInvalid) continue;
-    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-    stage[loc[fw.div(fm.mod(h[j]) - lo)] + rk[j]] = make_uint2(h[j], r.row(i));
-  }
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
-    const uint2 e = stage[k];
-    const uint32_t p = fw.div(fm.mod(e.x) - lo);
-    out[gb[p] + (k - loc[p])] = e;
+    for (int j = 0; j < kPRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], r.row(i));
+    }
+    __syncthreads();
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
+      h[j] = i < r.n ? r.key(i) : 0u;
+    }
+    for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
+      const uint2 e = stage[k];
+      const uint32_t p = fw.div(fm.mod(e.x) - lo);
+      out[gb[p] + (k - loc[p])] = e;
+    }
+    __syncthreads();
   }
 }
 
@@ -299,6 +317,19 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ 
   uint32_t* loff = lds;
   const uint32_t ent_word = (nbs + 2) & ~1u;
   uint2* lent = reinterpret_cast<uint2*>(lds + ent_word);
+  const uint32_t s0 = ps[p], s1 = ps[p + 1];
+  const uint32_t len = s1 - s0;
+  const uint32_t q0 = s0 + uint32_t(uint64_t(len) * sp / splits);
+  const uint32_t q1 = s0 + uint32_t(uint64_t(len) * (sp + 1) / splits);
+  constexpr uint32_t kStep = kJBlock * kItems;
+  // software pipeline: the first batch of pairs is in flight while the slice is staged, and
+  // batch k+1 while batch k is probed
+  uint64_t cur[kItems];
+#pragma unroll
+  for (int j = 0; j < kItems; ++j) {
+    const uint32_t i = q0 + j * kJBlock + threadIdx.x;
+    cur[j] = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
+  }
   if (fits) {  // stage the slice: every thread keeps kStage loads in flight before writing LDS
     constexpr int kStage = 8;
     for (uint32_t k0 = threadIdx.x; k0 <= nbs; k0 += kJBlock * kStage) {
@@ -331,33 +362,31 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ 
     }
   }
   __syncthreads();
-  const uint32_t s0 = ps[p], s1 = ps[p + 1];
-  const uint32_t len = s1 - s0;
-  const uint32_t q0 = s0 + uint32_t(uint64_t(len) * sp / splits);
-  const uint32_t q1 = s0 + uint32_t(uint64_t(len) * (sp + 1) / splits);
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t base = q0; base < q1; base += kJBlock * kItems) {
-    uint2 pr[kItems];
+  for (uint32_t base = q0; base < q1; base += kStep) {
+    uint64_t nxt[kItems];
+    const uint32_t nbase = base + kStep;
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
-      const uint32_t i = base + j * kJBlock + threadIdx.x;
-      const uint64_t v = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
-      pr[j] = make_uint2(uint32_t(v), uint32_t(v >> 32));
+      const uint32_t i = nbase + j * kJBlock + threadIdx.x;
+      nxt[j] = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
     }
 #pragma unroll
     for (int j = 0; j < kItems; ++j) {
       const uint32_t i = base + j * kJBlock + threadIdx.x;
       if (i >= q1) continue;
-      const uint32_t h = pr[j].x;
+      const uint32_t h = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
       const uint32_t bl = fm.mod(h) - lo - b0;
       if (fits) {
         const uint32_t s = loff[bl];
-        probe_bucket<UNIQUE, MODE, CK>(h, pr[j].y, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(h, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
       } else {
         const uint32_t s = off[b0 + bl];
-        probe_bucket<UNIQUE, MODE, CK>(h, pr[j].y, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(h, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
       }
     }
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
   }
   if (MODE != kWrite) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
 }
@@ -395,7 +424,8 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   if ((e = exclusive_scan_u32(ctx, hist, hist, hn - 1, s)) != hipSuccess) return e;
   if (r.n) {
     PhaseTimer tm(ctx, t_scatter);
-    hipLaunchKernelGGL(k_rp_scatter, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
+    const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
+    hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
                        pl.ntiles, hist, out);
   }
   if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
