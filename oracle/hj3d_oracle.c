@@ -298,7 +298,9 @@ static void rsv_erase(reservoir* r) { /* Reservoir::erase: release every chunk *
 }
 
 static inline uint32_t key_of(const orc_rel* r, const uint32_t* t) { return t[r->key]; }
-static inline uint64_t row_of(const orc_rel* r, const uint32_t* t) { return (uint64_t)(t - r->base) / r->stride; }
+static inline uint64_t row_of(const orc_rel* r, const uint32_t* t) {
+  return r->row == ORC_ROW_IMPLICIT ? (uint64_t)(t - r->base) / r->stride : t[r->row];
+}
 
 static void stats_init(orc_stats* s, uint64_t nb) {
   memset(s, 0, sizeof(*s));
@@ -392,7 +394,7 @@ int orc_chain_plan(const orc_rel* build, const orc_rel* probe, uint64_t num_buck
         ++c;
         if (it->hash == hv && pk == key_of(build, it->data)) {
           ++cnt;
-          if (agg) agg2(&res->out, i, row_of(build, it->data));
+          if (agg) agg2(&res->out, row_of(probe, t), row_of(build, it->data));
           if (unique) break;
         }
       }
@@ -520,13 +522,13 @@ int orc_nested_plan(const orc_rel* build, const orc_rel* probe, uint64_t num_buc
       ++cnt;
       if (unnest) { /* AlgUnnestHt::step (algebra.hh:510-541): main datum, then sub-chain */
         ++un;
-        if (agg) agg2(&res->out, i, row_of(build, m->data));
+        if (agg) agg2(&res->out, row_of(probe, t), row_of(build, m->data));
         for (const snode* s = m->sub; s; s = s->next) {
           ++un;
-          if (agg) agg2(&res->out, i, row_of(build, s->data));
+          if (agg) agg2(&res->out, row_of(probe, t), row_of(build, s->data));
         }
       } else if (agg) {
-        agg2(&res->out, i, row_of(build, m->data));
+        agg2(&res->out, row_of(probe, t), row_of(build, m->data));
       }
     }
     const double t2 = now_ns();
@@ -585,7 +587,7 @@ int orc_exp4_plan(const orc_rel* R, const orc_rel* S, const orc_rel* T, uint64_t
           const snode* ssub = ms->sub;
           for (;;) {
             ++u2;
-            if (agg) agg3(&res->out, i, row_of(S, sd), row_of(T, td));
+            if (agg) agg3(&res->out, row_of(R, R->base + i * R->stride), row_of(S, sd), row_of(T, td));
             if (!ssub) break;
             sd = ssub->data; ssub = ssub->next;
           }
@@ -630,7 +632,7 @@ int orc_exp4_plan(const orc_rel* R, const orc_rel* S, const orc_rel* T, uint64_t
             ++crt;
             if (b->hash == hv && k == key_of(T, b->data)) {
               ++prt;
-              if (agg) agg3(&res->out, i, row_of(S, a->data), row_of(T, b->data));
+              if (agg) agg3(&res->out, row_of(R, r), row_of(S, a->data), row_of(T, b->data));
             }
           }
         }

@@ -21,11 +21,16 @@ extern "C" {
 
 typedef struct { uint32_t mt[624]; int idx; } orc_mt19937;
 
+#define ORC_ROW_IMPLICIT 0xFFFFFFFFu
+
 typedef struct {
   const uint32_t* base;
   uint64_t n;
   uint32_t stride; /* u32 words per tuple */
   uint32_t key;    /* word index of the join attribute */
+  uint32_t row;    /* word index of an explicit row id (exchanged (key,row) pairs of the
+                      multi-GPU path), or ORC_ROW_IMPLICIT: row id = index in the relation */
+  uint32_t pad;
 } orc_rel;
 
 typedef struct {

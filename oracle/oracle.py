@@ -22,7 +22,11 @@ LIB_PATH = os.path.join(HERE, "liboracle.so")
 
 
 class _Rel(C.Structure):
-    _fields_ = [("base", C.c_void_p), ("n", C.c_uint64), ("stride", C.c_uint32), ("key", C.c_uint32)]
+    _fields_ = [("base", C.c_void_p), ("n", C.c_uint64), ("stride", C.c_uint32), ("key", C.c_uint32),
+                ("row", C.c_uint32), ("pad", C.c_uint32)]
+
+
+ROW_IMPLICIT = 0xFFFFFFFF
 
 
 class _Stats(C.Structure):
@@ -134,9 +138,10 @@ def tuples2(k: np.ndarray, a: np.ndarray) -> np.ndarray:
     return t
 
 
-def _rel(t: np.ndarray, key: int) -> _Rel:
+def _rel(t: np.ndarray, key: int, row: int | None = None) -> _Rel:
     t = np.ascontiguousarray(t, dtype=np.uint32)
-    return _Rel(_ptr(t) if t.size else None, t.shape[0], t.shape[1], key)
+    return _Rel(_ptr(t) if t.size else None, t.shape[0], t.shape[1], key,
+                ROW_IMPLICIT if row is None else row, 0)
 
 
 @dataclass
@@ -157,10 +162,10 @@ def _agg(a: _Agg) -> dict:
     return {f: getattr(a, f) for f, _ in _Agg._fields_}
 
 
-def _plan(fn, build, bkey, probe, pkey, nb, flag, agg, min_ms, min_reps) -> PlanResult:
+def _plan(fn, build, bkey, probe, pkey, nb, flag, agg, min_ms, min_reps, brow=None, prow=None) -> PlanResult:
     build = np.ascontiguousarray(build, dtype=np.uint32)
     probe = np.ascontiguousarray(probe, dtype=np.uint32)
-    rb, rp = _rel(build, bkey), _rel(probe, pkey)
+    rb, rp = _rel(build, bkey, brow), _rel(probe, pkey, prow)
     res = _PlanRes()
     rc = fn(C.byref(rb), C.byref(rp), nb, int(flag), int(agg), float(min_ms), int(min_reps), C.byref(res))
     if rc != 0:
@@ -170,14 +175,17 @@ def _plan(fn, build, bkey, probe, pkey, nb, flag, agg, min_ms, min_reps) -> Plan
                       res.build_ns, res.probe_ns, st, _agg(res.out))
 
 
-def chain_plan(build, bkey, probe, pkey, nb, unique, agg=True, min_ms=0.0, min_reps=1) -> PlanResult:
-    """Chaining build on `build` (key word `bkey`), probe with `probe` (ht_chaining.hh + algebra.hh:555-672)."""
-    return _plan(lib().orc_chain_plan, build, bkey, probe, pkey, nb, unique, agg, min_ms, min_reps)
+def chain_plan(build, bkey, probe, pkey, nb, unique, agg=True, min_ms=0.0, min_reps=1, brow=None,
+               prow=None) -> PlanResult:
+    """Chaining build on `build` (key word `bkey`), probe with `probe` (ht_chaining.hh + algebra.hh:555-672).
+    brow / prow: word of an explicit row id (exchanged (key,row) pairs), else row = index."""
+    return _plan(lib().orc_chain_plan, build, bkey, probe, pkey, nb, unique, agg, min_ms, min_reps, brow, prow)
 
 
-def nested_plan(build, bkey, probe, pkey, nb, unnest, agg=True, min_ms=0.0, min_reps=1) -> PlanResult:
+def nested_plan(build, bkey, probe, pkey, nb, unnest, agg=True, min_ms=0.0, min_reps=1, brow=None,
+                prow=None) -> PlanResult:
     """Nested (3D) build/probe(/unnest) (ht_nested.hh + algebra.hh:362-552)."""
-    return _plan(lib().orc_nested_plan, build, bkey, probe, pkey, nb, unnest, agg, min_ms, min_reps)
+    return _plan(lib().orc_nested_plan, build, bkey, probe, pkey, nb, unnest, agg, min_ms, min_reps, brow, prow)
 
 
 def exp4_plan(R, S, T, nb, nested, agg=True, min_ms=0.0, min_reps=1) -> dict:

@@ -1,0 +1,129 @@
+"""Multi-GPU path rehearsed on CPU: world size 2, gloo backend.
+
+Each rank holds a contiguous slice of R and S (global row ids), partitions it by bucket range
+exactly as hj3d_partition does (owner = bucket * P / NB, stable; restated here in numpy),
+exchanges (key, row) pairs with hj3d.dist.exchange (all_to_all), and joins its received pairs
+with the oracle over the full bucket space (only its own buckets are populated). The per-rank
+counters, all-reduced with hj3d.dist, must equal the single-table oracle on the whole relations:
+join cardinality, c_htProbeCmp, unnest counts, output checksums and the table statistics.
+That is the property the device path relies on (bucket ranges keep per-bucket chain order when
+received segments are concatenated in source-rank order)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+WORLD = 2
+
+
+def murmur32(x):
+    x = x.astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    x = (x * np.uint32(0x85EBCA6B)).astype(np.uint32)
+    x ^= x >> np.uint32(13)
+    x = (x * np.uint32(0xC2B2AE35)).astype(np.uint32)
+    x ^= x >> np.uint32(16)
+    return x
+
+
+def partition(keys, rows, nb, parts):
+    """(key, row) pairs grouped by owner(bucket) = bucket * parts // nb, stable (hj3d_partition)."""
+    b = (murmur32(keys).astype(np.uint64) % np.uint64(nb)).astype(np.uint64)
+    owner = (b * np.uint64(parts) // np.uint64(nb)).astype(np.int64)
+    order = np.argsort(owner, kind="stable")
+    pairs = np.stack([keys[order], rows[order]], axis=1).astype(np.uint32)
+    counts = np.bincount(owner, minlength=parts).astype(np.int64)
+    return pairs, counts
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, port, case, q):
+    import torch
+    import torch.distributed as dist
+    import hj3d
+    from hj3d import dist as hdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        nR, nS, skew = case
+        Rk, Sa, _ = O.gen_exp1(nR, nS, skew, 1.0, 0)
+        dv = O.num_distinct(Sa)
+        out = {}
+        for plan, (bkeys, pkeys, nb) in {
+            "Csr": (Rk, Sa, nR), "Nsr": (Rk, Sa, nR), "Crs": (Sa, Rk, dv), "Nrs": (Sa, Rk, dv),
+        }.items():
+            # contiguous slices of the build and probe relations, global row ids
+            def local(keys):
+                n = len(keys)
+                lo, hi = rank * n // WORLD, (rank + 1) * n // WORLD
+                return keys[lo:hi], np.arange(lo, hi, dtype=np.uint32)
+
+            recv = []
+            for keys in (bkeys, pkeys):
+                k, r = local(keys)
+                pairs, counts = partition(k, r, nb, WORLD)
+                got = hdist.exchange(torch.from_numpy(pairs.view(np.int32)), torch.from_numpy(counts))
+                recv.append(got.numpy().view(np.uint32))
+            # the owned bucket range agrees with hj3d_part_range
+            lo, hi = hj3d.part_range(nb, WORLD, rank)
+            bk = murmur32(recv[0][:, 0]).astype(np.uint64) % np.uint64(nb)
+            assert ((bk >= lo) & (bk < hi)).all()
+            if plan.startswith("C"):
+                e = O.chain_plan(recv[0], 0, recv[1], 0, nb, plan == "Csr", brow=1, prow=1)
+            else:
+                e = O.nested_plan(recv[0], 0, recv[1], 0, nb, True, brow=1, prow=1)
+            st = e.stats
+            owned = hi - lo
+            sums = [e.c_probe, e.c_cmp, e.c_unnest, e.c_top, e.out["n"], e.out["sum_a"], e.out["sum_b"],
+                    e.out["sum_h"], st["empty"] - (nb - owned), st["entries"], st["distinct"], st["cc0_sum"],
+                    st["cc1_sum"], st["cc1_cnt"]]
+            tot = hdist.allreduce_sum_u64(sums, "cpu")
+            x = hdist.allreduce_xor_u64(e.out["xor_h"], "cpu")
+            mx = hdist.allreduce_max(float(st["cc0_max"]), "cpu")
+            out[plan] = (tot, x, int(mx))
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("case", [(4096, 32768, False), (2048, 65536, True)], ids=["uniform", "zipf"])
+def test_bucket_range_exchange_world2(case):
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, case, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nR, nS, skew = case
+    Rk, Sa, _ = O.gen_exp1(nR, nS, skew, 1.0, 0)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    dv = O.num_distinct(Sa)
+    exp = {"Csr": O.chain_plan(R, 0, S, 1, nR, True), "Nsr": O.nested_plan(R, 0, S, 1, nR, True),
+           "Crs": O.chain_plan(S, 1, R, 0, dv, False), "Nrs": O.nested_plan(S, 1, R, 0, dv, True)}
+    for plan, e in exp.items():
+        tot, x, mx = res[0][plan]
+        assert res[1][plan] == res[0][plan]  # every rank sees the same reduced values
+        st = e.stats
+        want = [e.c_probe, e.c_cmp, e.c_unnest, e.c_top, e.out["n"], e.out["sum_a"], e.out["sum_b"], e.out["sum_h"],
+                st["empty"], st["entries"], st["distinct"], st["cc0_sum"], st["cc1_sum"], st["cc1_cnt"]]
+        assert tot == [v & ((1 << 64) - 1) for v in want], plan
+        assert x == e.out["xor_h"] and mx == st["cc0_max"], plan
