@@ -371,6 +371,15 @@ hj3d_status hj3d_gen_fk(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride
   return from_hip(ctx, gen_fk(tuples, n, stride, key_off, row_base, fk_max, seed, ctx->stream), "hj3d_gen_fk");
 }
 
+hj3d_status hj3d_gen_zipf(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
+                          uint64_t row_base, uint32_t fk_max, double theta, uint64_t seed) {
+  if (!ctx || (n && !tuples) || stride == 0 || (stride & 3) || (key_off & 3) || key_off + 4 > stride || fk_max == 0 ||
+      !(theta > 0.0) || theta > 10.0)
+    return HJ3D_EINVAL;
+  return from_hip(ctx, gen_zipf(tuples, n, stride, key_off, row_base, fk_max, theta, seed, ctx->stream),
+                  "hj3d_gen_zipf");
+}
+
 hj3d_status hj3d_expected_fk_join(hj3d_ctx* ctx, const hj3d_rel* build, const hj3d_rel* probe, uint64_t n_keys,
                                   int swap, void* res_dev) {
   if (!ctx || !rel_ok(build) || !rel_ok(probe) || !res_dev) return HJ3D_EINVAL;

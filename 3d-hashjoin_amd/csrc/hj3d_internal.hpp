@@ -120,6 +120,8 @@ hipError_t gen_keys(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
                     uint64_t n_keys, uint64_t seed, hipStream_t s);
 hipError_t gen_fk(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,
                   uint64_t seed, hipStream_t s);
+hipError_t gen_zipf(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,
+                    double theta, uint64_t seed, hipStream_t s);
 hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel& probe, uint64_t n_keys,
                             bool swap, void* res, hipStream_t s);
 hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n_keys, uint64_t seed, bool swap,

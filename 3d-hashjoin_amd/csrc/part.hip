@@ -151,6 +151,55 @@ __global__ __launch_bounds__(kBlock) void k_gen_fk(char* __restrict__ t, uint64_
   }
 }
 
+// Zipf(theta) over {1..n} by rejection-inversion (Hoermann & Derflinger 1996, the method of the
+// reference's util/zipf_distribution.hh), driven by a counter-based RNG of the global row so
+// every row's value is independent of the launch geometry. Not the reference's sequential
+// mt19937 stream: full-size runs check parity through the key/FK pair identity instead.
+struct ZipfRI {
+  double q, n, hx1, hn, s;
+  __host__ __device__ static double helper1(double x) {
+    return fabs(x) > 1e-8 ? log1p(x) / x : 1.0 - x * (0.5 - x * (1.0 / 3.0 - 0.25 * x));
+  }
+  __host__ __device__ static double helper2(double x) {
+    return fabs(x) > 1e-8 ? expm1(x) / x : 1.0 + x * 0.5 * (1.0 + x * (1.0 / 3.0) * (1.0 + 0.25 * x));
+  }
+  __host__ __device__ double h(double x) const { return exp(-q * log(x)); }
+  __host__ __device__ double H(double x) const {
+    const double lx = log(x);
+    return helper2((1.0 - q) * lx) * lx;
+  }
+  __host__ __device__ double Hinv(double x) const {
+    double t = x * (1.0 - q);
+    if (t < -1.0) t = -1.0;
+    return exp(helper1(t) * x);
+  }
+  static ZipfRI make(uint32_t n, double theta) {
+    ZipfRI z;
+    z.q = theta;
+    z.n = double(n);
+    z.hx1 = z.H(1.5) - 1.0;
+    z.hn = z.H(z.n + 0.5);
+    z.s = 2.0 - z.Hinv(z.H(2.5) - z.h(2.0));
+    return z;
+  }
+  __device__ uint32_t sample(uint64_t key) const {
+    for (uint64_t c = 0;; ++c) {
+      const double u01 = double(mix64(key ^ (c * 0x9E3779B97F4A7C15ull + 0x632BE59BD9B4E019ull)) >> 11) * 0x1.0p-53;
+      const double u = hn + u01 * (hx1 - hn);
+      const double x = Hinv(u);
+      double k = floor(x + 0.5);
+      k = k < 1.0 ? 1.0 : (k > n ? n : k);
+      if (k - x <= s || u >= H(k + 0.5) - h(k)) return uint32_t(k);
+    }
+  }
+};
+
+__global__ __launch_bounds__(kBlock) void k_gen_zipf(char* __restrict__ t, uint64_t n, uint32_t stride,
+                                                     uint32_t key_off, uint64_t row_base, ZipfRI z, uint64_t seed) {
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock)
+    *reinterpret_cast<uint32_t*>(t + i * stride + key_off) = z.sample(mix64((row_base + i) ^ seed)) - 1u;
+}
+
 __global__ __launch_bounds__(kBlock) void k_inv(RelView b, uint64_t n_keys, uint32_t* __restrict__ inv) {
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < b.n; i += uint64_t(gridDim.x) * kBlock) {
     const uint32_t k = b.key(i);
@@ -239,6 +288,16 @@ hipError_t gen_fk(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, u
   const unsigned g = unsigned(n / kBlock + 1 < 4096 ? n / kBlock + 1 : 4096);
   hipLaunchKernelGGL(k_gen_fk, dim3(g), dim3(kBlock), 0, s, static_cast<char*>(tuples), n, stride, key_off, row_base,
                      fk_max, seed);
+  return hipGetLastError();
+}
+
+hipError_t gen_zipf(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,
+                    double theta, uint64_t seed, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  const ZipfRI z = ZipfRI::make(fk_max, theta);
+  const unsigned g = unsigned(n / kBlock + 1 < 4096 ? n / kBlock + 1 : 4096);
+  hipLaunchKernelGGL(k_gen_zipf, dim3(g), dim3(kBlock), 0, s, static_cast<char*>(tuples), n, stride, key_off,
+                     row_base, z, seed);
   return hipGetLastError();
 }
 

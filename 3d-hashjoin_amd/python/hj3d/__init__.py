@@ -107,6 +107,7 @@ def lib():
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_gen_keys": (st, [p, p, u64, u32, u32, u64, u64, u64]),
         "hj3d_gen_fk": (st, [p, p, u64, u32, u32, u64, u32, u64]),
+        "hj3d_gen_zipf": (st, [p, p, u64, u32, u32, u64, u32, C.c_double, u64]),
         "hj3d_expected_fk_join": (st, [p, R, R, u64, i32, p]),
         "hj3d_expected_fk_join_gen": (st, [p, R, u64, u64, i32, p]),
     }
@@ -276,6 +277,11 @@ class Context:
     def gen_fk(self, tensor, key_word: int, row_base: int, fk_max: int, seed: int):
         self._check(lib().hj3d_gen_fk(self.h, tensor.data_ptr(), tensor.shape[0], 4 * tensor.shape[1],
                                       4 * key_word, row_base, fk_max, seed), "hj3d_gen_fk")
+
+    def gen_zipf(self, tensor, key_word: int, row_base: int, fk_max: int, theta: float, seed: int):
+        """key column ~ Zipf(theta) over [0, fk_max), value 0 the most frequent (config C)."""
+        self._check(lib().hj3d_gen_zipf(self.h, tensor.data_ptr(), tensor.shape[0], 4 * tensor.shape[1],
+                                        4 * key_word, row_base, fk_max, float(theta), seed), "hj3d_gen_zipf")
 
     def expected_fk_join(self, build: Rel, probe: Rel, n_keys: int, swap: bool = False) -> dict:
         torch = _torch()

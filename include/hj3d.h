@@ -207,6 +207,11 @@ hj3d_status hj3d_gen_keys(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t 
                           uint64_t row_base, uint64_t n_keys, uint64_t seed);
 hj3d_status hj3d_gen_fk(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t stride, uint32_t key_off,
                         uint64_t row_base, uint32_t fk_max, uint64_t seed);
+/* S.a ~ Zipf(theta) over [0, fk_max) (value 0 the most frequent; P(v) ~ (v+1)^-theta), sampled by
+ * rejection-inversion (the method of util/zipf_distribution.hh) from a counter-based RNG of the
+ * global row id: config C (nested table, Zipf 0.8 duplicates) at full size. */
+hj3d_status hj3d_gen_zipf(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t stride, uint32_t key_off,
+                          uint64_t row_base, uint32_t fk_max, double theta, uint64_t seed);
 /* Expected key/FK join aggregates WITHOUT a hash table (full-size verification of the
  * key/FK plans): `build` holds unique keys in [0, n_keys); every probe tuple's partner row is
  * inv[key], inv being the inverse of the build key column. Accumulates {n_out, sum_a, sum_b,

@@ -91,3 +91,79 @@ def test_device_generator_cmps_vs_oracle(ctx, nR, nS):
         assert (got["c_probe"], got["c_cmp"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_top), plan
         assert got["out"] == e.out, plan
         assert got["stats"]["cc0_max"] == e.stats["cc0_max"] and got["stats"]["empty"] == e.stats["empty"]
+
+
+# ---- config C: nested table on a non-unique build side with Zipf(0.8) duplicates ----
+
+def make_zipf(ctx, nR, nS, theta=0.8):
+    import torch
+    R = torch.zeros((nR, 3), dtype=torch.int32, device="cuda")
+    S = torch.zeros((nS, 3), dtype=torch.int32, device="cuda")
+    ctx.gen_keys(R, 0, 0, nR, SEED_R)
+    ctx.gen_keys(S, 0, 0, 0, 0)
+    ctx.gen_zipf(S, 1, 0, nR, theta, SEED_S)
+    return R, S
+
+
+def test_device_zipf_matches_pmf(ctx):
+    """The device sampler's value frequencies follow P(v) ~ (v+1)^-theta (5-sigma bounds)."""
+    import torch
+    nR, nS, theta = 1_000_000, 10_000_000, 0.8
+    _, S = make_zipf(ctx, nR, nS, theta)
+    a = S[:, 1]
+    assert int(a.min()) >= 0 and int(a.max()) < nR
+    cnt = torch.bincount(a.long(), minlength=nR)[:16].cpu().numpy().astype(np.float64)
+    w = np.arange(1, nR + 1, dtype=np.float64) ** -theta
+    p = w[:16] / w.sum()
+    sd = np.sqrt(nS * p * (1 - p))
+    assert (np.abs(cnt - nS * p) < 5 * sd + 1).all(), (cnt, nS * p)
+
+
+@pytest.mark.parametrize("theta", [0.8, 1.0])
+def test_config_c_zipf_plans_vs_oracle(ctx, theta):
+    """Config C plans (Nrs, NrsNU, Nsr, Crs) on device-generated Zipf FKs at 1e6 / 1e7: every
+    counter equal to the oracle's on the same (downloaded) relations."""
+    import hj3d
+    nR, nS = 1_000_000, 10_000_000
+    R, S = make_zipf(ctx, nR, nS, theta)
+    Rh = R.cpu().numpy().view(np.uint32)
+    Sh = S.cpu().numpy().view(np.uint32)
+    dv = O.num_distinct(Sh[:, 1])
+    cases = {
+        "Nrs": (dv, lambda: O.nested_plan(Sh, 1, Rh, 0, dv, True)),
+        "NrsNU": (dv, lambda: O.nested_plan(Sh, 1, Rh, 0, dv, False)),
+        "Nsr": (nR, lambda: O.nested_plan(Rh, 0, Sh, 1, nR, True)),
+        "Crs": (dv, lambda: O.chain_plan(Sh, 1, Rh, 0, dv, False)),
+    }
+    for plan, (nb, fn) in cases.items():
+        e = fn()
+        got = hj3d.exp1_plan(ctx, plan, R, S, nb)
+        assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
+            (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), plan
+        assert got["out"] == e.out, plan
+        for k in ("empty", "distinct", "cc0_max", "cc0_sum", "cc1_cnt"):
+            assert got["stats"][k] == e.stats[k], (plan, k)
+
+
+def test_config_c_full_size(ctx):
+    """Config C at full size (|R| = 1e7, |S| = 1e8, Zipf 0.8): Nrs (3D table on S.a, probe R,
+    unnest) and NrsNU produce exactly the key/FK pair set; the hot key's ~1% of S is one
+    sub-list expanded by whole workgroups."""
+    import hj3d
+    nR, nS = 10_000_000, 100_000_000
+    R, S = make_zipf(ctx, nR, nS, 0.8)
+    exp_rs = ctx.expected_fk_join(hj3d.Rel(R, 0), hj3d.Rel(S, 1), nR, swap=True)
+    exp_sr = ctx.expected_fk_join(hj3d.Rel(R, 0), hj3d.Rel(S, 1), nR)
+    assert exp_rs["n"] == nS
+    t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nR)
+    t.build(hj3d.Rel(S, 1))
+    st = t.stats()
+    dv = st["distinct"]
+    assert st["entries"] == nS and dv < nR
+    got = hj3d.exp1_plan(ctx, "Nrs", R, S, dv)
+    assert got["c_probe"] == dv and got["c_unnest"] == nS and got["c_top"] == nS
+    assert {k: got["out"][k] for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h")} == exp_rs
+    nu = hj3d.exp1_plan(ctx, "NrsNU", R, S, dv, stats=False)
+    assert nu["c_probe"] == dv and nu["c_top"] == dv and nu["c_cmp"] == got["c_cmp"]
+    sr = hj3d.exp1_plan(ctx, "Nsr", R, S, nR, stats=False)
+    assert {k: sr["out"][k] for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h")} == exp_sr
