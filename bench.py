@@ -46,6 +46,11 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--pmc-json", default=latest_pmc(), help="PMC summary (scripts/pmc_summary.py) for roofline.traffic")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--workload", default="B", choices=["B", "C", "E"],
+                   help="B: the headline key/FK chaining join (default); C: 3D table on Zipf(0.8) S.a, Nrs plan; "
+                        "E: experiment-4 deferred unnesting (Ndu)")
+    p.add_argument("--theta", type=float, default=0.8, help="config C Zipf parameter")
+    p.add_argument("--log2R", type=int, default=23, help="config E: |R| = 2^log2R")
     return p.parse_args()
 
 
@@ -99,6 +104,8 @@ def cpu_baseline(R_host, S_host, nb, reps):
 
 def main():
     args = parse()
+    if args.workload != "B":
+        return main_single_config(args)
     import torch
     import hj3d
 
@@ -322,6 +329,155 @@ def main():
         torch.distributed.destroy_process_group()
     if not verified:
         raise SystemExit("verification failed: join output differs from the expected key/FK pair set")
+
+
+def _events(torch, n):
+    return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
+
+
+def _emit(line, args):
+    s = json.dumps(line)
+    print(s, flush=True)
+    if args.json_out:
+        with open(args.json_out, "w") as f:
+            f.write(s + "\n")
+
+
+def main_single_config(args):
+    """Configs C and E of BASELINE.json (one GPU). Same protocol as config B: inputs generated and
+    resident before timing, W warmup steps, K timed steps bracketed by synchronize, one
+    verification step after timing (bit-exact identities)."""
+    import torch
+    import hj3d
+
+    if int(os.environ.get("WORLD_SIZE", "1")) != 1 or args.gpus != 1:
+        raise SystemExit("--workload C/E run on one GPU")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(0)
+    ctx = hj3d.Context(0)
+    ctx.timing(True)
+
+    if args.workload == "C":
+        nR, nS = args.nR, args.nS
+        R = torch.zeros((nR, 3), dtype=torch.int32, device=dev)
+        S = torch.zeros((nS, 3), dtype=torch.int32, device=dev)
+        ctx.gen_keys(R, 0, 0, nR, SEED_R)
+        ctx.gen_keys(S, 0, 0, 0, 0)
+        ctx.gen_zipf(S, 1, 0, nR, args.theta, SEED_S)
+        relR, relS = hj3d.Rel(R, key_word=0), hj3d.Rel(S, key_word=1)
+        probe_t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nR)
+        probe_t.build(relS)
+        dv = probe_t.stats()["distinct"]  # NB = #dv(S.a) as the reference sizes Nrs (main_experiment1.cc:1001)
+        del probe_t
+        table = hj3d.Table(ctx, hj3d.HJ3D_NESTED, dv)
+        table.reserve(nS)
+        out = torch.empty((nS, 2), dtype=torch.int32, device=dev)
+        state = {"ck": False}
+
+        def step(ev):
+            ev[0].record()
+            table.build(relS)
+            ev[1].record()
+            ctx.probe(table, relR, unnest=True, out=out, fetch=False, checksum=state["ck"])
+            ev[2].record()
+
+        n_probe, n_build = nR, nS
+    else:
+        import numpy as np
+        log2R, a, A, b, B = args.log2R, 3, 4, 2, 2
+        nR = 1 << log2R
+        nc, ne = nR >> a, nR >> b
+        rng = np.random.default_rng(5489)
+        common = np.repeat(np.arange(nc, dtype=np.uint32), A)
+        exS = np.repeat(np.arange(nc, nc + ne, dtype=np.uint32), B)
+        exT = np.repeat(np.arange(nc + ne, nc + 2 * ne, dtype=np.uint32), B)
+        Sa = np.concatenate([rng.permutation(common), rng.permutation(exS)])
+        Ta = np.concatenate([rng.permutation(common), rng.permutation(exT)])
+
+        def rel2(a_col):
+            t = np.zeros((len(a_col), 2), dtype=np.uint32)
+            t[:, 0] = np.arange(len(a_col), dtype=np.uint32)
+            t[:, 1] = a_col
+            return torch.from_numpy(t.view(np.int32)).to(dev)
+
+        R = rel2(np.zeros(nR, dtype=np.uint32))
+        S, T = rel2(Sa), rel2(Ta)
+        nb = nc + ne  # numFkCommon + numFkExclusive (main_experiment4.cc:855)
+        ts, tt = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb), hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+        ts.reserve(len(Sa))
+        tt.reserve(len(Ta))
+        relR, relS, relT = hj3d.Rel(R, key_word=0), hj3d.Rel(S, key_word=1), hj3d.Rel(T, key_word=1)
+        state = {}
+
+        def step(ev):
+            ev[0].record()
+            ts.build(relS)
+            tt.build(relT)
+            ev[1].record()
+            ctx.probe2(ts, tt, relR, fetch=False)
+            ev[2].record()
+
+        n_probe, n_build = nR, len(Sa) + len(Ta)
+
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        step(_events(torch, 3))
+    torch.cuda.synchronize()
+    evs = [_events(torch, 3) for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e in evs:
+        step(e)
+    torch.cuda.synchronize()
+    wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
+    build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+
+    if args.workload == "C":
+        state["ck"] = True
+        step(_events(torch, 3))
+        torch.cuda.synchronize()
+        r = ctx.probe_result()
+        exp = ctx.expected_fk_join(relR, relS, nR, swap=True)
+        got = {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_h": r.sum_h, "xor_h": r.xor_h}
+        verified = got == exp and r.n_out == nS and r.n_matched == dv
+        n_out = r.n_out
+        counters = {"c_htProbe": r.n_matched, "c_htProbeCmp": r.n_cmps, "c_unnest": r.n_out, "numDvSa": dv}
+        # phase bytes (SURVEY §8d): build 20 B/tuple; probe 20 B/probe + unnest 12 B/output
+        build_bytes, probe_bytes = nS * 20, nR * 20 + n_out * 12
+        workload = f"exp1 plan Nrs (3D table on S.a, probe R, unnest), |R|={nR} |S|={nS}, S.a ~ Zipf({args.theta})"
+        data = f"synthetic (device-generated: R.k = seeded permutation, S.a ~ Zipf(theta={args.theta}) over [0,|R|))"
+        metric, unit, value = ("unnested output tuples/s (probe + unnest phase), config C", "output tuples/s",
+                               n_out / (probe_ms * 1e-3))
+    else:
+        r = ctx.probe2_result()
+        nc, A = nR >> 3, 4
+        verified = (r["c_top"] == nc * A * A and r["c_unnest_1"] == nc * A and r["c_probe_rt"] == nc
+                    and r["c_probe_rs"] == nc + (nR >> 2))
+        counters = {k: r[k] for k in ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp", "c_unnest_1",
+                                      "c_unnest_2", "c_top")}
+        n_out = r["c_top"]
+        build_bytes = n_build * 16  # 8-B {k,a} tuple read + 8 B (key,row) written
+        probe_bytes = nR * 8 * 2 + n_out * 12
+        workload = (f"exp4 plan Ndu (two 3D probes, deferred unnesting), log2R={args.log2R} alpha=3 A=4 beta=2 B=2, "
+                    f"|S|=|T|={len(Sa)}")
+        data = "synthetic (numpy: R.k = iota, S.a/T.a = shuffled FK blocks as main_experiment4.cc:517-575)"
+        metric, unit, value = ("probe tuples/s (R through both 3D probes + deferred unnest), config E",
+                               "probe tuples/s", nR / (probe_ms * 1e-3))
+    line = {
+        "metric": metric, "value": value, "unit": unit, "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+        "data": data, "config": {"workload": workload, "parallelism": "single GPU"},
+        "build_ms": build_ms, "probe_ms": probe_ms,
+        "roofline": {"bound": "hbm", "kernel": "phase (build / probe)", "unit": "GB/s", "peak": PEAK_HBM_GBS,
+                     "achieved": probe_bytes / (probe_ms * 1e-3) / 1e9,
+                     "frac": probe_bytes / (probe_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                     "build_achieved": build_bytes / (build_ms * 1e-3) / 1e9},
+        "counters": counters, "verified_bit_exact": verified, "cpu_baseline": None,
+    }
+    _emit(line, args)
+    if not verified:
+        raise SystemExit("verification failed")
 
 
 if __name__ == "__main__":
