@@ -64,6 +64,7 @@ struct hj3d_ctx {
   bool timing = false;
   bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
   uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
+  bool nested_radix = false;      // HJ3D_OPT_NESTED_RADIX
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;
@@ -90,9 +91,10 @@ namespace hj3d {
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
 hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
 // sort.hip: stable LSD radix sort of (key,val) u32 pairs on key bits [0, bits). Result lands in
-// (k0,v0); (k1,v1) is a same-size scratch double buffer.
+// (k0,v0); (k1,v1) is a same-size scratch double buffer. With in_alt, an odd number of passes
+// leaves the result in (k1,v1) and sets *in_alt instead of copying it back.
 hipError_t radix_sort_pairs(hj3d_ctx* ctx, uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint64_t n,
-                            int bits, hipStream_t s);
+                            int bits, hipStream_t s, bool* in_alt = nullptr);
 // radix.hip: partitioned (LDS-slice) build / probe of the chaining table
 bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
 hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
@@ -106,6 +108,10 @@ hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
                        uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // nested.hip
 hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+// nested_radix.hip: nested build from the radix-partitioned bucket CSR (large inputs);
+// hipErrorNotSupported when a bucket holds too many distinct keys (use nested_build).
+bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n);
+hipError_t nested_build_radix(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                         uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // exp4.hip

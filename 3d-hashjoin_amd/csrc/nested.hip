@@ -24,18 +24,22 @@ constexpr uint32_t kInline = 32;
 
 __device__ __forceinline__ bool is_head(const uint32_t* hk, uint64_t e) { return e == 0 || hk[e] != hk[e - 1]; }
 
+// (key, row) pairs in input order; counts[0] += owned tuples, counts[3] = max key (sort width)
 __global__ __launch_bounds__(kBlock) void k_extract(RelView r, FastMod fm, uint32_t lo, uint32_t nbl,
                                                     uint32_t* __restrict__ hk, uint32_t* __restrict__ rv,
                                                     uint64_t* __restrict__ counts) {
-  uint64_t owned = 0;
+  uint64_t owned = 0, mx = 0;
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock) {
-    const uint32_t h = murmur32(r.key(i));
-    hk[i] = h;
+    const uint32_t k = r.key(i);
+    hk[i] = k;
     rv[i] = r.row(i);
-    owned += (fm.mod(h) - lo) < nbl;
+    owned += (fm.mod(murmur32(k)) - lo) < nbl;
+    mx = k > mx ? k : mx;
   }
   uint64_t v[1] = {owned};
   block_flush<1, 0>(v, counts);  // counts[0] = stored tuples (HtStatistics::_numEntries)
+  const uint64_t wm = wave_max(mx);
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(reinterpret_cast<unsigned long long*>(counts + 3), wm);
 }
 
 __global__ __launch_bounds__(kBlock) void k_heads(const uint32_t* __restrict__ hk, uint64_t n, uint32_t* __restrict__ x) {
@@ -43,16 +47,18 @@ __global__ __launch_bounds__(kBlock) void k_heads(const uint32_t* __restrict__ h
     x[e] = is_head(hk, e) ? 1u : 0u;
 }
 
-// One main record per run: hash and run start; first_row initialised for the min pass.
+// One main record per run of equal keys: hash, run start and (rows ascending within the run,
+// i.e. implicit row ids and a stable sort) first_row; else first_row is left to k_run_min.
 __global__ __launch_bounds__(kBlock) void k_runs(const uint32_t* __restrict__ hk, uint64_t n,
-                                                 const uint32_t* __restrict__ x, uint32_t* __restrict__ mh,
+                                                 const uint32_t* __restrict__ x, const uint32_t* __restrict__ rows,
+                                                 bool rows_sorted, uint32_t* __restrict__ mh,
                                                  uint32_t* __restrict__ msub, uint32_t* __restrict__ mfirst) {
   for (uint64_t e = uint64_t(blockIdx.x) * kBlock + threadIdx.x; e < n; e += uint64_t(gridDim.x) * kBlock) {
     if (!is_head(hk, e)) continue;
     const uint32_t m = x[e];
-    mh[m] = hk[e];
+    mh[m] = murmur32(hk[e]);
     msub[m] = uint32_t(e);
-    mfirst[m] = kInvalid;
+    mfirst[m] = rows_sorted ? rows[e] : kInvalid;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) msub[x[n]] = uint32_t(n);
 }
@@ -214,17 +220,18 @@ __global__ __launch_bounds__(kBlock) void k_nested_probe(RelView r, FastMod fm, 
   block_flush<kProbeFields, 1>(acc, res);
 }
 
-// Heavy matches: one workgroup expands one (probe row, main) pair at a time.
+// Heavy matches (> kInline rows): every workgroup takes a share of every queued (probe row,
+// main) pair, so one Zipf hot key is expanded by the whole chip, not by one workgroup.
 __global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict__ heavy,
                                                          const uint64_t* __restrict__ nheavy,
                                                          const uint4* __restrict__ mains,
                                                          const uint32_t* __restrict__ sub, uint64_t* __restrict__ res) {
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint64_t nh = *nheavy;
-  for (uint64_t q = blockIdx.x; q < nh; q += gridDim.x) {
+  for (uint64_t q = 0; q < nh; ++q) {
     const Heavy hv = heavy[q];
     const uint4 M = mains[hv.main_idx];
-    for (uint32_t k = threadIdx.x; k < M.w; k += kBlock) {
+    for (uint32_t k = blockIdx.x * kBlock + threadIdx.x; k < M.w; k += gridDim.x * kBlock) {
       const uint32_t br = sub[M.z + k];
       acc[4] += hv.probe_row;
       acc[5] += br;
@@ -236,34 +243,99 @@ __global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict
   block_flush<kProbeFields, 1>(acc, res);
 }
 
-// Load-balanced unnest with materialisation: output position p belongs to the probe tuple i
-// with ooff[i] <= p < ooff[i+1]; each thread takes a run of kSpan consecutive positions and
-// binary-searches its first probe tuple once.
-constexpr int kSpan = 8;
-__global__ __launch_bounds__(kBlock) void k_expand_write(RelView r, const uint64_t* __restrict__ ooff,
+// Materialised unnest. Output slots of probe tuple i are [ooff[i], ooff[i+1]) (exclusive scan of
+// the per-probe output counts). One workgroup per 256 consecutive probe tuples: their light
+// outputs (<= kHeavyOut per probe) are enumerated p = 0..L-1 by consecutive threads, each
+// finding its probe tuple by a binary search over the 256 local offsets in LDS, so the stores
+// of a workgroup form one (nearly) contiguous, coalesced range. Heavier probes are queued and
+// written by k_expand_heavy_write with all workgroups.
+constexpr uint32_t kHeavyOut = 8192;
+
+__global__ __launch_bounds__(kBlock) void k_expand_light(RelView r, const uint64_t* __restrict__ ooff,
                                                          const uint32_t* __restrict__ mid,
                                                          const uint4* __restrict__ mains,
                                                          const uint32_t* __restrict__ sub, uint2* __restrict__ out,
-                                                         uint64_t out_cap, uint64_t* __restrict__ res) {
+                                                         uint64_t out_cap, uint32_t* __restrict__ heavy,
+                                                         uint32_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
+  __shared__ uint32_t loff[kBlock + 1];
+  __shared__ uint32_t lz[kBlock];
+  __shared__ uint32_t lpr[kBlock];
+  __shared__ uint64_t lpos[kBlock];
+  __shared__ uint32_t wsum[kBlock / kWave];
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t total = ooff[r.n];
-  const uint64_t lim = total < out_cap ? total : out_cap;
-  for (uint64_t p0 = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) * kSpan; p0 < lim;
-       p0 += uint64_t(gridDim.x) * kBlock * kSpan) {
-    uint64_t lo = 0, hi = r.n;  // largest i with ooff[i] <= p0
-    while (hi - lo > 1) {
-      const uint64_t md = (lo + hi) >> 1;
-      if (ooff[md] <= p0) lo = md; else hi = md;
+  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  uint32_t c = 0, z = 0, pr = 0;
+  uint64_t pos = 0;
+  if (i < r.n) {
+    pos = ooff[i];
+    const uint64_t cc = ooff[i + 1] - pos;
+    if (cc) {
+      z = mains[mid[i]].z;
+      pr = r.row(i);
+      if (cc > kHeavyOut) heavy[atomicAdd(nheavy, 1u)] = uint32_t(i);
+      else c = uint32_t(cc);
     }
-    uint64_t i = lo;
-    for (uint64_t p = p0; p < p0 + kSpan && p < lim; ++p) {
-      while (ooff[i + 1] <= p) ++i;
-      const uint4 M = mains[mid[i]];
-      const uint32_t pr = r.row(i), br = sub[M.z + uint32_t(p - ooff[i])];
-      out[p] = make_uint2(pr, br);
-      acc[4] += pr;
+  }
+  // block exclusive scan of the light counts
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t wt;
+  const uint32_t wx = wave_excl_scan(c, &wt);
+  if (lane == 63) wsum[wid] = wx + c;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    const uint32_t v = wsum[w];
+    if (w < wid) pre += v;
+    tot += v;
+  }
+  loff[threadIdx.x] = pre + wx;
+  if (threadIdx.x == 0) loff[kBlock] = tot;
+  lz[threadIdx.x] = z;
+  lpr[threadIdx.x] = pr;
+  lpos[threadIdx.x] = pos;
+  __syncthreads();
+  for (uint32_t p = threadIdx.x; p < tot; p += kBlock) {
+    uint32_t lo = 0, hi = kBlock;  // largest t with loff[t] <= p (probes with c = 0 are skipped over)
+#pragma unroll
+    for (int step = 0; step < 8; ++step) {
+      const uint32_t md = (lo + hi) >> 1;
+      if (loff[md] <= p) lo = md; else hi = md;
+    }
+    const uint32_t q = p - loff[lo];
+    const uint32_t br = sub[lz[lo] + q], prow = lpr[lo];
+    const uint64_t o = lpos[lo] + q;
+    if (o < out_cap) __builtin_nontemporal_store((uint64_t(br) << 32) | prow, reinterpret_cast<uint64_t*>(out + o));
+    acc[4] += prow;
+    acc[5] += br;
+    const uint64_t ph = pair_hash(prow, br);
+    acc[7] += ph;
+    acc[8] ^= ph;
+  }
+  block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+}
+
+__global__ __launch_bounds__(kBlock) void k_expand_heavy_write(RelView r, const uint64_t* __restrict__ ooff,
+                                                               const uint32_t* __restrict__ mid,
+                                                               const uint4* __restrict__ mains,
+                                                               const uint32_t* __restrict__ sub,
+                                                               const uint32_t* __restrict__ heavy,
+                                                               const uint32_t* __restrict__ nheavy,
+                                                               uint2* __restrict__ out, uint64_t out_cap,
+                                                               uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint32_t nh = *nheavy;
+  for (uint32_t q = 0; q < nh; ++q) {
+    const uint32_t i = heavy[q];
+    const uint64_t base = ooff[i], cnt = ooff[i + 1] - base;
+    const uint32_t z = mains[mid[i]].z, prow = r.row(i);
+    for (uint64_t k = uint64_t(blockIdx.x) * kBlock + threadIdx.x; k < cnt; k += uint64_t(gridDim.x) * kBlock) {
+      const uint32_t br = sub[z + k];
+      if (base + k < out_cap)
+        __builtin_nontemporal_store((uint64_t(br) << 32) | prow, reinterpret_cast<uint64_t*>(out + base + k));
+      acc[4] += prow;
       acc[5] += br;
-      const uint64_t ph = pair_hash(pr, br);
+      const uint64_t ph = pair_hash(prow, br);
       acc[7] += ph;
       acc[8] ^= ph;
     }
@@ -302,11 +374,22 @@ hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStre
   const unsigned g = grid_for(ctx, nn, kBlock * 4);
   if (n) {
     hipLaunchKernelGGL(k_extract, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, hk, rows, counts);
-    if ((e = radix_sort_pairs(ctx, hk, rows, k1, v1, n, 32, s)) != hipSuccess) return e;
+    // sort by key, only over its significant bits (equal keys <=> equal hashes: murmur32 is a bijection)
+    uint64_t maxkey = 0;
+    if ((e = hipMemcpyAsync(&maxkey, counts + 3, sizeof(maxkey), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+    const int bits = maxkey ? 32 - __builtin_clz(uint32_t(maxkey)) : 0;
+    bool alt = false;
+    if ((e = radix_sort_pairs(ctx, hk, rows, k1, v1, n, bits, s, &alt)) != hipSuccess) return e;
+    if (alt) {  // odd number of passes: the sorted keys are in k1, the sorted rows in v1
+      hk = k1;
+      if ((e = hipMemcpyAsync(rows, v1, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+    }
+    const bool rows_sorted = r.row_off == HJ3D_ROW_IMPLICIT;  // stable sort keeps input (= row) order
     hipLaunchKernelGGL(k_heads, dim3(g), dim3(kBlock), 0, s, hk, n, x);
     if ((e = exclusive_scan_u32(ctx, x, x, n, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_runs, dim3(g), dim3(kBlock), 0, s, hk, n, x, mh, msub, mfirst);
-    hipLaunchKernelGGL(k_run_min, dim3(g), dim3(kBlock), 0, s, hk, rows, n, x, mfirst);
+    hipLaunchKernelGGL(k_runs, dim3(g), dim3(kBlock), 0, s, hk, n, x, rows, rows_sorted, mh, msub, mfirst);
+    if (!rows_sorted) hipLaunchKernelGGL(k_run_min, dim3(g), dim3(kBlock), 0, s, hk, rows, n, x, mfirst);
     hipLaunchKernelGGL(k_main_count, dim3(g), dim3(kBlock), 0, s, mh, x, n, t->fm, lo, nbl, off, mslot);
   }
   if ((e = exclusive_scan_u32(ctx, off, off, nbl, s)) != hipSuccess) return e;
@@ -350,17 +433,26 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
     hipLaunchKernelGGL(k_expand_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, heavy, nheavy, mains, sub, res);
     return hipGetLastError();
   }
-  // materialised unnest: count -> scan -> load-balanced expansion
+  // materialised unnest: count -> scan -> expansion (light: per 256 probes; heavy: all workgroups)
+  const uint32_t nblk = uint32_t((r.n + kBlock - 1) / kBlock);
   if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrC].ensure(r.n * sizeof(uint32_t) + 16)) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrC].ensure(2 * r.n * sizeof(uint32_t) + 64)) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblk) * kProbeFields * sizeof(uint64_t))) != hipSuccess) return e;
   uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
-  uint32_t* mid = ctx->scratch[kScrC].as<uint32_t>();
+  uint32_t* nheavy = ctx->scratch[kScrC].as<uint32_t>();
+  uint32_t* mid = nheavy + 16;
+  uint32_t* heavy = mid + r.n;
+  uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_nested_probe<kCountUN>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub,
                      nullptr, 0, cnt, mid, nullptr, nullptr, res);
   if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_expand_write, dim3(ctx->num_cus * 8), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, o, out_cap,
-                     res);
-  return hipGetLastError();
+  hipLaunchKernelGGL(k_expand_light, dim3(nblk), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, o, out_cap, heavy,
+                     nheavy, partials);
+  hipLaunchKernelGGL(k_expand_heavy_write, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, heavy,
+                     nheavy, o, out_cap, res);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  return reduce_partials(partials, nblk, kProbeFields, 1, res, s);
 }
 
 }  // namespace hj3d

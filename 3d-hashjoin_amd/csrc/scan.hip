@@ -133,25 +133,43 @@ hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t
   return hipGetLastError();
 }
 
-// Column sums of per-block partials: one wave per field (nf <= 16), xor for the last nxor.
+// Column sums of per-block partials (nf <= 16 fields per row, xor for the last nxor): every
+// thread folds whole rows (coalesced 8*nf-byte reads), then one block reduction per field.
 __global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __restrict__ part, uint32_t nblocks, int nf,
                                                           int nxor, uint64_t* __restrict__ res, uint64_t set0) {
-  const int f = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (f >= nf) return;
-  const bool x = f >= nf - nxor;
-  uint64_t acc = 0;
-  for (uint32_t b = lane; b < nblocks; b += 64) {
-    const uint64_t v = part[uint64_t(b) * nf + f];
-    acc = x ? (acc ^ v) : (acc + v);
-  }
+  __shared__ uint64_t red[16][16];
+  uint64_t acc[16];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const uint64_t w = __shfl_xor(acc, o, kWave);
-    acc = x ? (acc ^ w) : (acc + w);
+  for (int f = 0; f < 16; ++f) acc[f] = 0;
+  for (uint32_t b = threadIdx.x; b < nblocks; b += 1024) {
+#pragma unroll
+    for (int f = 0; f < 16; ++f) {
+      if (f >= nf) break;
+      const uint64_t v = part[uint64_t(b) * nf + f];
+      acc[f] = f >= nf - nxor ? (acc[f] ^ v) : (acc[f] + v);
+    }
   }
-  if (lane == 0) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#pragma unroll
+  for (int f = 0; f < 16; ++f) {
+    if (f >= nf) break;
+    const bool x = f >= nf - nxor;
+    uint64_t a = acc[f];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint64_t w = __shfl_xor(a, o, kWave);
+      a = x ? (a ^ w) : (a + w);
+    }
+    if (lane == 0) red[wid][f] = a;
+  }
+  __syncthreads();
+  if (threadIdx.x < nf) {
+    const int f = threadIdx.x;
+    const bool x = f >= nf - nxor;
+    uint64_t a = 0;
+    for (int w = 0; w < 16; ++w) a = x ? (a ^ red[w][f]) : (a + red[w][f]);
     if (f == 0 && set0 != ~0ull) res[0] = set0;
-    else res[f] = x ? (res[f] ^ acc) : (res[f] + acc);
+    else res[f] = x ? (res[f] ^ a) : (res[f] + a);
   }
 }
 

@@ -25,7 +25,7 @@ HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM = 0x1, 0x2, 0x4, 0x8
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
-OPT_FORCE_DIRECT, OPT_RADIX_MIN = 1, 2
+OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX = 1, 2, 3
 
 MASK64 = (1 << 64) - 1
 
@@ -218,6 +218,10 @@ class Context:
     def force_direct(self, on: bool = True):
         """A/B switch: chaining build/probe without the radix-partitioned kernels."""
         self.set_option(OPT_FORCE_DIRECT, int(on))
+
+    def nested_radix(self, on: bool = True):
+        """Nested builds from the radix-partitioned bucket CSR instead of the key sort."""
+        self.set_option(OPT_NESTED_RADIX, int(on))
 
     def radix_min(self, n: int):
         """Smallest probe side (tuples) that takes the radix-partitioned chaining kernels."""

@@ -135,7 +135,11 @@ enum {
   HJ3D_OPT_FORCE_DIRECT = 1,
   /* HJ3D_OPT_RADIX_MIN (tuples): probes of at least this many tuples (builds of at least 1/16 of
    * it) use the radix-partitioned kernels; default 2^20. */
-  HJ3D_OPT_RADIX_MIN = 2
+  HJ3D_OPT_RADIX_MIN = 2,
+  /* HJ3D_OPT_NESTED_RADIX (0/1, default 0): build nested tables from the radix-partitioned bucket
+   * CSR with per-bucket key grouping instead of the key sort (faster at low bucket fill, slower
+   * under heavy skew). */
+  HJ3D_OPT_NESTED_RADIX = 3
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

@@ -101,10 +101,11 @@ def test_exp1_both_chaining_paths(ctx, name, g, path):
     dR, dS = dev(R), dev(S)
     if path == "radix":
         ctx.radix_min(0)
+        ctx.nested_radix(True)
     else:
         ctx.force_direct(True)
     try:
-        for plan in ("Csr", "CsrUU", "Crs"):
+        for plan in ("Csr", "CsrUU", "Crs", "Nsr", "Nrs", "NrsNU"):
             nb = hj3d.num_buckets_exp1(plan, len(R), g["numDvSa"], b)
             ref = g["plans"][plan]
             got = hj3d.exp1_plan(ctx, plan, dR, dS, nb)
@@ -115,11 +116,44 @@ def test_exp1_both_chaining_paths(ctx, name, g, path):
             out = torch.zeros((cap, 2), dtype=torch.int32, device="cuda")
             got = hj3d.exp1_plan(ctx, plan, dR, dS, nb, out=out, stats=False)
             host = out.cpu().numpy().view(np.uint32)
-            host = host[host[:, 1] != 0xFFFFFFFF][: ref["out"]["n"]] if plan == "Csr" else host[: ref["out"]["n"]]
+            dense = plan in ("Csr", "NrsNU")  # one slot per probe tuple
+            host = host[host[:, 1] != 0xFFFFFFFF][: ref["out"]["n"]] if dense else host[: ref["out"]["n"]]
             assert host_checksums(host) == ref["out"], plan
     finally:
         ctx.radix_min(1 << 20)
         ctx.force_direct(False)
+        ctx.nested_radix(False)
+
+
+@pytest.mark.parametrize("nb", [64, 2000, 50000])
+@pytest.mark.parametrize("path", ["radix", "direct"])
+def test_nested_many_keys_per_bucket(ctx, nb, path):
+    """Nested build with many distinct keys per bucket: ~1560 (the radix grouping gives up after
+    64 keys in one bucket and the sort-based build takes over), ~50 (many grouping passes) and
+    ~2 per bucket; every counter and the output equal the oracle's."""
+    import hj3d
+    rng = np.random.default_rng(nb)
+    nR, nS = 100_000, 400_000
+    Rk = rng.permutation(nR).astype(np.uint32)
+    Sa = rng.integers(0, nR, nS, dtype=np.uint32)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    if path == "radix":
+        ctx.radix_min(0)
+        ctx.nested_radix(True)
+    else:
+        ctx.force_direct(True)
+    try:
+        for plan, e in (("Nsr", O.nested_plan(R, 0, S, 1, nb, True)), ("Nrs", O.nested_plan(S, 1, R, 0, nb, True))):
+            got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb)
+            assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
+                (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), plan
+            assert got["out"] == e.out, plan
+            assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, plan
+    finally:
+        ctx.radix_min(1 << 20)
+        ctx.force_direct(False)
+        ctx.nested_radix(False)
 
 
 @pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
