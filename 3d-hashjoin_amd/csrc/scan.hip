@@ -133,39 +133,37 @@ hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t
   return hipGetLastError();
 }
 
-// Column sums of per-block partials (nf <= 16 fields per row, xor for the last nxor): every
-// thread folds whole rows (coalesced 8*nf-byte reads), then one block reduction per field.
-__global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __restrict__ part, uint32_t nblocks, int nf,
-                                                          int nxor, uint64_t* __restrict__ res, uint64_t set0) {
-  __shared__ uint64_t red[16][16];
-  uint64_t acc[16];
+// Column sums of per-block partials (NF u64 fields per row, xor for the last NXOR): every
+// thread folds whole rows (coalesced 8*NF-byte reads), then one block reduction per field.
+template <int NF, int NXOR>
+__global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __restrict__ part, uint32_t nblocks,
+                                                          uint64_t* __restrict__ res, uint64_t set0) {
+  __shared__ uint64_t red[16][NF];
+  uint64_t acc[NF];
 #pragma unroll
-  for (int f = 0; f < 16; ++f) acc[f] = 0;
+  for (int f = 0; f < NF; ++f) acc[f] = 0;
   for (uint32_t b = threadIdx.x; b < nblocks; b += 1024) {
 #pragma unroll
-    for (int f = 0; f < 16; ++f) {
-      if (f >= nf) break;
-      const uint64_t v = part[uint64_t(b) * nf + f];
-      acc[f] = f >= nf - nxor ? (acc[f] ^ v) : (acc[f] + v);
+    for (int f = 0; f < NF; ++f) {
+      const uint64_t v = part[uint64_t(b) * NF + f];
+      acc[f] = f >= NF - NXOR ? (acc[f] ^ v) : (acc[f] + v);
     }
   }
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #pragma unroll
-  for (int f = 0; f < 16; ++f) {
-    if (f >= nf) break;
-    const bool x = f >= nf - nxor;
+  for (int f = 0; f < NF; ++f) {
     uint64_t a = acc[f];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       const uint64_t w = __shfl_xor(a, o, kWave);
-      a = x ? (a ^ w) : (a + w);
+      a = f >= NF - NXOR ? (a ^ w) : (a + w);
     }
     if (lane == 0) red[wid][f] = a;
   }
   __syncthreads();
-  if (threadIdx.x < nf) {
-    const int f = threadIdx.x;
-    const bool x = f >= nf - nxor;
+  const int f = int(threadIdx.x);
+  if (f < NF) {
+    const bool x = f >= NF - NXOR;
     uint64_t a = 0;
     for (int w = 0; w < 16; ++w) a = x ? (a ^ red[w][f]) : (a + red[w][f]);
     if (f == 0 && set0 != ~0ull) res[0] = set0;
@@ -177,8 +175,8 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __rest
 
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
                            uint64_t set0) {
-  if (nf > 16) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_reduce_partials, dim3(1), dim3(1024), 0, s, partials, nblocks, nf, nxor, res, set0);
+  if (nf != kProbeFields || nxor != 1) return hipErrorInvalidValue;  // the one shape in use
+  hipLaunchKernelGGL((k_reduce_partials<kProbeFields, 1>), dim3(1), dim3(1024), 0, s, partials, nblocks, res, set0);
   return hipGetLastError();
 }
 
