@@ -15,6 +15,8 @@
 //              CSR layout of chain.hip (probe-side partitioning is independent of the build).
 // Bucket ranges keep the reference's per-bucket semantics (chain order, comparison counts,
 // statistics) untouched: every counter is computed per bucket exactly as in chain.hip.
+#include <cmath>
+
 #include "hj3d_internal.hpp"
 
 namespace hj3d {
@@ -28,7 +30,6 @@ constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partiti
 constexpr int kJBlock = 1024;                    // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
 constexpr uint32_t kProbeLdsWords = 36864;       // 144 KB LDS table slice per probe workgroup
-constexpr int kItems = 12;
 constexpr uint32_t kSortedMax = 32;             // buckets up to this size are kept sorted by row
 
 struct FastDiv {  // exact floor(a / d) for u32 a, 1 <= d < 2^32
@@ -299,96 +300,236 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
   }
 }
 
-// One workgroup per (partition, split): the partition's table slice is staged in LDS when it
-// fits (always, for key builds of uniform size), else the workgroup reads it through L2.
+// Copy the table slice of buckets [b0, b0 + nbs) (directory rebased to 0 + entries) into LDS;
+// every thread keeps kStage loads in flight before writing LDS.
+__device__ __forceinline__ void stage_slice(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
+                                            uint32_t nbs, uint32_t e0, uint32_t ne, uint32_t* loff, uint2* lent) {
+  constexpr int kStage = 8;
+  for (uint32_t k0 = threadIdx.x; k0 <= nbs; k0 += kJBlock * kStage) {
+    uint32_t v[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      v[u] = k <= nbs ? off[b0 + k] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      if (k <= nbs) loff[k] = v[u] - e0;
+    }
+  }
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(lent);
+  for (uint32_t k0 = threadIdx.x; k0 < ne; k0 += kJBlock * kStage) {
+    uint64_t v[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      v[u] = k < ne ? src[k] : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      if (k < ne) dst[k] = v[u];
+    }
+  }
+}
+
+// ---- single-pass probe-side partitioning (no histogram pass) ----
+// Persistent workgroup g owns, for every partition p, a private region of `cap` pairs
+// (region[(g * P + p) * cap ...]) and its fill cursor in LDS. Per tile: rank per partition (LDS
+// atomics), stage in partition order (LDS), write each partition's run at the cursor. A run that
+// does not fit (skewed probe keys) goes to the overflow list, probed by k_probe_ovf. S is read
+// once instead of twice (histogram + scatter).
+__global__ __launch_bounds__(kPBlock) void k_rp_part1(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                      uint32_t P, uint32_t ntiles, uint32_t cap,
+                                                      uint2* __restrict__ region, uint32_t* __restrict__ counts,
+                                                      uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
+  __shared__ uint2 stage[kPTile];
+  __shared__ uint32_t loc[kMaxParts + 1];  // tile counts, then tile-local run starts (loc[P] = tile size)
+  __shared__ uint32_t cur[kMaxParts];      // region fill of each partition
+  __shared__ uint32_t wsum[kPBlock / kWave];
+  const uint64_t gbase = uint64_t(blockIdx.x) * P;
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] = 0;
+  uint32_t h[kPRounds];
+#pragma unroll
+  for (int j = 0; j < kPRounds; ++j) {
+    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
+    h[j] = i < r.n ? r.key(i) : 0u;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) loc[p] = 0;
+    const uint64_t base = uint64_t(tile) * kPTile;
+    uint32_t rk[kPRounds];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+      h[j] = murmur32(h[j]);
+      const uint32_t bl = fm.mod(h[j]) - lo;
+      if (i < r.n && bl < nbl) {
+        const uint32_t part = fw.div(bl);
+        rk[j] = (part << 14) | atomicAdd(&loc[part], 1u);
+      } else {
+        rk[j] = kInvalid;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = lds_excl_scan(loc, P, wsum);
+    if (threadIdx.x == 0) loc[P] = m;
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], r.row(i));
+    }
+    __syncthreads();
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
+      h[j] = i < r.n ? r.key(i) : 0u;
+    }
+    for (uint32_t k0 = 0; k0 < m; k0 += kPBlock) {
+      const uint32_t k = k0 + threadIdx.x;
+      const bool v = k < m;
+      uint2 e = make_uint2(0, 0);
+      uint32_t o = 0, p = 0;
+      if (v) {
+        e = stage[k];
+        p = fw.div(fm.mod(e.x) - lo);
+        o = cur[p] + (k - loc[p]);
+        if (o < cap) region[(gbase + p) * cap + o] = e;
+      }
+      const uint64_t spill = __ballot(v && o >= cap);
+      if (spill) {  // wave-aggregated append to the overflow list
+        const int leader = __ffsll((unsigned long long)spill) - 1;
+        unsigned long long b0 = 0;
+        if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
+        b0 = __shfl(b0, leader, kWave);
+        if (v && o >= cap) ovf[b0 + __popcll(spill & lt)] = e;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] += loc[p + 1] - loc[p];
+    __syncthreads();
+  }
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) counts[gbase + p] = min(cur[p], cap);
+}
+
+// cnt_pm[p * G + g] = counts[g * P + p]: partition-major order for the output-slot scan.
+__global__ void k_transpose_counts(const uint32_t* __restrict__ counts, uint32_t G, uint32_t P,
+                                   uint32_t* __restrict__ cnt_pm) {
+  const uint64_t n = uint64_t(G) * P;
+  for (uint64_t q = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; q < n; q += uint64_t(gridDim.x) * blockDim.x) {
+    const uint32_t p = uint32_t(q / G), g = uint32_t(q % G);
+    cnt_pm[q] = counts[uint64_t(g) * P + p];
+  }
+}
+
+// Probe of one partition's regions (one per partitioning workgroup): the table slice is staged in
+// LDS, then wave w walks regions g = g_lo + w, g_lo + w + 16, ... in chunks of 64 * kSegItems
+// pairs, the next chunk in flight while the current one is probed. The output slot of a pair is
+// seg[p * G + g] + its position in the region (dense over all regions, partition-major).
+constexpr int kSegItems = 8;
 template <bool UNIQUE, int MODE, bool CK>
-__global__ __launch_bounds__(kJBlock) void k_rp_probe(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                      const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
-                                                      FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
-                                                      uint32_t splits, uint2* __restrict__ out, uint64_t out_cap,
-                                                      uint64_t* __restrict__ cnt, uint64_t* __restrict__ partials) {
+__global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restrict__ region,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
+                                                          const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
+                                                          FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
+                                                          uint32_t splits, uint2* __restrict__ out, uint64_t out_cap,
+                                                          uint64_t* __restrict__ cnt, uint64_t* __restrict__ partials) {
   __shared__ uint32_t lds[kProbeLdsWords];
   const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
   const uint32_t b0 = p * W;
   const uint32_t nbs = min(W, nbl - b0);
   const uint32_t e0 = off[b0], e1 = off[b0 + nbs];
   const uint32_t ne = e1 - e0;
-  const bool fits = (nbs + 1) + 2ull * ne + 1 <= kProbeLdsWords;  // +1 word: 8-B alignment of entries
+  const bool fits = (nbs + 1) + 2ull * ne + 1 <= kProbeLdsWords;
   uint32_t* loff = lds;
-  const uint32_t ent_word = (nbs + 2) & ~1u;
-  uint2* lent = reinterpret_cast<uint2*>(lds + ent_word);
-  const uint32_t s0 = ps[p], s1 = ps[p + 1];
-  const uint32_t len = s1 - s0;
-  const uint32_t q0 = s0 + uint32_t(uint64_t(len) * sp / splits);
-  const uint32_t q1 = s0 + uint32_t(uint64_t(len) * (sp + 1) / splits);
-  constexpr uint32_t kStep = kJBlock * kItems;
-  // software pipeline: the first batch of pairs is in flight while the slice is staged, and
-  // batch k+1 while batch k is probed
-  uint64_t cur[kItems];
-#pragma unroll
-  for (int j = 0; j < kItems; ++j) {
-    const uint32_t i = q0 + j * kJBlock + threadIdx.x;
-    cur[j] = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
-  }
-  if (fits) {  // stage the slice: every thread keeps kStage loads in flight before writing LDS
-    constexpr int kStage = 8;
-    for (uint32_t k0 = threadIdx.x; k0 <= nbs; k0 += kJBlock * kStage) {
-      uint32_t v[kStage];
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const uint32_t k = k0 + u * kJBlock;
-        v[u] = k <= nbs ? off[b0 + k] : 0u;
-      }
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const uint32_t k = k0 + u * kJBlock;
-        if (k <= nbs) loff[k] = v[u] - e0;
-      }
+  uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
+  constexpr uint32_t kChunk = 64 * kSegItems;
+  // wave-local cursor over (region g, offset q); len = pairs in region g
+  uint32_t g = g_lo + wid, q = 0, len = g < g_hi ? counts[uint64_t(g) * P + p] : 0u;
+  auto advance = [&](uint32_t& gg, uint32_t& qq, uint32_t& ll) {
+    qq += kChunk;
+    while (gg < g_hi && qq >= ll) {
+      gg += kJBlock / kWave;
+      qq = 0;
+      ll = gg < g_hi ? counts[uint64_t(gg) * P + p] : 0u;
     }
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
-    uint64_t* dst = reinterpret_cast<uint64_t*>(lent);
-    for (uint32_t k0 = threadIdx.x; k0 < ne; k0 += kJBlock * kStage) {
-      uint64_t v[kStage];
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const uint32_t k = k0 + u * kJBlock;
-        v[u] = k < ne ? src[k] : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < kStage; ++u) {
-        const uint32_t k = k0 + u * kJBlock;
-        if (k < ne) dst[k] = v[u];
-      }
-    }
+  };
+  while (g < g_hi && len == 0) {  // first non-empty region of this wave
+    g += kJBlock / kWave;
+    len = g < g_hi ? counts[uint64_t(g) * P + p] : 0u;
   }
+  uint64_t cur[kSegItems];
+  auto load = [&](uint64_t (&v)[kSegItems], uint32_t gg, uint32_t qq, uint32_t ll) {
+    const uint2* src = region + (uint64_t(gg) * P + p) * cap;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = qq + j * 64 + lane;
+      v[j] = (gg < g_hi && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
+    }
+  };
+  load(cur, g, q, len);
+  if (fits) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent);
   __syncthreads();
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t base = q0; base < q1; base += kStep) {
-    uint64_t nxt[kItems];
-    const uint32_t nbase = base + kStep;
+  while (g < g_hi) {
+    uint32_t ng = g, nq = q, nl = len;
+    advance(ng, nq, nl);
+    uint64_t nxt[kSegItems];
+    load(nxt, ng, nq, nl);
+    const uint64_t obase = uint64_t(seg[uint64_t(p) * G + g]) + q;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      const uint32_t i = nbase + j * kJBlock + threadIdx.x;
-      nxt[j] = i < q1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
-    }
-#pragma unroll
-    for (int j = 0; j < kItems; ++j) {
-      const uint32_t i = base + j * kJBlock + threadIdx.x;
-      if (i >= q1) continue;
-      const uint32_t h = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
-      const uint32_t bl = fm.mod(h) - lo - b0;
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = q + j * 64 + lane;
+      if (k >= len) continue;
+      const uint32_t hv = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
+      const uint32_t bl = fm.mod(hv) - lo - b0;
+      const uint64_t i = obase + j * 64 + lane;
       if (fits) {
         const uint32_t s = loff[bl];
-        probe_bucket<UNIQUE, MODE, CK>(h, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
       } else {
         const uint32_t s = off[b0 + bl];
-        probe_bucket<UNIQUE, MODE, CK>(h, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
+        probe_bucket<UNIQUE, MODE, CK>(hv, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
       }
     }
+    g = ng;
+    q = nq;
+    len = nl;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
+    for (int j = 0; j < kSegItems; ++j) cur[j] = nxt[j];
   }
   if (MODE != kWrite) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+}
+
+// Overflow pairs (runs that did not fit their region): probed against the table in HBM; output
+// slots follow the regions' (base = seg[P * G]).
+template <bool UNIQUE, int MODE, bool CK>
+__global__ __launch_bounds__(kBlock) void k_probe_ovf(const uint2* __restrict__ ovf,
+                                                      const unsigned long long* __restrict__ novf,
+                                                      const uint32_t* __restrict__ base_slot,
+                                                      const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
+                                                      FastMod fm, uint32_t lo, uint2* __restrict__ out,
+                                                      uint64_t out_cap, uint64_t* __restrict__ cnt,
+                                                      uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t n = *novf, b = *base_slot;
+  for (uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += uint64_t(gridDim.x) * kBlock) {
+    const uint2 e = ovf[j];
+    const uint32_t bl = fm.mod(e.x) - lo;
+    const uint32_t s = off[bl];
+    probe_bucket<UNIQUE, MODE, CK>(e.x, e.y, ent, s, off[bl + 1] - s, acc, b + j, out, out_cap, cnt);
+  }
+  if (MODE != kWrite) block_flush<kProbeFields, 1>(acc, res);
 }
 
 struct Plan {
@@ -431,19 +572,6 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
   hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, pl.ntiles, pl.P, ps);
   return hipGetLastError();
-}
-
-template <bool UNIQUE, int MODE>
-void launch_probe(const hj3d_table* t, const Plan& pl, uint32_t splits, const uint2* pairs, const uint32_t* ps,
-                  uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, bool ck, hipStream_t s) {
-  if (ck)
-    hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE, true>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
-                       t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
-                       t->nb_local, pl.W, splits, out, cap, cnt, partials);
-  else
-    hipLaunchKernelGGL((k_rp_probe<UNIQUE, MODE, false>), dim3(pl.P * splits), dim3(kJBlock), 0, s, pairs, ps,
-                       t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm, uint32_t(t->desc.bucket_lo),
-                       t->nb_local, pl.W, splits, out, cap, cnt, partials);
 }
 
 // Sort every bucket of 2..kSortedMax entries by row (insertion sort, one thread per bucket; the
@@ -501,6 +629,46 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   return hipGetLastError();
 }
 
+namespace {
+
+struct SegLaunch {
+  const hj3d_table* t;
+  Plan pl;
+  uint32_t G, cap, splits;
+  const uint2* region;
+  const uint32_t* counts;
+  const uint32_t* seg;
+  const uint2* ovf;
+  const unsigned long long* novf;
+  int ovf_grid;
+};
+
+template <bool UNIQUE, int MODE, bool CK>
+void launch_seg(const SegLaunch& L, uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, uint64_t* res,
+                hipStream_t s) {
+  const hj3d_table* t = L.t;
+  hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s, L.region,
+                     L.counts, L.seg, L.G, L.cap, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
+                     uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, out, cap, cnt, partials);
+  hipLaunchKernelGGL((k_probe_ovf<UNIQUE, MODE, CK>), dim3(L.ovf_grid), dim3(kBlock), 0, s, L.ovf, L.novf,
+                     L.seg + uint64_t(L.G) * L.pl.P, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
+                     uint32_t(t->desc.bucket_lo), out, cap, cnt, res);
+}
+
+template <int MODE>
+void launch_seg_any(const SegLaunch& L, bool unique, bool ck, uint2* out, uint64_t cap, uint64_t* cnt,
+                    uint64_t* partials, uint64_t* res, hipStream_t s) {
+  if (unique) {
+    if (ck) launch_seg<true, MODE, true>(L, out, cap, cnt, partials, res, s);
+    else launch_seg<true, MODE, false>(L, out, cap, cnt, partials, res, s);
+  } else {
+    if (ck) launch_seg<false, MODE, true>(L, out, cap, cnt, partials, res, s);
+    else launch_seg<false, MODE, false>(L, out, cap, cnt, partials, res, s);
+  }
+}
+
+}  // namespace
+
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                        uint64_t out_cap, uint64_t* res, hipStream_t s) {
   hipError_t e;
@@ -509,38 +677,67 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
   uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
   if (W < 64) W = 64;
-  const Plan pl = plan_for(nbl, W, r.n);
-  if (pl.P > kMaxParts) return hipErrorNotSupported;
-  uint32_t splits = 1;
+  SegLaunch L;
+  L.t = t;
+  L.pl = plan_for(nbl, W, r.n);
+  const uint32_t P = L.pl.P;
+  if (P > kMaxParts) return hipErrorNotSupported;
+  L.G = L.pl.ntiles < uint32_t(ctx->num_cus) ? L.pl.ntiles : uint32_t(ctx->num_cus);
+  // region capacity: expected pairs per (workgroup, partition) + 8 sigma + slack, 128-B multiple
+  const uint64_t per_g = uint64_t((L.pl.ntiles + L.G - 1) / L.G) * kPTile;
+  const double ex = double(per_g < r.n ? per_g : r.n) / P;
+  uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
+  cap = (cap + 15) & ~uint64_t(15);
+  L.cap = uint32_t(cap);
+  const uint64_t nreg = uint64_t(L.G) * P;
+  if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPHist].ensure((3 * nreg + 2) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2) + 64)) != hipSuccess) return e;
+  uint2* region = ctx->scratch[kScrPairs].as<uint2>();
+  uint32_t* counts = ctx->scratch[kScrPHist].as<uint32_t>();
+  uint32_t* seg = counts + nreg;  // nreg + 1 (transposed counts, scanned in place)
+  unsigned long long* novf = ctx->scratch[kScrSortV].as<unsigned long long>();
+  uint2* ovf = reinterpret_cast<uint2*>(ctx->scratch[kScrSortV].as<char>() + 64);
+  L.region = region;
+  L.counts = counts;
+  L.seg = seg;
+  L.ovf = ovf;
+  L.novf = novf;
+  L.ovf_grid = ctx->num_cus;
+  L.splits = 1;
   const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
-  if (pl.P < want_blocks) splits = (want_blocks + pl.P - 1) / pl.P;
-  if ((e = ctx->scratch[kScrPairs].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
-  const uint32_t nblocks = pl.P * splits;
+  if (P < want_blocks) L.splits = (want_blocks + P - 1) / P;
+  if (L.splits > L.G) L.splits = L.G;
+  const uint32_t nblocks = P * L.splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
-  uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
-  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
-  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s, HJ3D_T_HIST, HJ3D_T_SCATTER)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  const RelView v = view_of(r);
+  {
+    PhaseTimer tm(ctx, HJ3D_T_SCATTER);
+    hipLaunchKernelGGL(k_rp_part1, dim3(L.G), dim3(kPBlock), 0, s, v, t->fm, uint32_t(t->desc.bucket_lo), nbl,
+                       L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
+  }
+  hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, L.G, P, seg);
+  if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
   const bool unique = flags & HJ3D_PROBE_UNIQUE;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   uint2* o = static_cast<uint2*>(out);
   PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);  // for the non-unique EMIT form this includes the offset scan
   if (!emit) {
-    if (unique) launch_probe<true, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);
-    else launch_probe<false, kAgg>(t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, ck, s);
+    launch_seg_any<kAgg>(L, unique, ck, nullptr, 0, nullptr, partials, res, s);
   } else if (unique) {
-    launch_probe<true, kDense>(t, pl, splits, pairs, ps, o, out_cap, nullptr, partials, ck, s);
+    launch_seg_any<kDense>(L, true, ck, o, out_cap, nullptr, partials, res, s);
   } else {
     if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
     uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
     if ((e = hipMemsetAsync(cnt, 0, (r.n + 1) * sizeof(uint64_t), s)) != hipSuccess) return e;
-    launch_probe<false, kCount>(t, pl, splits, pairs, ps, nullptr, 0, cnt, partials, ck, s);
-    // only the probes that landed in owned buckets are counted; unowned pairs were dropped
+    launch_seg_any<kCount>(L, false, ck, nullptr, 0, cnt, partials, res, s);
+    // slots of unowned tuples (dropped by the partition) stay 0
     if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
-    launch_probe<false, kWrite>(t, pl, splits, pairs, ps, o, out_cap, cnt, nullptr, ck, s);
+    launch_seg_any<kWrite>(L, false, ck, o, out_cap, cnt, nullptr, res, s);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)

@@ -201,8 +201,7 @@ def main():
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     # per-kernel averages over the timed steps (HIP events on the engine's stream)
     kern_avg = {}
-    for name, ph in (("k_rp_probe", hj3d.T_PROBE_KERNEL), ("k_rp_scatter", hj3d.T_SCATTER),
-                     ("k_rp_hist", hj3d.T_HIST)):
+    for name, ph in (("k_rp_probe_seg", hj3d.T_PROBE_KERNEL), ("k_rp_part1", hj3d.T_SCATTER)):
         ms, cnt = ctx.timer(ph)
         kern_avg[name] = ms / cnt if cnt else None
     # verification step (outside the timed region): the same step once more with the
@@ -243,18 +242,15 @@ def main():
 
     # ---- roofline of the dominant kernel ----
     # Algorithmic bytes per launch (DESIGN.md "Kernels"), n = probe tuples of this rank:
-    #   k_rp_hist     n * 12                      read the S tuple (AoS {k,a,b}; the key's line)
-    #   k_rp_scatter  n * (12 + 8)                read the S tuple, write the (hash,row) pair
-    #   k_rp_probe    n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
-    #                                                  the table slices (entries + directory) once
-    # (N > 1: the probe side is the received pair array, 8 B per tuple, and has no hist/scatter
-    # tuple read beyond it.)
+    #   k_rp_part1      n * (12 + 8)                read the S tuple (AoS {k,a,b}), write the (hash,row) pair
+    #   k_rp_probe_seg  n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
+    #                                                    the table slices (entries + directory) once
+    # (N > 1: the probe side is the received pair array, 8 B per tuple.)
     n = probe_n_local
     tuple_bytes = 12 if world == 1 else 8
     alg = {
-        "k_rp_hist": n * tuple_bytes,
-        "k_rp_scatter": n * (tuple_bytes + 8),
-        "k_rp_probe": n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4,
+        "k_rp_part1": n * (tuple_bytes + 8),
+        "k_rp_probe_seg": n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4,
     }
     kernels = {}
     for k, ms in kern_avg.items():
