@@ -72,6 +72,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * ntiles + blockIdx.x] = cnt[p];
 }
 
+template <int BLOCK = kJBlock>
 __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
 
 // Scatter (hash, row) pairs to their partitions. The tile is first ranked per partition with
@@ -143,9 +144,10 @@ __global__ void k_rp_starts(const uint32_t* __restrict__ offs, uint32_t ntiles, 
     ps[p] = offs[uint64_t(p) * ntiles];
 }
 
-// Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. 1024 threads.
+// Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. BLOCK threads.
+template <int BLOCK>
 __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
-  const uint32_t per = (n + kJBlock - 1) / kJBlock;
+  const uint32_t per = (n + BLOCK - 1) / BLOCK;
   const uint32_t beg = threadIdx.x * per;
   const uint32_t end = min(beg + per, n);
   uint32_t local = 0;
@@ -160,7 +162,7 @@ __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
   if (lane == 63) wsum[wid] = x;
   __syncthreads();
   uint32_t wpre = 0, tot = 0;
-  for (int w = 0; w < kJBlock / kWave; ++w) {
+  for (int w = 0; w < BLOCK / kWave; ++w) {
     const uint32_t v = wsum[w];
     if (w < wid) wpre += v;
     tot += v;
@@ -341,58 +343,62 @@ __device__ __forceinline__ void stage_slice(const uint32_t* __restrict__ off, co
 // atomics), stage in partition order (LDS), write each partition's run at the cursor. A run that
 // does not fit (skewed probe keys) goes to the overflow list, probed by k_probe_ovf. S is read
 // once instead of twice (histogram + scatter).
-__global__ __launch_bounds__(kPBlock) void k_rp_part1(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
-                                                      uint32_t P, uint32_t ntiles, uint32_t cap,
-                                                      uint2* __restrict__ region, uint32_t* __restrict__ counts,
-                                                      uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
-  __shared__ uint2 stage[kPTile];
-  __shared__ uint32_t loc[kMaxParts + 1];  // tile counts, then tile-local run starts (loc[P] = tile size)
-  __shared__ uint32_t cur[kMaxParts];      // region fill of each partition
-  __shared__ uint32_t wsum[kPBlock / kWave];
+template <int BLOCK, int ROUNDS, int MAXP>
+__global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                    uint32_t P, uint32_t ntiles, uint32_t cap,
+                                                    uint2* __restrict__ region, uint32_t* __restrict__ counts,
+                                                    uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
+  constexpr int TILE = BLOCK * ROUNDS;
+  constexpr int TBITS = __builtin_ctz(TILE);
+  static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 16), "tile must be a power of two");
+  __shared__ uint2 stage[TILE];
+  __shared__ uint32_t loc[MAXP + 1];  // tile counts, then tile-local run starts (loc[P] = tile size)
+  __shared__ uint32_t cur[MAXP];      // region fill of each partition
+  __shared__ uint32_t wsum[BLOCK / kWave];
   const uint64_t gbase = uint64_t(blockIdx.x) * P;
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] = 0;
-  uint32_t h[kPRounds];
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] = 0;
+  uint32_t h[ROUNDS];
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
+  for (int j = 0; j < ROUNDS; ++j) {
+    const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
   }
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) loc[p] = 0;
-    const uint64_t base = uint64_t(tile) * kPTile;
-    uint32_t rk[kPRounds];
+    for (uint32_t p = threadIdx.x; p < P; p += BLOCK) loc[p] = 0;
+    const uint64_t base = uint64_t(tile) * TILE;
+    uint32_t rk[ROUNDS];
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = murmur32(h[j]);
       const uint32_t bl = fm.mod(h[j]) - lo;
       if (i < r.n && bl < nbl) {
         const uint32_t part = fw.div(bl);
-        rk[j] = (part << 14) | atomicAdd(&loc[part], 1u);
+        rk[j] = (part << TBITS) | atomicAdd(&loc[part], 1u);
       } else {
         rk[j] = kInvalid;
       }
     }
     __syncthreads();
-    const uint32_t m = lds_excl_scan(loc, P, wsum);
+    const uint32_t m = lds_excl_scan<BLOCK>(loc, P, wsum);
     if (threadIdx.x == 0) loc[P] = m;
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
+    for (int j = 0; j < ROUNDS; ++j) {
       if (rk[j] == kInvalid) continue;
-      const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], r.row(i));
+      const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
+      stage[loc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], r.row(i));
     }
     __syncthreads();
-    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;  // next tile: loads in flight
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = i < r.n ? r.key(i) : 0u;
     }
-    for (uint32_t k0 = 0; k0 < m; k0 += kPBlock) {
+    for (uint32_t k0 = 0; k0 < m; k0 += BLOCK) {
       const uint32_t k = k0 + threadIdx.x;
       const bool v = k < m;
       uint2 e = make_uint2(0, 0);
@@ -413,10 +419,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_part1(RelView r, FastMod fm, uin
       }
     }
     __syncthreads();
-    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cur[p] += loc[p + 1] - loc[p];
+    for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] += loc[p + 1] - loc[p];
     __syncthreads();
   }
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) counts[gbase + p] = min(cur[p], cap);
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
 }
 
 // cnt_pm[p * G + g] = counts[g * P + p]: partition-major order for the output-slot scan.
@@ -433,8 +439,10 @@ __global__ void k_transpose_counts(const uint32_t* __restrict__ counts, uint32_t
 // LDS, then wave w walks regions g = g_lo + w, g_lo + w + 16, ... in chunks of 64 * kSegItems
 // pairs, the next chunk in flight while the current one is probed. The output slot of a pair is
 // seg[p * G + g] + its position in the region (dense over all regions, partition-major).
+// FITS: the kernel handles only the partitions whose slice fits LDS (the common case, a tight
+// loop over LDS), or only the others (reads the slice through L2); both are launched.
 constexpr int kSegItems = 8;
-template <bool UNIQUE, int MODE, bool CK>
+template <bool UNIQUE, int MODE, bool CK, bool FITS>
 __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restrict__ region,
                                                           const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
@@ -449,44 +457,56 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
   const uint32_t e0 = off[b0], e1 = off[b0 + nbs];
   const uint32_t ne = e1 - e0;
   const bool fits = (nbs + 1) + 2ull * ne + 1 <= kProbeLdsWords;
+  if (fits != FITS) {  // the other kernel takes this partition; keep this block's partial row zero
+    if (FITS && MODE != kWrite && threadIdx.x < kProbeFields)
+      partials[uint64_t(blockIdx.x) * kProbeFields + threadIdx.x] = 0;
+    return;
+  }
   uint32_t* loff = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kJBlock / kWave;
   const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
   constexpr uint32_t kChunk = 64 * kSegItems;
-  // wave-local cursor over (region g, offset q); len = pairs in region g
-  uint32_t g = g_lo + wid, q = 0, len = g < g_hi ? counts[uint64_t(g) * P + p] : 0u;
-  auto advance = [&](uint32_t& gg, uint32_t& qq, uint32_t& ll) {
-    qq += kChunk;
-    while (gg < g_hi && qq >= ll) {
-      gg += kJBlock / kWave;
-      qq = 0;
-      ll = gg < g_hi ? counts[uint64_t(gg) * P + p] : 0u;
-    }
-  };
-  while (g < g_hi && len == 0) {  // first non-empty region of this wave
-    g += kJBlock / kWave;
-    len = g < g_hi ? counts[uint64_t(g) * P + p] : 0u;
+  // The regions of wave wid are g = g_lo + wid + kWaves * r; lane r holds region r's pair count and
+  // output base, so the walk below never waits on a global load for its bookkeeping.
+  const uint32_t nr = g_hi > g_lo + wid ? (g_hi - g_lo - wid + kWaves - 1) / kWaves : 0u;  // <= 64 (G <= 1024)
+  uint32_t my_len = 0, my_seg = 0;
+  if (uint32_t(lane) < nr) {
+    const uint32_t gg = g_lo + wid + kWaves * lane;
+    my_len = counts[uint64_t(gg) * P + p];
+    my_seg = seg[uint64_t(p) * G + gg];
   }
-  uint64_t cur[kSegItems];
-  auto load = [&](uint64_t (&v)[kSegItems], uint32_t gg, uint32_t qq, uint32_t ll) {
-    const uint2* src = region + (uint64_t(gg) * P + p) * cap;
+  // wave-uniform cursor: region index r, offset q
+  uint32_t r = 0, q = 0;
+  uint32_t len = __shfl(my_len, 0, kWave);
+  while (r < nr && len == 0) {
+    ++r;
+    len = __shfl(my_len, int(r & 63), kWave);
+  }
+  auto load = [&](uint64_t (&v)[kSegItems], uint32_t rr, uint32_t qq, uint32_t ll) {
+    const uint2* src = region + (uint64_t(g_lo + wid + kWaves * rr) * P + p) * cap;
 #pragma unroll
     for (int j = 0; j < kSegItems; ++j) {
       const uint32_t k = qq + j * 64 + lane;
-      v[j] = (gg < g_hi && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
+      v[j] = (rr < nr && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
     }
   };
-  load(cur, g, q, len);
-  if (fits) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent);
+  uint64_t cur[kSegItems];
+  load(cur, r, q, len);
+  if (FITS) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent);
   __syncthreads();
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  while (g < g_hi) {
-    uint32_t ng = g, nq = q, nl = len;
-    advance(ng, nq, nl);
+  while (r < nr) {
+    uint32_t nr_ = r, nq = q + kChunk, nl = len;
+    while (nr_ < nr && nq >= nl) {
+      ++nr_;
+      nq = 0;
+      nl = __shfl(my_len, int(nr_ & 63), kWave);
+    }
     uint64_t nxt[kSegItems];
-    load(nxt, ng, nq, nl);
-    const uint64_t obase = uint64_t(seg[uint64_t(p) * G + g]) + q;
+    load(nxt, nr_, nq, nl);
+    const uint64_t obase = uint64_t(__shfl(my_seg, int(r & 63), kWave)) + q;
 #pragma unroll
     for (int j = 0; j < kSegItems; ++j) {
       const uint32_t k = q + j * 64 + lane;
@@ -494,7 +514,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
       const uint32_t hv = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
       const uint32_t bl = fm.mod(hv) - lo - b0;
       const uint64_t i = obase + j * 64 + lane;
-      if (fits) {
+      if (FITS) {
         const uint32_t s = loff[bl];
         probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
       } else {
@@ -502,13 +522,16 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
         probe_bucket<UNIQUE, MODE, CK>(hv, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
       }
     }
-    g = ng;
+    r = nr_;
     q = nq;
     len = nl;
 #pragma unroll
     for (int j = 0; j < kSegItems; ++j) cur[j] = nxt[j];
   }
-  if (MODE != kWrite) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+  if (MODE != kWrite) {
+    if (FITS) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+    else block_flush<kProbeFields, 1>(acc, partials + uint64_t(gridDim.x) * kProbeFields);  // extra row (atomics)
+  }
 }
 
 // Overflow pairs (runs that did not fit their region): probed against the table in HBM; output
@@ -647,9 +670,13 @@ template <bool UNIQUE, int MODE, bool CK>
 void launch_seg(const SegLaunch& L, uint2* out, uint64_t cap, uint64_t* cnt, uint64_t* partials, uint64_t* res,
                 hipStream_t s) {
   const hj3d_table* t = L.t;
-  hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s, L.region,
+  hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK, true>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s, L.region,
                      L.counts, L.seg, L.G, L.cap, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
                      uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, out, cap, cnt, partials);
+  hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK, false>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s,
+                     L.region, L.counts, L.seg, L.G, L.cap, t->off.as<const uint32_t>(), t->ent.as<const uint2>(),
+                     t->fm, uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, out, cap, cnt,
+                     partials);
   hipLaunchKernelGGL((k_probe_ovf<UNIQUE, MODE, CK>), dim3(L.ovf_grid), dim3(kBlock), 0, s, L.ovf, L.novf,
                      L.seg + uint64_t(L.G) * L.pl.P, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
                      uint32_t(t->desc.bucket_lo), out, cap, cnt, res);
@@ -709,15 +736,19 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   if (P < want_blocks) L.splits = (want_blocks + P - 1) / P;
   if (L.splits > L.G) L.splits = L.G;
   const uint32_t nblocks = P * L.splits;
-  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+  // one row per probe workgroup + one extra row accumulated with atomics by the non-fitting kernel
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 1) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  if ((e = hipMemsetAsync(partials + uint64_t(nblocks) * kProbeFields, 0, kProbeFields * sizeof(uint64_t), s)) !=
+      hipSuccess)
+    return e;
   if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
   const RelView v = view_of(r);
   {
     PhaseTimer tm(ctx, HJ3D_T_SCATTER);
-    hipLaunchKernelGGL(k_rp_part1, dim3(L.G), dim3(kPBlock), 0, s, v, t->fm, uint32_t(t->desc.bucket_lo), nbl,
-                       L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
+    hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
+                       uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
   }
   hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, L.G, P, seg);
   if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
@@ -741,7 +772,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
-  return reduce_partials(partials, nblocks, kProbeFields, 1, res, s, r.n);
+  return reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n);
 }
 
 }  // namespace hj3d

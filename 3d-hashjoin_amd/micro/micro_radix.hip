@@ -1,11 +1,11 @@
-// micro_radix.hip — diagnostic microbenchmark of the radix-join kernels (not product).
+// micro_radix.hip — diagnostic microbenchmark of the radix-join probe kernels (not product).
 //
 // Compiles radix.hip + scan.hip into this translation unit (under a renamed namespace) so the
-// real kernels can be launched next to stripped variants on the same data:
-//   probe:   real k_rp_probe (dense EMIT / aggregate) vs copy-only (pairs -> out at the same
-//            geometry) vs copy + slice staging
-//   scatter: real k_rp_scatter vs a streaming floor (read tuple, write pair in place)
-// Config B shapes: |R| = 1e7 keys, |S| = 1e8 AoS {k,a,b} with S.a uniform in [0, |R|).
+// real kernels can be launched with other template parameters and next to streaming floors on
+// the same data. Config B shapes: |R| = 1e7 keys, |S| = 1e8 AoS {k,a,b}, S.a uniform in [0,|R|).
+//   part1<B,R,MAXP>  single-pass partitioner variants (workgroup size, tile, occupancy)
+//   probe_seg        the segmented probe on each variant's regions
+//   stream floors    read the tuple + write a pair in place; read pairs + write pairs
 #define hj3d hj3d_micro
 #include "../csrc/radix.hip"
 #include "../csrc/scan.hip"
@@ -32,41 +32,6 @@ __global__ void k_fill(uint32_t* t, uint64_t n, uint32_t stride_w, uint32_t nr, 
   }
 }
 
-// copy-only: same grid/partition geometry as k_rp_probe, pairs -> out, optional slice stage
-template <bool STAGE>
-__global__ __launch_bounds__(1024) void k_copy(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                               const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
-                                               uint32_t nbl, uint32_t W, uint2* __restrict__ out) {
-  __shared__ uint32_t lds[36864];
-  const uint32_t p = blockIdx.x;
-  const uint32_t b0 = p * W;
-  const uint32_t nbs = min(W, nbl - b0);
-  if (STAGE) {
-    const uint32_t e0 = off[b0], ne = off[b0 + nbs] - e0;
-    for (uint32_t k = threadIdx.x; k <= nbs; k += 1024) lds[k] = off[b0 + k] - e0;
-    uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
-    for (uint32_t k = threadIdx.x; k < ne; k += 1024) lent[k] = ent[e0 + k];
-    __syncthreads();
-  }
-  const uint32_t s0 = ps[p], s1 = ps[p + 1];
-  uint32_t x = 0;
-  for (uint32_t base = s0; base < s1; base += 1024 * 12) {
-    uint64_t v[12];
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const uint32_t i = base + j * 1024 + threadIdx.x;
-      v[j] = i < s1 ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(pairs + i)) : 0ull;
-    }
-#pragma unroll
-    for (int j = 0; j < 12; ++j) {
-      const uint32_t i = base + j * 1024 + threadIdx.x;
-      if (STAGE) x += lds[uint32_t(v[j]) % (nbs + 1)];
-      if (i < s1) __builtin_nontemporal_store(v[j] ^ x, reinterpret_cast<uint64_t*>(out + i));
-    }
-  }
-}
-
-// streaming floor of the scatter: read the AoS key, hash, write (hash,row) in place
 __global__ __launch_bounds__(1024) void k_stream_pairs(RelView r, uint2* __restrict__ out) {
   const uint64_t stride = uint64_t(gridDim.x) * 1024 * 16;
   for (uint64_t base = uint64_t(blockIdx.x) * 1024 * 16; base < r.n; base += stride) {
@@ -83,6 +48,176 @@ __global__ __launch_bounds__(1024) void k_stream_pairs(RelView r, uint2* __restr
     }
   }
 }
+
+__global__ __launch_bounds__(256) void k_copy_pairs(const uint2* __restrict__ in, uint64_t n, uint2* __restrict__ out) {
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(in + i)) ^ 1ull,
+                                reinterpret_cast<uint64_t*>(out + i));
+}
+
+
+// Diagnostic copy of k_rp_part1 with phases switched off (timing only; results are garbage).
+// KNOB bit 0: skip rank atomics (rank = round), bit 1: skip staging, bit 2: skip global stores,
+// bit 3: skip the write-out loop entirely, bit 4: skip key loads (keys = index hash)
+template <int KNOB>
+__global__ __launch_bounds__(1024) void k_part1_knob(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                     uint32_t P, uint32_t ntiles, uint32_t cap,
+                                                     uint2* __restrict__ region, uint32_t* __restrict__ counts) {
+  constexpr int BLOCK = 1024, ROUNDS = 16, TILE = BLOCK * ROUNDS, TBITS = 14;
+  __shared__ uint2 stage[TILE];
+  __shared__ uint32_t loc[2049];
+  __shared__ uint32_t cur[2048];
+  __shared__ uint32_t wsum[BLOCK / kWave];
+  const uint64_t gbase = uint64_t(blockIdx.x) * P;
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] = 0;
+  uint32_t h[ROUNDS];
+#pragma unroll
+  for (int j = 0; j < ROUNDS; ++j) {
+    const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
+    h[j] = (KNOB & 16) ? uint32_t(i * 2654435761u) : (i < r.n ? r.key(i) : 0u);
+  }
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    for (uint32_t p = threadIdx.x; p < P; p += BLOCK) loc[p] = 0;
+    const uint64_t base = uint64_t(tile) * TILE;
+    uint32_t rk[ROUNDS];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
+      h[j] = murmur32(h[j]);
+      const uint32_t bl = fm.mod(h[j]) - lo;
+      if (i < r.n && bl < nbl) {
+        const uint32_t part = fw.div(bl);
+        rk[j] = (part << TBITS) | ((KNOB & 1) ? uint32_t(j) : atomicAdd(&loc[part], 1u));
+      } else {
+        rk[j] = kInvalid;
+      }
+    }
+    __syncthreads();
+    const uint32_t m = lds_excl_scan<BLOCK>(loc, P, wsum);
+    if (threadIdx.x == 0) loc[P] = m;
+    if (!(KNOB & 2)) {
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        if (rk[j] == kInvalid) continue;
+        const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
+        stage[(loc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))) & (TILE - 1)] = make_uint2(h[j], r.row(i));
+      }
+    }
+    __syncthreads();
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
+      h[j] = (KNOB & 16) ? uint32_t(i * 2654435761u) : (i < r.n ? r.key(i) : 0u);
+    }
+    if (!(KNOB & 8)) {
+      for (uint32_t k = threadIdx.x; k < TILE; k += BLOCK) {
+        const uint2 e = stage[k];
+        const uint32_t p = fw.div(fm.mod(e.x) - lo) % P;
+        const uint32_t o = (cur[p] + (k - loc[p])) % cap;
+        if (!(KNOB & 4)) region[(gbase + p) * cap + o] = e;
+        else if (e.x == 0x12345678u && o == 7u) region[0] = e;
+      }
+    }
+    __syncthreads();
+    for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] += loc[p + 1] - loc[p];
+    __syncthreads();
+  }
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
+}
+
+template <int KNOB>
+__global__ __launch_bounds__(kJBlock) void k_probe_knob(const uint2* __restrict__ region,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
+                                                          const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
+                                                          FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
+                                                          uint32_t splits, uint2* __restrict__ out, uint64_t out_cap,
+                                                          uint64_t* __restrict__ cnt, uint64_t* __restrict__ partials) {
+  __shared__ uint32_t lds[kProbeLdsWords];
+  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, nbl - b0);
+  const uint32_t e0 = off[b0], e1 = off[b0 + nbs];
+  const uint32_t ne = e1 - e0;
+  const bool fits = (nbs + 1) + 2ull * ne + 1 <= kProbeLdsWords;
+  uint32_t* loff = lds;
+  uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kJBlock / kWave;
+  const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
+  constexpr uint32_t kChunk = 64 * kSegItems;
+  // The regions of wave wid are g = g_lo + wid + kWaves * r; lane r holds region r's pair count and
+  // output base, so the walk below never waits on a global load for its bookkeeping.
+  const uint32_t nr = g_hi > g_lo + wid ? (g_hi - g_lo - wid + kWaves - 1) / kWaves : 0u;  // <= 64 (G <= 1024)
+  uint32_t my_len = 0, my_seg = 0;
+  if (uint32_t(lane) < nr) {
+    const uint32_t gg = g_lo + wid + kWaves * lane;
+    my_len = counts[uint64_t(gg) * P + p];
+    my_seg = seg[uint64_t(p) * G + gg];
+  }
+  // wave-uniform cursor: region index r, offset q
+  uint32_t r = 0, q = 0;
+  uint32_t len = __shfl(my_len, 0, kWave);
+  while (r < nr && len == 0) {
+    ++r;
+    len = __shfl(my_len, int(r & 63), kWave);
+  }
+  auto load = [&](uint64_t (&v)[kSegItems], uint32_t rr, uint32_t qq, uint32_t ll) {
+    const uint2* src = region + (uint64_t(g_lo + wid + kWaves * rr) * P + p) * cap;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = qq + j * 64 + lane;
+      v[j] = (rr < nr && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
+    }
+  };
+  uint64_t cur[kSegItems];
+  load(cur, r, q, len);
+  if (fits && !(KNOB & 1)) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent);
+  __syncthreads();
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  while (r < nr) {
+    uint32_t nr_ = r, nq = q + kChunk, nl = len;
+    while (nr_ < nr && nq >= nl) {
+      ++nr_;
+      nq = 0;
+      nl = __shfl(my_len, int(nr_ & 63), kWave);
+    }
+    uint64_t nxt[kSegItems];
+    load(nxt, nr_, nq, nl);
+    const uint64_t obase = uint64_t(__shfl(my_seg, int(r & 63), kWave)) + q;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = q + j * 64 + lane;
+      if (k >= len) continue;
+      const uint32_t hv = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
+      const uint32_t bl = fm.mod(hv) - lo - b0;
+      const uint64_t i = obase + j * 64 + lane;
+      if (KNOB & 2) {
+        acc[0] += bl;
+        if (!(KNOB & 4)) __builtin_nontemporal_store(cur[j] ^ bl, reinterpret_cast<uint64_t*>(out + i));
+      } else if (KNOB & 4) {
+        const uint32_t s = loff[bl];
+        probe_bucket<true, kAgg, false>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+      } else if (KNOB & 8) {  // directory lookup only
+        const uint32_t s = loff[bl], e = loff[bl + 1];
+        acc[0] += s ^ e;
+        __builtin_nontemporal_store(cur[j] ^ (uint64_t(s) << 32 | e), reinterpret_cast<uint64_t*>(out + i));
+      } else {
+        const uint32_t s = loff[bl];
+        probe_bucket<true, kDense, false>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+      }
+    }
+    r = nr_;
+    q = nq;
+    len = nl;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) cur[j] = nxt[j];
+  }
+  block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+}
+
 
 }  // namespace
 
@@ -112,8 +247,9 @@ int main(int argc, char** argv) {
   CK(t.counts.ensure(32));
   CK(radix_build(&ctx, &t, rr, 0));
   CK(sort_small_buckets(&ctx, &t, 0));
-  uint2* out;
+  uint2 *out, *pairs;
   CK(hipMalloc(&out, nS * 8));
+  CK(hipMalloc(&pairs, nS * 8));
   uint64_t* res;
   CK(hipMalloc(&res, 16 * 8));
   hipEvent_t a, b;
@@ -129,38 +265,100 @@ int main(int argc, char** argv) {
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     ms /= reps;
-    printf("%-28s %8.3f ms  %7.0f GB/s (alg)\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+    printf("%-40s %8.3f ms  %7.0f GB/s (alg)\n", name, ms, bytes / (ms * 1e-3) / 1e9);
+    return ms;
   };
-  // the real probe (partition + probe); afterwards the scratch holds the partitioned pairs
-  ctx.timing = false;
-  timeit("radix_probe dense (all)", [&] { CK(radix_probe(&ctx, &t, rs, HJ3D_PROBE_UNIQUE | HJ3D_PROBE_EMIT, out, nS, res, 0)); }, nS * 28.0);
-  // reconstruct the probe plan
-  const double fill = double(nR) / nR;
-  uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
-  const Plan pl = plan_for(nR, W, nS);
-  const uint2* pairs = ctx.scratch[kScrPairs].as<uint2>();
-  const uint32_t* ps = ctx.scratch[kScrPStart].as<uint32_t>();
-  uint64_t* partials = ctx.scratch[kScrPartial].as<uint64_t>();
-  uint32_t splits = 1;
-  if (pl.P < uint32_t(ctx.num_cus) * 2) splits = (uint32_t(ctx.num_cus) * 2 + pl.P - 1) / pl.P;
-  printf("P=%u W=%u splits=%u ntiles=%u\n", pl.P, pl.W, splits, pl.ntiles);
-  const double pb = nS * 16.0 + nR * 12.0;
-  timeit("k_rp_probe dense", [&] { launch_probe<true, kDense>(&t, pl, splits, pairs, ps, out, nS, nullptr, partials, false, 0); }, pb);
-  timeit("k_rp_probe agg", [&] { launch_probe<true, kAgg>(&t, pl, splits, pairs, ps, nullptr, 0, nullptr, partials, false, 0); }, nS * 8.0 + nR * 12.0);
-  timeit("copy (no stage)", [&] { hipLaunchKernelGGL(k_copy<false>, dim3(pl.P), dim3(1024), 0, 0, pairs, ps, t.off.as<const uint32_t>(), t.ent.as<const uint2>(), nR, pl.W, out); }, pb);
-  timeit("copy + stage + 1 lds", [&] { hipLaunchKernelGGL(k_copy<true>, dim3(pl.P), dim3(1024), 0, 0, pairs, ps, t.off.as<const uint32_t>(), t.ent.as<const uint2>(), nR, pl.W, out); }, pb);
-  // scatter side
-  uint2* pout = ctx.scratch[kScrPairs].as<uint2>();
-  timeit("partition_pairs (hist+scan+scatter)", [&] { CK(partition_pairs(&ctx, &t, rs, pl, pout, ctx.scratch[kScrPStart].as<uint32_t>(), 0)); }, nS * 32.0);
+  timeit("radix_probe dense (product, all)",
+         [&] { CK(radix_probe(&ctx, &t, rs, HJ3D_PROBE_UNIQUE | HJ3D_PROBE_EMIT, out, nS, res, 0)); }, nS * 28.0);
   const RelView v = view_of(rs);
-  const uint32_t* hist = ctx.scratch[kScrPHist].as<uint32_t>();
-  const uint32_t g = pl.ntiles < uint32_t(ctx.num_cus) ? pl.ntiles : uint32_t(ctx.num_cus);
-  timeit("k_rp_scatter", [&] { hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, 0, v, t.fm, 0u, nR, pl.fw, pl.P, pl.ntiles, hist, pout); }, nS * 20.0);
-  timeit("k_rp_hist", [&] { hipLaunchKernelGGL(k_rp_hist, dim3(pl.ntiles), dim3(kPBlock), 0, 0, v, t.fm, 0u, nR, pl.fw, pl.P, pl.ntiles, const_cast<uint32_t*>(hist)); }, nS * 12.0);
-  for (unsigned gg : {256u, 512u, 1024u, 2048u})
-    timeit(gg == 256 ? "stream pairs g=256" : gg == 512 ? "stream pairs g=512" : gg == 1024 ? "stream pairs g=1024" : "stream pairs g=2048",
-           [&] { hipLaunchKernelGGL(k_stream_pairs, dim3(gg), dim3(1024), 0, 0, v, out); }, nS * 20.0);
-  // restore the partitioned pairs for any later use and check nothing faulted
+  timeit("floor: read tuple, write pair", [&] { hipLaunchKernelGGL(k_stream_pairs, dim3(1024), dim3(1024), 0, 0, v, pairs); },
+         nS * 20.0);
+  timeit("floor: read pair, write pair", [&] { hipLaunchKernelGGL(k_copy_pairs, dim3(4096), dim3(256), 0, 0, pairs, nS, out); },
+         nS * 16.0);
+
+  const double fill = 1.0;
+  const uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
+  const Plan pl0 = plan_for(nR, W, nS);
+  const uint32_t P = pl0.P;
+  uint32_t* counts;
+  uint32_t* seg;
+  uint2* ovf;
+  unsigned long long* novf;
+  uint2* region;
+  const uint64_t region_bytes = 3ull << 30;
+  CK(hipMalloc(&region, region_bytes));
+  CK(hipMalloc(&counts, 4096ull * P * 4));
+  CK(hipMalloc(&seg, (4096ull * P + 1) * 4));
+  CK(hipMalloc(&ovf, nS * 8));
+  CK(hipMalloc(&novf, 8));
+  uint64_t* partials;
+  CK(hipMalloc(&partials, 1ull << 24));
+
+  auto variant = [&](const char* name, auto kern, int block, int tile, int per_cu) {
+    const uint32_t ntiles = uint32_t((nS + tile - 1) / tile);
+    uint32_t G = uint32_t(ctx.num_cus) * per_cu;
+    if (G > ntiles) G = ntiles;
+    const uint64_t per_g = uint64_t((ntiles + G - 1) / G) * tile;
+    const double ex = double(per_g) / P;
+    uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
+    cap = (cap + 15) & ~uint64_t(15);
+    if (uint64_t(G) * P * cap * 8 > region_bytes) {
+      printf("%s: region too large\n", name);
+      return;
+    }
+    char nm[128];
+    snprintf(nm, sizeof nm, "part1 %s (G=%u cap=%llu)", name, G, (unsigned long long)cap);
+    timeit(nm, [&] {
+      CK(hipMemsetAsync(novf, 0, 8, 0));
+      hipLaunchKernelGGL(kern, dim3(G), dim3(block), 0, 0, v, t.fm, 0u, nR, pl0.fw, P, ntiles, uint32_t(cap), region,
+                         counts, ovf, novf);
+    }, nS * 20.0);
+    unsigned long long h_novf = 0;
+    CK(hipMemcpy(&h_novf, novf, 8, hipMemcpyDeviceToHost));
+    hipLaunchKernelGGL(k_transpose_counts, dim3(1024), dim3(256), 0, 0, counts, G, P, seg);
+    CK(exclusive_scan_u32(&ctx, seg, seg, uint64_t(G) * P, 0));
+    uint32_t splits = 1;
+    if (P < uint32_t(ctx.num_cus) * 2) splits = (uint32_t(ctx.num_cus) * 2 + P - 1) / P;
+    snprintf(nm, sizeof nm, "  probe_seg on it (ovf=%llu)", h_novf);
+    timeit(nm, [&] {
+      hipLaunchKernelGGL((k_rp_probe_seg<true, kDense, false, true>), dim3(P * splits), dim3(kJBlock), 0, 0, region, counts,
+                         seg, G, uint32_t(cap), t.off.as<const uint32_t>(), t.ent.as<const uint2>(), t.fm, 0u, nR,
+                         pl0.W, P, splits, out, nS, nullptr, partials);
+    }, nS * 16.0 + nR * 12.0);
+  };
+  variant("1024x16 (1/CU)", k_rp_part1<1024, 16, 2048>, 1024, 16384, 1);
+  {
+    const uint32_t ntiles = uint32_t((nS + 16383) / 16384), G = 256;
+    const uint32_t cap = 576;
+    auto knob = [&](const char* nm, auto kern) {
+      timeit(nm, [&] { hipLaunchKernelGGL(kern, dim3(G), dim3(1024), 0, 0, v, t.fm, 0u, nR, pl0.fw, P, ntiles, cap,
+                                          region, counts); }, nS * 20.0);
+    };
+    knob("knob full copy", k_part1_knob<0>);
+    CK(hipMemsetAsync(novf, 0, 8, 0));
+    hipLaunchKernelGGL((k_rp_part1<1024, 16, 2048>), dim3(G), dim3(1024), 0, 0, v, t.fm, 0u, nR, pl0.fw, P, ntiles, cap,
+                       region, counts, ovf, novf);
+    hipLaunchKernelGGL(k_transpose_counts, dim3(1024), dim3(256), 0, 0, counts, G, P, seg);
+    CK(exclusive_scan_u32(&ctx, seg, seg, uint64_t(G) * P, 0));
+    auto pk = [&](const char* nm, auto kern) {
+      timeit(nm, [&] { hipLaunchKernelGGL(kern, dim3(P), dim3(1024), 0, 0, region, counts, seg, G, cap,
+                                          t.off.as<const uint32_t>(), t.ent.as<const uint2>(), t.fm, 0u, nR, pl0.W, P,
+                                          1u, out, nS, nullptr, partials); }, nS * 16.0 + nR * 12.0);
+    };
+    pk("probe knob full (dense)", k_probe_knob<0>);
+    pk("probe knob no slice stage", k_probe_knob<1>);
+    pk("probe knob no probe (copy)", k_probe_knob<2>);
+    pk("probe knob no probe no store", k_probe_knob<2 | 4>);
+    pk("probe knob probe agg (no store)", k_probe_knob<4>);
+    pk("probe knob dir lookup only", k_probe_knob<8>);
+    knob("knob no rank atomics", k_part1_knob<1>);
+    knob("knob no staging", k_part1_knob<2>);
+    knob("knob no global stores", k_part1_knob<4>);
+    knob("knob no write-out loop", k_part1_knob<8>);
+    knob("knob no key loads", k_part1_knob<16>);
+    knob("knob only loads+hash+rank+scan", k_part1_knob<2 | 8>);
+    knob("knob only loads+hash+scan", k_part1_knob<1 | 2 | 8>);
+  }
   CK(hipDeviceSynchronize());
   printf("ok\n");
   return 0;
