@@ -67,7 +67,7 @@ struct RelView {
   uint64_t row_base;
 
   __device__ __forceinline__ uint32_t key(uint64_t i) const {
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + i * stride + key_off));
+    return *reinterpret_cast<const uint32_t*>(base + i * stride + key_off);
   }
   __device__ __forceinline__ uint32_t row(uint64_t i) const {
     if (row_off == 0xFFFFFFFFu) return uint32_t(row_base + i);

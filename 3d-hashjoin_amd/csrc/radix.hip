@@ -407,7 +407,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
         e = stage[k];
         p = fw.div(fm.mod(e.x) - lo);
         o = cur[p] + (k - loc[p]);
-        if (o < cap) region[(gbase + p) * cap + o] = e;
+        if (o < cap) region[(gbase + p) * cap + o] = e;  // plain stores: L2 merges the partial lines of a run
       }
       const uint64_t spill = __ballot(v && o >= cap);
       if (spill) {  // wave-aggregated append to the overflow list
