@@ -13,6 +13,12 @@ import torch
 import torch.distributed as dist
 
 
+def _host_staged(group=None) -> bool:
+    """gloo moves host tensors only: device tensors are staged through host memory (the
+    single-GPU rehearsal of the multi-GPU path, bench.py --rehearse)."""
+    return dist.get_backend(group) == "gloo"
+
+
 def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torch.Tensor | None = None,
              group=None) -> torch.Tensor:
     """all_to_all of (n, 2) int32 (key, row) pairs grouped by destination.
@@ -20,6 +26,13 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
     send_counts: int64 tensor [P] on the pairs' device (as written by hj3d_partition).
     Returns the received pairs (a view of recv_buf when it is large enough)."""
     world = dist.get_world_size(group)
+    if _host_staged(group) and send_pairs.is_cuda:
+        rb = recv_buf.cpu() if recv_buf is not None else None
+        got = exchange(send_pairs.cpu(), send_counts.cpu(), rb, group)
+        if recv_buf is not None and recv_buf.shape[0] >= got.shape[0]:
+            recv_buf[: got.shape[0]].copy_(got)
+            return recv_buf[: got.shape[0]]
+        return got.to(send_pairs.device)
     recv_counts = torch.empty_like(send_counts)
     dist.all_to_all_single(recv_counts, send_counts, group=group)
     sc = send_counts.tolist()
@@ -35,12 +48,14 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
 
 def allreduce_sum_u64(values: list[int], device) -> list[int]:
     """Sum u64 counters over ranks (mod 2^64, as the reference's u64 counters would wrap)."""
+    device = "cpu" if _host_staged() else device
     t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in values], dtype=torch.int64, device=device)
     dist.all_reduce(t)
     return [int(x) & ((1 << 64) - 1) for x in t.tolist()]
 
 
 def allreduce_xor_u64(value: int, device) -> int:
+    device = "cpu" if _host_staged() else device
     world = dist.get_world_size()
     t = torch.tensor([value - (1 << 64) if value >= (1 << 63) else value], dtype=torch.int64, device=device)
     out = [torch.zeros_like(t) for _ in range(world)]
@@ -52,6 +67,7 @@ def allreduce_xor_u64(value: int, device) -> int:
 
 
 def allreduce_max(value: float, device) -> float:
+    device = "cpu" if _host_staged() else device
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

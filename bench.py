@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--pmc-json", default=latest_pmc(), help="PMC summary (scripts/pmc_summary.py) for roofline.traffic")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--rehearse", action="store_true",
+                   help="N>1 on ONE GPU: every rank on cuda:0, gloo exchange staged through host memory "
+                        "(checks the multi-GPU code path; the numbers are not a scaling measurement)")
     p.add_argument("--workload", default="B", choices=["B", "C", "E"],
                    help="B: the headline key/FK chaining join (default); C: 3D table on Zipf(0.8) S.a, Nrs plan; "
                         "E: experiment-4 deferred unnesting (Ndu)")
@@ -114,12 +117,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    local = 0 if args.rehearse else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
         from hj3d import dist as hdist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
         if world > 1:
@@ -293,6 +300,7 @@ def main():
             "workload": f"exp1 key/FK plan Csr, |R|={nR} |S|={nS} per GPU, uniform FKs, b={args.b}",
             "plan": "Csr", "R_per_gpu": nR, "S_per_gpu": nS, "num_buckets": nb,
             "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if world > 1 else "single GPU",
+            "rehearsal_one_gpu": bool(args.rehearse),
         },
         "build_ms": build_ms,
         "probe_ms": probe_ms,
