@@ -243,7 +243,8 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   if (t->desc.kind == HJ3D_CHAIN) {
     e = (!ctx->force_direct && build->n >= (ctx->radix_min >> 4) && build->n > 0 && t->nb_local >= 64)
             ? radix_build(ctx, t, *build, ctx->stream)
-            : chain_build(ctx, t, *build, ctx->stream);
+            : hipErrorNotSupported;
+    if (e == hipErrorNotSupported) e = chain_build(ctx, t, *build, ctx->stream);
     if (e == hipSuccess) e = sort_small_buckets(ctx, t, ctx->stream);
   } else {
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
@@ -281,9 +282,10 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   uint64_t* res = ctx->res.as<uint64_t>();
   hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) {
-    if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n)) {
+    e = hipErrorNotSupported;
+    if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n))
       e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);  // times its own kernels
-    } else {
+    if (e == hipErrorNotSupported) {
       PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
       e = (t->desc.kind == HJ3D_CHAIN) ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)
                                        : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);

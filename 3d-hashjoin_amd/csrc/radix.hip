@@ -342,8 +342,9 @@ __device__ __forceinline__ void stage_slice(const uint32_t* __restrict__ off, co
 // (region[(g * P + p) * cap ...]) and its fill cursor in LDS. Per tile: rank per partition (LDS
 // atomics), stage in partition order (LDS), write each partition's run at the cursor. A run that
 // does not fit (skewed probe keys) goes to the overflow list, probed by k_probe_ovf. S is read
-// once instead of twice (histogram + scatter).
-template <int BLOCK, int ROUNDS, int MAXP>
+// once instead of twice (histogram + scatter). IMPLICIT (row id = row_base + index): the stage
+// holds {hash, partition << 16 | tile index} so the write-out needs no second modulo/division.
+template <int BLOCK, int ROUNDS, int MAXP, bool IMPLICIT>
 __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                     uint32_t P, uint32_t ntiles, uint32_t cap,
                                                     uint2* __restrict__ region, uint32_t* __restrict__ counts,
@@ -351,6 +352,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
   constexpr int TILE = BLOCK * ROUNDS;
   constexpr int TBITS = __builtin_ctz(TILE);
   static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 16), "tile must be a power of two");
+  static_assert(MAXP < (1 << 16), "partition ids are packed into 16 bits");
   __shared__ uint2 stage[TILE];
   __shared__ uint32_t loc[MAXP + 1];  // tile counts, then tile-local run starts (loc[P] = tile size)
   __shared__ uint32_t cur[MAXP];      // region fill of each partition
@@ -388,8 +390,9 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
 #pragma unroll
     for (int j = 0; j < ROUNDS; ++j) {
       if (rk[j] == kInvalid) continue;
-      const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
-      stage[loc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], r.row(i));
+      const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
+      const uint32_t y = IMPLICIT ? (((rk[j] >> TBITS) << 16) | li) : r.row(base + li);
+      stage[loc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
     }
     __syncthreads();
     const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;  // next tile: loads in flight
@@ -405,7 +408,12 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
       uint32_t o = 0, p = 0;
       if (v) {
         e = stage[k];
-        p = fw.div(fm.mod(e.x) - lo);
+        if (IMPLICIT) {
+          p = e.y >> 16;
+          e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+        } else {
+          p = fw.div(fm.mod(e.x) - lo);
+        }
         o = cur[p] + (k - loc[p]);
         if (o < cap) region[(gbase + p) * cap + o] = e;  // plain stores: L2 merges the partial lines of a run
       }
@@ -422,6 +430,118 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
     for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] += loc[p + 1] - loc[p];
     __syncthreads();
   }
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
+}
+
+// Software-pipelined variant of k_rp_part1: per iteration, the rank atomics of tile t run in the
+// same phase as the write-out of tile t-1 (its staged runs) and the key loads of tile t+1, with
+// double-buffered per-tile offsets; 4 barriers per tile instead of 6.
+template <int BLOCK, int ROUNDS, int MAXP, bool IMPLICIT>
+__global__ __launch_bounds__(BLOCK) void k_rp_part1p(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                     uint32_t P, uint32_t ntiles, uint32_t cap,
+                                                     uint2* __restrict__ region, uint32_t* __restrict__ counts,
+                                                     uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
+  constexpr int TILE = BLOCK * ROUNDS;
+  constexpr int TBITS = __builtin_ctz(TILE);
+  static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 16), "tile must be a power of two");
+  static_assert(MAXP < (1 << 16), "partition ids are packed into 16 bits");
+  __shared__ uint2 stage[TILE];
+  __shared__ uint32_t lbuf[2][MAXP + 1];  // per tile: counts, then run starts (lbuf[.][P] = tile size)
+  __shared__ uint32_t cur[MAXP];
+  __shared__ uint32_t wsum[BLOCK / kWave];
+  const uint64_t gbase = uint64_t(blockIdx.x) * P;
+  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) {
+    cur[p] = 0;
+    lbuf[0][p] = 0;
+    lbuf[1][p] = 0;
+  }
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint32_t h[ROUNDS], rk[ROUNDS];
+#pragma unroll
+  for (int j = 0; j < ROUNDS; ++j) {
+    const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
+    h[j] = i < r.n ? r.key(i) : 0u;
+  }
+  __syncthreads();
+  uint32_t prev_m = 0, prev_base = 0;  // staged tile t-1 (prev_m == 0: none)
+  int cb = 0;                           // lbuf[cb]: tile t, lbuf[cb ^ 1]: tile t-1
+  for (uint32_t tile = blockIdx.x;; tile += gridDim.x) {
+    const bool have = tile < ntiles;
+    const uint64_t base = uint64_t(tile) * TILE;
+    uint32_t* lc = lbuf[cb];
+    const uint32_t* lp = lbuf[cb ^ 1];
+    // ---- phase A: rank tile t | write out tile t-1 | load keys of tile t+1
+    if (have) {
+#pragma unroll
+      for (int j = 0; j < ROUNDS; ++j) {
+        const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
+        h[j] = murmur32(h[j]);
+        const uint32_t bl = fm.mod(h[j]) - lo;
+        if (i < r.n && bl < nbl) {
+          const uint32_t part = fw.div(bl);
+          rk[j] = (part << TBITS) | atomicAdd(&lc[part], 1u);
+        } else {
+          rk[j] = kInvalid;
+        }
+      }
+    }
+    for (uint32_t k0 = 0; k0 < prev_m; k0 += BLOCK) {
+      const uint32_t k = k0 + threadIdx.x;
+      const bool v = k < prev_m;
+      uint2 e = make_uint2(0, 0);
+      uint32_t o = 0, p = 0;
+      if (v) {
+        e = stage[k];
+        if (IMPLICIT) {
+          p = e.y >> 16;
+          e.y = uint32_t(r.row_base) + prev_base + (e.y & 0xFFFFu);
+        } else {
+          p = fw.div(fm.mod(e.x) - lo);
+        }
+        o = cur[p] + (k - lp[p]);
+        if (o < cap) region[(gbase + p) * cap + o] = e;
+      }
+      const uint64_t spill = __ballot(v && o >= cap);
+      if (spill) {
+        const int leader = __ffsll((unsigned long long)spill) - 1;
+        unsigned long long b0 = 0;
+        if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
+        b0 = __shfl(b0, leader, kWave);
+        if (v && o >= cap) ovf[b0 + __popcll(spill & lt)] = e;
+      }
+    }
+    uint32_t hn[ROUNDS];
+    const uint64_t nbase = base + uint64_t(gridDim.x) * TILE;
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
+      hn[j] = (have && i < r.n) ? r.key(i) : 0u;
+    }
+    __syncthreads();
+    // ---- phase B: advance the region cursors past tile t-1; scan tile t's counts
+    if (prev_m)
+      for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] += lp[p + 1] - lp[p];
+    if (!have) break;
+    const uint32_t m = lds_excl_scan<BLOCK>(lc, P, wsum);  // ends with a barrier
+    if (threadIdx.x == 0) lc[P] = m;
+    // ---- phase C: stage tile t in partition order; clear tile t-1's offsets for tile t+1
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
+      const uint32_t y = IMPLICIT ? (((rk[j] >> TBITS) << 16) | li) : r.row(base + li);
+      stage[lc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
+    }
+    for (uint32_t p = threadIdx.x; p <= P; p += BLOCK) lbuf[cb ^ 1][p] = 0;
+    __syncthreads();
+    prev_m = m;
+    prev_base = uint32_t(base);
+    cb ^= 1;
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) h[j] = hn[j];
+  }
+  __syncthreads();
   for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
 }
 
@@ -637,6 +757,7 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = t->ent.ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
   const Plan pl = plan_for(nbl, kBuildSlice, r.n);
+  if (pl.P > kMaxParts) return hipErrorNotSupported;  // > 2048 x 16384 buckets: the direct build
   if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
@@ -704,6 +825,9 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
   uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
   if (W < 64) W = 64;
+  // more than kMaxParts slices: wider slices that no longer fit LDS (probed through L2 by the
+  // non-fitting kernel, still one bucket range per workgroup)
+  if ((uint64_t(nbl) + W - 1) / W > kMaxParts) W = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
   SegLaunch L;
   L.t = t;
   L.pl = plan_for(nbl, W, r.n);
@@ -747,8 +871,12 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   const RelView v = view_of(r);
   {
     PhaseTimer tm(ctx, HJ3D_T_SCATTER);
-    hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
-                       uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
+    if (r.row_off == HJ3D_ROW_IMPLICIT)
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
+                         uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
+    else
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, false>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
+                         uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
   }
   hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, L.G, P, seg);
   if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;

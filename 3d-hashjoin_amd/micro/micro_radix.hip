@@ -326,7 +326,10 @@ int main(int argc, char** argv) {
                          pl0.W, P, splits, out, nS, nullptr, partials);
     }, nS * 16.0 + nR * 12.0);
   };
-  variant("1024x16 (1/CU)", k_rp_part1<1024, 16, 2048>, 1024, 16384, 1);
+  variant("1024x16 (1/CU)", k_rp_part1<1024, 16, 2048, true>, 1024, 16384, 1);
+  variant("pipelined 1024x16", k_rp_part1p<1024, 16, 2048, true>, 1024, 16384, 1);
+  variant("pipelined 1024x8", k_rp_part1p<1024, 8, 2048, true>, 1024, 8192, 1);
+  variant("pipelined 512x16", k_rp_part1p<512, 16, 2048, true>, 512, 8192, 1);
   {
     const uint32_t ntiles = uint32_t((nS + 16383) / 16384), G = 256;
     const uint32_t cap = 576;
@@ -336,7 +339,7 @@ int main(int argc, char** argv) {
     };
     knob("knob full copy", k_part1_knob<0>);
     CK(hipMemsetAsync(novf, 0, 8, 0));
-    hipLaunchKernelGGL((k_rp_part1<1024, 16, 2048>), dim3(G), dim3(1024), 0, 0, v, t.fm, 0u, nR, pl0.fw, P, ntiles, cap,
+    hipLaunchKernelGGL((k_rp_part1<1024, 16, 2048, true>), dim3(G), dim3(1024), 0, 0, v, t.fm, 0u, nR, pl0.fw, P, ntiles, cap,
                        region, counts, ovf, novf);
     hipLaunchKernelGGL(k_transpose_counts, dim3(1024), dim3(256), 0, 0, counts, G, P, seg);
     CK(exclusive_scan_u32(&ctx, seg, seg, uint64_t(G) * P, 0));
