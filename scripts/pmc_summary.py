@@ -29,7 +29,10 @@ KERNELS = ("k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe", "k_rp_sc
 def short(name):
     for k in KERNELS:
         if k in name:
-            return k
+            # template instantiations of one kernel are kept apart (e.g. the LDS-slice and the
+            # L2-slice k_rp_probe_seg); the heaviest is reported under the plain name below
+            i = name.find(k) + len(k)
+            return k + (name[i:name.find(">", i) + 1] if i < len(name) and name[i] == "<" else "")
     return None
 
 
@@ -51,11 +54,17 @@ def main():
                 if k is None:
                     continue
                 vals[(k, r["Counter_Name"])].append((int(r["Grid_Size"]), float(r["Counter_Value"])))
-    kern = {}
+    per = {}
     for (k, c), lst in vals.items():
         gmax = max(g for g, _ in lst)
         v = statistics.median([x for g, x in lst if g == gmax])
-        kern.setdefault(k, {"grid_size": gmax})[c] = v
+        per.setdefault(k, {"grid_size": gmax})[c] = v
+    # one entry per kernel name: the instantiation that moved the most bytes
+    kern = {}
+    for k, d in per.items():
+        base = k.split("<")[0]
+        if base not in kern or d.get("FETCH_SIZE", 0) > kern[base].get("FETCH_SIZE", 0):
+            kern[base] = dict(d, instantiation=k)
     for k, d in kern.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * 2
