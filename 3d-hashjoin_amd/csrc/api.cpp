@@ -241,11 +241,12 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
   if (t->desc.kind == HJ3D_CHAIN) {
+    bool sorted = false;
     e = (!ctx->force_direct && build->n >= (ctx->radix_min >> 4) && build->n > 0 && t->nb_local >= 64)
-            ? radix_build(ctx, t, *build, ctx->stream)
+            ? radix_build(ctx, t, *build, ctx->stream, &sorted)
             : hipErrorNotSupported;
     if (e == hipErrorNotSupported) e = chain_build(ctx, t, *build, ctx->stream);
-    if (e == hipSuccess) e = sort_small_buckets(ctx, t, ctx->stream);
+    if (e == hipSuccess && !sorted) e = sort_small_buckets(ctx, t, ctx->stream);
   } else {
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
                                                   : hipErrorNotSupported;

@@ -97,7 +97,8 @@ hipError_t radix_sort_pairs(hj3d_ctx* ctx, uint32_t* k0, uint32_t* v0, uint32_t*
                             int bits, hipStream_t s, bool* in_alt = nullptr);
 // radix.hip: partitioned (LDS-slice) build / probe of the chaining table
 bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
-hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+// rows_sorted (optional): set when the small buckets already come out sorted by row.
+hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, bool* rows_sorted = nullptr);
 // after every chaining build: buckets of <= 32 entries sorted by row (single-pass probe order)
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,

@@ -202,6 +202,77 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
   }
 }
 
+// One workgroup per build partition of kBuildSlice2 buckets: count (LDS atomics), scan, then rank
+// every pair into an LDS stage in bucket order, sort the small buckets by row in LDS, and write
+// the partition's CSR slice out coalesced. A partition with more pairs than the stage holds
+// (skewed keys) scatters to HBM instead and sorts its small buckets there.
+constexpr uint32_t kBuildSlice2 = 8192;
+constexpr uint32_t kBuildStage = 15000;
+__global__ __launch_bounds__(kJBlock) void k_rp_build2(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                       FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
+                                                       uint32_t* __restrict__ off, uint2* __restrict__ ent) {
+  __shared__ uint32_t cnt[kBuildSlice2];
+  __shared__ uint2 stage[kBuildStage];
+  __shared__ uint32_t wsum[kJBlock / kWave];
+  const uint32_t p = blockIdx.x;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, nbl - b0);
+  const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
+  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
+  __syncthreads();
+  for (uint32_t i0 = s0; i0 < s1; i0 += kJBlock * 4) {
+    uint32_t h[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * kJBlock + threadIdx.x;
+      h[u] = i < s1 ? pairs[i].x : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (i0 + u * kJBlock + threadIdx.x < s1) atomicAdd(&cnt[fm.mod(h[u]) - lo - b0], 1u);
+  }
+  __syncthreads();
+  lds_excl_scan(cnt, nbs, wsum);
+  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+  if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
+  __syncthreads();
+  const bool staged = m <= kBuildStage;
+  for (uint32_t i0 = s0; i0 < s1; i0 += kJBlock * 4) {
+    uint2 e[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint32_t i = i0 + u * kJBlock + threadIdx.x;
+      e[u] = i < s1 ? pairs[i] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (i0 + u * kJBlock + threadIdx.x >= s1) continue;
+      const uint32_t pos = atomicAdd(&cnt[fm.mod(e[u].x) - lo - b0], 1u);  // cnt[b] walks to b's end
+      if (staged) stage[pos] = e[u];
+      else ent[s0 + pos] = e[u];
+    }
+  }
+  __syncthreads();
+  // buckets of 2..kSortedMax entries sorted by row; bucket k = [k ? cnt[k-1] : 0, cnt[k])
+  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) {
+    const uint32_t bs = k ? cnt[k - 1] : 0u, n = cnt[k] - bs;
+    if (n < 2 || n > kSortedMax) continue;
+    uint2* E = staged ? stage + bs : ent + s0 + bs;
+    for (uint32_t q = 1; q < n; ++q) {
+      const uint2 x = E[q];
+      uint32_t j = q;
+      while (j > 0 && E[j - 1].y > x.y) {
+        E[j] = E[j - 1];
+        --j;
+      }
+      E[j] = x;
+    }
+  }
+  if (!staged) return;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < m; k += kJBlock) ent[s0 + k] = stage[k];
+}
+
 enum Mode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
 
 // Reference comparison count and match of one probe against bucket entries [s, s+n) of `E`
@@ -302,22 +373,24 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
   }
 }
 
-// Copy the table slice of buckets [b0, b0 + nbs) (directory rebased to 0 + entries) into LDS;
-// every thread keeps kStage loads in flight before writing LDS.
+// Copy the table slice of buckets [b0, b0 + nbs) into LDS: directory word k = (start of bucket k
+// relative to the slice) << 16 | (its entry count) (both < 2^16: a slice holds < 18432 entries),
+// then the entries. Every thread keeps kStage loads in flight before writing LDS.
 __device__ __forceinline__ void stage_slice(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
-                                            uint32_t nbs, uint32_t e0, uint32_t ne, uint32_t* loff, uint2* lent) {
+                                            uint32_t nbs, uint32_t e0, uint32_t ne, uint32_t* ldir, uint2* lent) {
   constexpr int kStage = 8;
-  for (uint32_t k0 = threadIdx.x; k0 <= nbs; k0 += kJBlock * kStage) {
-    uint32_t v[kStage];
+  for (uint32_t k0 = threadIdx.x; k0 < nbs; k0 += kJBlock * kStage) {
+    uint32_t v[kStage], w[kStage];
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
-      v[u] = k <= nbs ? off[b0 + k] : 0u;
+      v[u] = k < nbs ? off[b0 + k] : 0u;
+      w[u] = k < nbs ? off[b0 + k + 1] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
-      if (k <= nbs) loff[k] = v[u] - e0;
+      if (k < nbs) ldir[k] = ((v[u] - e0) << 16) | (w[u] - v[u]);
     }
   }
   const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
@@ -635,8 +708,8 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
       const uint32_t bl = fm.mod(hv) - lo - b0;
       const uint64_t i = obase + j * 64 + lane;
       if (FITS) {
-        const uint32_t s = loff[bl];
-        probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        const uint32_t d = loff[bl];
+        probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, d >> 16, d & 0xFFFFu, acc, i, out, out_cap, cnt);
       } else {
         const uint32_t s = off[b0 + bl];
         probe_bucket<UNIQUE, MODE, CK>(hv, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
@@ -751,19 +824,28 @@ bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n
          t->nb_local >= 64 && n_probe < (1ull << 32);
 }
 
-hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, bool* rows_sorted) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;
+  if (rows_sorted) *rows_sorted = false;
   if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = t->ent.ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
-  const Plan pl = plan_for(nbl, kBuildSlice, r.n);
+  // staged build (8192-bucket slices, small buckets sorted in LDS) while the fill leaves room in
+  // the stage; else the 16384-bucket counting build; beyond 2048 slices the direct build
+  const double fill = nbl ? double(r.n) / nbl : 0.0;
+  const bool staged = fill * kBuildSlice2 * 1.25 <= kBuildStage && (uint64_t(nbl) + kBuildSlice2 - 1) / kBuildSlice2 <= kMaxParts;
+  const Plan pl = plan_for(nbl, staged ? kBuildSlice2 : kBuildSlice, r.n);
   if (pl.P > kMaxParts) return hipErrorNotSupported;  // > 2048 x 16384 buckets: the direct build
   if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
-  if (nbl) {
+  if (nbl && staged) {
+    hipLaunchKernelGGL(k_rp_build2, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo),
+                       nbl, pl.W, t->off.as<uint32_t>(), t->ent.as<uint2>());
+    if (rows_sorted) *rows_sorted = true;
+  } else if (nbl) {
     hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
                        pl.W, t->off.as<uint32_t>(), t->ent.as<uint2>());
   } else {

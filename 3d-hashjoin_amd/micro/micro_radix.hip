@@ -198,15 +198,15 @@ __global__ __launch_bounds__(kJBlock) void k_probe_knob(const uint2* __restrict_
         acc[0] += bl;
         if (!(KNOB & 4)) __builtin_nontemporal_store(cur[j] ^ bl, reinterpret_cast<uint64_t*>(out + i));
       } else if (KNOB & 4) {
-        const uint32_t s = loff[bl];
-        probe_bucket<true, kAgg, false>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        const uint32_t d = loff[bl];
+        probe_bucket<true, kAgg, false>(hv, row, lent, d >> 16, d & 0xFFFFu, acc, i, out, out_cap, cnt);
       } else if (KNOB & 8) {  // directory lookup only
         const uint32_t s = loff[bl], e = loff[bl + 1];
         acc[0] += s ^ e;
         __builtin_nontemporal_store(cur[j] ^ (uint64_t(s) << 32 | e), reinterpret_cast<uint64_t*>(out + i));
       } else {
-        const uint32_t s = loff[bl];
-        probe_bucket<true, kDense, false>(hv, row, lent, s, loff[bl + 1] - s, acc, i, out, out_cap, cnt);
+        const uint32_t d = loff[bl];
+        probe_bucket<true, kDense, false>(hv, row, lent, d >> 16, d & 0xFFFFu, acc, i, out, out_cap, cnt);
       }
     }
     r = nr_;
