@@ -281,7 +281,8 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
     return fail(ctx, HJ3D_EINVAL, "hj3d_probe: UNNEST needs a nested table");
   PhaseTimer tm(ctx, HJ3D_T_PROBE);
   uint64_t* res = ctx->res.as<uint64_t>();
-  hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+  const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
+  hipError_t e = acc ? hipSuccess : hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) {
     e = hipErrorNotSupported;
     if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n))
@@ -296,7 +297,11 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   ctx->res_flags = flags;
   ctx->res_dense = (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
   ctx->res_cap = (flags & HJ3D_PROBE_EMIT) ? out_cap : ~0ull;
-  ctx->res_nprobe = probe->n;
+  ctx->res_nprobe = acc ? ctx->res_nprobe + probe->n : probe->n;
+  // dense output: each call needs one slot per probe tuple of its own buffer
+  const bool ovf_dense = ctx->res_dense && (flags & HJ3D_PROBE_EMIT) && probe->n > out_cap;
+  ctx->res_overflow = (acc && ctx->res_overflow) || ovf_dense;
+  ctx->res_accumulated = acc;
   return from_hip(ctx, e, "hj3d_probe");
 }
 
@@ -315,8 +320,8 @@ hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out) {
   out->sum_c = h[6];
   out->sum_h = h[7];
   out->xor_h = h[8];
-  const uint64_t need = ctx->res_dense ? ctx->res_nprobe : out->n_out;
-  if ((ctx->res_flags & HJ3D_PROBE_EMIT) && need > ctx->res_cap) return fail(ctx, HJ3D_EOVERFLOW, "hj3d_probe: output buffer too small");
+  const bool ovf = ctx->res_dense ? ctx->res_overflow : (!ctx->res_accumulated && out->n_out > ctx->res_cap);
+  if ((ctx->res_flags & HJ3D_PROBE_EMIT) && ovf) return fail(ctx, HJ3D_EOVERFLOW, "hj3d_probe: output buffer too small");
   return HJ3D_OK;
 }
 

@@ -59,7 +59,9 @@ struct hj3d_ctx {
   uint32_t res_flags = 0;     // flags of the last probe (overflow check in hj3d_probe_result)
   bool res_dense = false;     // last probe emitted one slot per probe tuple
   uint64_t res_cap = ~0ull;   // output capacity of the last probe
-  uint64_t res_nprobe = 0;    // probe tuples of the last probe
+  uint64_t res_nprobe = 0;    // probe tuples of the last probe (strand, when accumulating)
+  bool res_overflow = false;  // a dense-output probe of the strand had fewer slots than tuples
+  bool res_accumulated = false;
   // phase timers
   bool timing = false;
   bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
@@ -145,9 +147,10 @@ enum ScratchSlot {
 
 // Per-block result partials: kernels store their block totals (block_store) to
 // partials[block * nf ...]; reduce_partials adds the column sums into res (stream-ordered).
-// set0 != ~0: res[0] is set to set0 instead of accumulated (scanned-tuple count known on the host).
+// set0 != ~0: res[0] is set to set0 (+ *base0 when given) instead of accumulated (the scanned-tuple
+// count is known on the host; base0 = res[0] before this probe, for accumulating probes).
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
-                           uint64_t set0 = ~0ull);
+                           uint64_t set0 = ~0ull, const uint64_t* base0 = nullptr);
 
 // Event spans on the context stream when timing is enabled (hj3d_ctx_timer): a PhaseTimer
 // brackets whatever is enqueued during its lifetime.

@@ -943,12 +943,15 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   if (L.splits > L.G) L.splits = L.G;
   const uint32_t nblocks = P * L.splits;
   // one row per probe workgroup + one extra row accumulated with atomics by the non-fitting kernel
-  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 1) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
   if ((e = hipMemsetAsync(partials + uint64_t(nblocks) * kProbeFields, 0, kProbeFields * sizeof(uint64_t), s)) !=
       hipSuccess)
     return e;
+  // n_probe of earlier accumulated probes (the reduction below sets res[0] = that + r.n)
+  uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
+  if ((e = hipMemcpyAsync(base0, res, sizeof(uint64_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
   const RelView v = view_of(r);
   {
@@ -982,7 +985,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
-  return reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n);
+  return reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n, base0);
 }
 
 }  // namespace hj3d

@@ -137,7 +137,8 @@ hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t
 // thread folds whole rows (coalesced 8*NF-byte reads), then one block reduction per field.
 template <int NF, int NXOR>
 __global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __restrict__ part, uint32_t nblocks,
-                                                          uint64_t* __restrict__ res, uint64_t set0) {
+                                                          uint64_t* __restrict__ res, uint64_t set0,
+                                                          const uint64_t* __restrict__ base0) {
   __shared__ uint64_t red[16][NF];
   uint64_t acc[NF];
 #pragma unroll
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __rest
     const bool x = f >= NF - NXOR;
     uint64_t a = 0;
     for (int w = 0; w < 16; ++w) a = x ? (a ^ red[w][f]) : (a + red[w][f]);
-    if (f == 0 && set0 != ~0ull) res[0] = set0;
+    if (f == 0 && set0 != ~0ull) res[0] = set0 + (base0 ? *base0 : 0ull);
     else res[f] = x ? (res[f] ^ a) : (res[f] + a);
   }
 }
@@ -174,9 +175,10 @@ __global__ __launch_bounds__(1024) void k_reduce_partials(const uint64_t* __rest
 }  // namespace
 
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
-                           uint64_t set0) {
+                           uint64_t set0, const uint64_t* base0) {
   if (nf != kProbeFields || nxor != 1) return hipErrorInvalidValue;  // the one shape in use
-  hipLaunchKernelGGL((k_reduce_partials<kProbeFields, 1>), dim3(1), dim3(1024), 0, s, partials, nblocks, res, set0);
+  hipLaunchKernelGGL((k_reduce_partials<kProbeFields, 1>), dim3(1), dim3(1024), 0, s, partials, nblocks, res, set0,
+                     base0);
   return hipGetLastError();
 }
 

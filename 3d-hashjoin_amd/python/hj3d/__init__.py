@@ -23,7 +23,7 @@ HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "hj3d.h")
 HJ3D_OK, HJ3D_EINVAL, HJ3D_ENOMEM, HJ3D_EDEVICE, HJ3D_EUNSUPPORTED, HJ3D_EOVERFLOW = range(6)
 HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
-PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM = 0x1, 0x2, 0x4, 0x8
+PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX = 1, 2, 3
 
@@ -240,11 +240,12 @@ class Context:
 
     # ---- probes ----
     def probe(self, table: "Table", rel: Rel, unique: bool = False, unnest: bool = False, out=None,
-              fetch: bool = True, checksum: bool = True) -> Optional[ProbeResult]:
+              fetch: bool = True, checksum: bool = True, accumulate: bool = False) -> Optional[ProbeResult]:
         """One probe strand. checksum=False skips the order-independent output checksums (a
-        verification aid the reference does not compute); all counters stay exact."""
+        verification aid the reference does not compute); all counters stay exact.
+        accumulate=True adds to the previous probe's result (one strand issued in chunks)."""
         flags = (PROBE_UNIQUE if unique else 0) | (PROBE_UNNEST if unnest else 0) | \
-                (PROBE_CHECKSUM if checksum else 0)
+                (PROBE_CHECKSUM if checksum else 0) | (PROBE_ACCUMULATE if accumulate else 0)
         ptr, cap = None, 0
         if out is not None:
             flags |= PROBE_EMIT

@@ -46,6 +46,28 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
     return out
 
 
+def exchange_async(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torch.Tensor, group=None):
+    """exchange() with the pair all-to-all left in flight: returns (received view, work handle).
+    The counts are exchanged synchronously (the host needs the split sizes). work.wait() makes
+    the current stream wait for the pairs; with gloo (host-staged rehearsal) it is synchronous and
+    the handle is None."""
+    if _host_staged(group):
+        return exchange(send_pairs, send_counts, recv_buf, group), None
+    world = dist.get_world_size(group)
+    recv_counts = torch.empty_like(send_counts)
+    dist.all_to_all_single(recv_counts, send_counts, group=group)
+    sc = send_counts.tolist()
+    rc = recv_counts.tolist()
+    assert len(sc) == world
+    total = int(sum(rc))
+    if recv_buf.shape[0] < total:
+        raise RuntimeError(f"exchange: receive buffer holds {recv_buf.shape[0]} pairs, {total} arrive")
+    out = recv_buf[:total]
+    work = dist.all_to_all_single(out, send_pairs[: int(sum(sc))], output_split_sizes=rc, input_split_sizes=sc,
+                                  group=group, async_op=True)
+    return out, work
+
+
 def allreduce_sum_u64(values: list[int], device) -> list[int]:
     """Sum u64 counters over ranks (mod 2^64, as the reference's u64 counters would wrap)."""
     device = "cpu" if _host_staged() else device

@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--pmc-json", default=latest_pmc(), help="PMC summary (scripts/pmc_summary.py) for roofline.traffic")
     p.add_argument("--json-out", default=None)
+    p.add_argument("--chunks", type=int, default=4,
+                   help="N>1: S is exchanged in this many chunks, each chunk's all-to-all overlapping the "
+                        "previous chunk's probe")
     p.add_argument("--rehearse", action="store_true",
                    help="N>1 on ONE GPU: every rank on cuda:0, gloo exchange staged through host memory "
                         "(checks the multi-GPU code path; the numbers are not a scaling measurement)")
@@ -160,13 +163,26 @@ def main():
         sendR = torch.empty((nR, 2), dtype=torch.int32, device=dev)
         sendS = torch.empty((nS, 2), dtype=torch.int32, device=dev)
         cntR = torch.zeros(world, dtype=torch.int64, device=dev)
-        cntS = torch.zeros(world, dtype=torch.int64, device=dev)
+        C = max(1, args.chunks)
+        sb = [nS * c // C for c in range(C + 1)]
+        relS_c = [hj3d.Rel(S[sb[c]:sb[c + 1]], key_word=1, row_base=rank * nS + sb[c]) for c in range(C)]
+        cntS = torch.zeros((C, world), dtype=torch.int64, device=dev)
         recvR = torch.empty((int(nR * slack) + 4096, 2), dtype=torch.int32, device=dev)
         recvS = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev)
         out = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev) if emit else None
     torch.cuda.synchronize()
 
     state = {}
+
+    def probe_chunk(pend, ooff, first):
+        rS, work = pend
+        if work is not None:
+            work.wait()
+        n = rS.shape[0]
+        ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True,
+                  out=out[ooff:ooff + n] if out is not None else None, fetch=False,
+                  checksum=state.get("ck", False), accumulate=not first)
+        return ooff + n
 
     def step(ev):
         ev[0].record()
@@ -179,11 +195,19 @@ def main():
             rR = hdist.exchange(sendR, cntR, recvR)
             table.build(hj3d.Rel(rR, key_word=0, row_word=1))
             ev[1].record()
-            ctx.partition(relS, nb, world, sendS, cntS)
-            rS = hdist.exchange(sendS, cntS, recvS)
-            state["probe_n"] = rS.shape[0]
-            ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True, out=out, fetch=False,
-                      checksum=state.get("ck", False))
+            # S in C chunks: partition chunk c, start its all-to-all, then probe chunk c-1 while
+            # chunk c is in flight (results accumulate into one probe strand)
+            roff, ooff, pend, first = 0, 0, None, True
+            for c in range(C):
+                ctx.partition(relS_c[c], nb, world, sendS[sb[c]:sb[c + 1]], cntS[c])
+                rS, work = hdist.exchange_async(sendS[sb[c]:sb[c + 1]], cntS[c], recvS[roff:])
+                roff += rS.shape[0]
+                if pend is not None:
+                    ooff = probe_chunk(pend, ooff, first)
+                    first = False
+                pend = (rS, work)
+            ooff = probe_chunk(pend, ooff, first)
+            state["probe_n"] = roff
         ev[2].record()
 
     def events():
@@ -253,7 +277,8 @@ def main():
     #   k_rp_probe_seg  n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
     #                                                    the table slices (entries + directory) once
     # (N > 1: the probe side is the received pair array, 8 B per tuple.)
-    n = probe_n_local
+    launches = 1 if world == 1 else max(1, args.chunks)
+    n = probe_n_local / launches  # probe tuples per kernel launch
     tuple_bytes = 12 if world == 1 else 8
     alg = {
         "k_rp_part1": n * (tuple_bytes + 8),
@@ -280,8 +305,8 @@ def main():
         for k in kernels:
             if k in pmc:
                 kernels[k]["traffic"] = pmc[k].get("traffic_bytes_per_launch")
-    # the whole probe phase (hist + scan + scatter + probe) against the plan's 28 B per probe
-    phase_alg = n * (tuple_bytes + 8 + (8 if emit else 0))
+    # the whole probe phase (partition + probe; N > 1: + exchange) against the plan's 28 B per probe
+    phase_alg = probe_n_local * (tuple_bytes + 8 + (8 if emit else 0))
 
     line = {
         "metric": METRIC,
@@ -300,6 +325,7 @@ def main():
             "workload": f"exp1 key/FK plan Csr, |R|={nR} |S|={nS} per GPU, uniform FKs, b={args.b}",
             "plan": "Csr", "R_per_gpu": nR, "S_per_gpu": nS, "num_buckets": nb,
             "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if world > 1 else "single GPU",
+            "exchange_chunks": (max(1, args.chunks) if world > 1 else None),
             "rehearsal_one_gpu": bool(args.rehearse),
         },
         "build_ms": build_ms,

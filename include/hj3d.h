@@ -84,6 +84,8 @@ typedef struct {
 #define HJ3D_PROBE_UNIQUE 0x1u /* IsBuildKeyUnique: stop at the first match (algebra.hh:653-655) */
 #define HJ3D_PROBE_UNNEST 0x2u /* nested table: expand main + sub-chain (AlgUnnestHt)           */
 #define HJ3D_PROBE_EMIT   0x4u /* write output tuples to out_dev (else aggregate only)          */
+#define HJ3D_PROBE_ACCUMULATE 0x10u /* add to the result slot of the previous probe instead of
+                                       restarting it (one probe strand issued in chunks) */
 #define HJ3D_PROBE_CHECKSUM 0x8u /* fold sum_a/sum_b/sum_h/xor_h over the output (verification;
                                     the reference itself only counts); counts are always exact */
 

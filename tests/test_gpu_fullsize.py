@@ -189,3 +189,33 @@ def test_large_table_beyond_partition_fanout(ctx):
     finally:
         ctx.force_direct(False)
     assert d["out"] == got["out"] and d["c_cmp"] == got["c_cmp"]
+
+
+@pytest.mark.parametrize("path", ["radix", "direct"])
+def test_probe_in_chunks_accumulates(ctx, path):
+    """One probe strand issued as 4 chunk probes with HJ3D_PROBE_ACCUMULATE (the multi-GPU
+    pipeline does this) gives the counters and output of the single probe."""
+    import torch
+    import hj3d
+    nR, nS = 2_000_000, 10_000_000
+    R, S = make_rel(ctx, nR, nS)
+    t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nR)
+    if path == "direct":
+        ctx.force_direct(True)
+    try:
+        t.build(hj3d.Rel(R, 0))
+        one = ctx.probe(t, hj3d.Rel(S, 1), unique=True)
+        out = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+        b = [0, 1_000_000, 4_000_000, 4_500_000, nS]
+        for c in range(4):
+            lo, hi = b[c], b[c + 1]
+            ctx.probe(t, hj3d.Rel(S[lo:hi], 1, row_base=lo), unique=True, out=out[lo:hi], fetch=False,
+                      accumulate=c > 0)
+        got = ctx.probe_result()
+    finally:
+        ctx.force_direct(False)
+    assert not got.overflow
+    assert (got.n_probe, got.n_matched, got.n_out, got.n_cmps) == (one.n_probe, one.n_matched, one.n_out, one.n_cmps)
+    assert (got.sum_a, got.sum_b, got.sum_h, got.xor_h) == (one.sum_a, one.sum_b, one.sum_h, one.xor_h)
+    rows = out[:, 0].sort().values
+    assert torch.equal(rows, torch.arange(nS, device="cuda", dtype=torch.int32))
