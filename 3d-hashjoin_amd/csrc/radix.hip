@@ -506,118 +506,6 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
   for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
 }
 
-// Software-pipelined variant of k_rp_part1: per iteration, the rank atomics of tile t run in the
-// same phase as the write-out of tile t-1 (its staged runs) and the key loads of tile t+1, with
-// double-buffered per-tile offsets; 4 barriers per tile instead of 6.
-template <int BLOCK, int ROUNDS, int MAXP, bool IMPLICIT>
-__global__ __launch_bounds__(BLOCK) void k_rp_part1p(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
-                                                     uint32_t P, uint32_t ntiles, uint32_t cap,
-                                                     uint2* __restrict__ region, uint32_t* __restrict__ counts,
-                                                     uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
-  constexpr int TILE = BLOCK * ROUNDS;
-  constexpr int TBITS = __builtin_ctz(TILE);
-  static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 16), "tile must be a power of two");
-  static_assert(MAXP < (1 << 16), "partition ids are packed into 16 bits");
-  __shared__ uint2 stage[TILE];
-  __shared__ uint32_t lbuf[2][MAXP + 1];  // per tile: counts, then run starts (lbuf[.][P] = tile size)
-  __shared__ uint32_t cur[MAXP];
-  __shared__ uint32_t wsum[BLOCK / kWave];
-  const uint64_t gbase = uint64_t(blockIdx.x) * P;
-  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) {
-    cur[p] = 0;
-    lbuf[0][p] = 0;
-    lbuf[1][p] = 0;
-  }
-  const int lane = threadIdx.x & 63;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  uint32_t h[ROUNDS], rk[ROUNDS];
-#pragma unroll
-  for (int j = 0; j < ROUNDS; ++j) {
-    const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
-    h[j] = i < r.n ? r.key(i) : 0u;
-  }
-  __syncthreads();
-  uint32_t prev_m = 0, prev_base = 0;  // staged tile t-1 (prev_m == 0: none)
-  int cb = 0;                           // lbuf[cb]: tile t, lbuf[cb ^ 1]: tile t-1
-  for (uint32_t tile = blockIdx.x;; tile += gridDim.x) {
-    const bool have = tile < ntiles;
-    const uint64_t base = uint64_t(tile) * TILE;
-    uint32_t* lc = lbuf[cb];
-    const uint32_t* lp = lbuf[cb ^ 1];
-    // ---- phase A: rank tile t | write out tile t-1 | load keys of tile t+1
-    if (have) {
-#pragma unroll
-      for (int j = 0; j < ROUNDS; ++j) {
-        const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
-        h[j] = murmur32(h[j]);
-        const uint32_t bl = fm.mod(h[j]) - lo;
-        if (i < r.n && bl < nbl) {
-          const uint32_t part = fw.div(bl);
-          rk[j] = (part << TBITS) | atomicAdd(&lc[part], 1u);
-        } else {
-          rk[j] = kInvalid;
-        }
-      }
-    }
-    for (uint32_t k0 = 0; k0 < prev_m; k0 += BLOCK) {
-      const uint32_t k = k0 + threadIdx.x;
-      const bool v = k < prev_m;
-      uint2 e = make_uint2(0, 0);
-      uint32_t o = 0, p = 0;
-      if (v) {
-        e = stage[k];
-        if (IMPLICIT) {
-          p = e.y >> 16;
-          e.y = uint32_t(r.row_base) + prev_base + (e.y & 0xFFFFu);
-        } else {
-          p = fw.div(fm.mod(e.x) - lo);
-        }
-        o = cur[p] + (k - lp[p]);
-        if (o < cap) region[(gbase + p) * cap + o] = e;
-      }
-      const uint64_t spill = __ballot(v && o >= cap);
-      if (spill) {
-        const int leader = __ffsll((unsigned long long)spill) - 1;
-        unsigned long long b0 = 0;
-        if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
-        b0 = __shfl(b0, leader, kWave);
-        if (v && o >= cap) ovf[b0 + __popcll(spill & lt)] = e;
-      }
-    }
-    uint32_t hn[ROUNDS];
-    const uint64_t nbase = base + uint64_t(gridDim.x) * TILE;
-#pragma unroll
-    for (int j = 0; j < ROUNDS; ++j) {
-      const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
-      hn[j] = (have && i < r.n) ? r.key(i) : 0u;
-    }
-    __syncthreads();
-    // ---- phase B: advance the region cursors past tile t-1; scan tile t's counts
-    if (prev_m)
-      for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] += lp[p + 1] - lp[p];
-    if (!have) break;
-    const uint32_t m = lds_excl_scan<BLOCK>(lc, P, wsum);  // ends with a barrier
-    if (threadIdx.x == 0) lc[P] = m;
-    // ---- phase C: stage tile t in partition order; clear tile t-1's offsets for tile t+1
-#pragma unroll
-    for (int j = 0; j < ROUNDS; ++j) {
-      if (rk[j] == kInvalid) continue;
-      const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
-      const uint32_t y = IMPLICIT ? (((rk[j] >> TBITS) << 16) | li) : r.row(base + li);
-      stage[lc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
-    }
-    for (uint32_t p = threadIdx.x; p <= P; p += BLOCK) lbuf[cb ^ 1][p] = 0;
-    __syncthreads();
-    prev_m = m;
-    prev_base = uint32_t(base);
-    cb ^= 1;
-#pragma unroll
-    for (int j = 0; j < ROUNDS; ++j) h[j] = hn[j];
-  }
-  __syncthreads();
-  for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
-}
-
 // cnt_pm[p * G + g] = counts[g * P + p]: partition-major order for the output-slot scan.
 __global__ void k_transpose_counts(const uint32_t* __restrict__ counts, uint32_t G, uint32_t P,
                                    uint32_t* __restrict__ cnt_pm) {
