@@ -277,9 +277,10 @@ enum Mode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
 
 // Reference comparison count and match of one probe against bucket entries [s, s+n) of `E`
 // (LDS or global). Buckets of <= kSortedMax entries are sorted by row (k_sort_small_buckets), so
-// the reference's walk [first insert, newest, ..., second insert] visits sorted index j at
-// position 1 (j == 0) or n - j + 1: one pass finds the first match of that walk. Longer
-// buckets use the order-free two-pass form of chain.hip. CK: fold output checksums.
+// the reference's walk [first insert, newest, ..., second insert] is sorted index 0, n-1, ..., 1
+// and the unique form stops at its first match like the reference (a wave runs the longest
+// match position of its lanes, not the longest bucket). Longer buckets use the order-free
+// two-pass form of chain.hip. CK: fold output checksums.
 template <bool UNIQUE, int MODE, bool CK, typename EntT>
 __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT* E, uint32_t s, uint32_t n,
                                              uint64_t (&acc)[kProbeFields], uint64_t i, uint2* __restrict__ out,
@@ -288,19 +289,16 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
   if (UNIQUE) {
     uint32_t match = kInvalid, cmps = 0;
     if (n <= kSortedMax) {
-      uint32_t jm = kInvalid, rowm = 0;
-      bool m0 = false;
-      for (uint32_t k = 0; k < n; ++k) {
-        const uint2 e = E[s + k];
+      // the reference's walk itself, stopping at the first match: sorted index 0, n-1, ..., 1
+      cmps = n;
+      for (uint32_t c = 0; c < n; ++c) {
+        const uint2 e = E[s + (c == 0 ? 0u : n - c)];
         if (e.x == h) {
-          m0 = m0 || k == 0;
-          if (k == 0) rowm = e.y;
-          if (!m0) { jm = k; rowm = e.y; }
+          cmps = c + 1;
+          match = e.y;
+          break;
         }
       }
-      if (m0) { cmps = 1; match = rowm; }
-      else if (jm != kInvalid) { cmps = n - jm + 1; match = rowm; }
-      else cmps = n;
     } else {
       uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
       for (uint32_t k = s; k < s + n; ++k) {

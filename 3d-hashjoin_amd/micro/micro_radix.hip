@@ -270,6 +270,22 @@ int main(int argc, char** argv) {
   };
   timeit("radix_probe dense (product, all)",
          [&] { CK(radix_probe(&ctx, &t, rs, HJ3D_PROBE_UNIQUE | HJ3D_PROBE_EMIT, out, nS, res, 0)); }, nS * 28.0);
+  // chunked: the same probe over S in C consecutive pieces (regions reused: do they stay in the
+  // 256 MB Infinity Cache between the partition and the probe of one piece?)
+  for (int C : {2, 4, 8, 16}) {
+    char nm[64];
+    snprintf(nm, sizeof nm, "radix_probe dense, %d chunks", C);
+    timeit(nm, [&] {
+      const uint64_t step = (nS + C - 1) / C;
+      for (uint64_t o = 0; o < nS; o += step) {
+        hj3d_rel c = rs;
+        c.base = reinterpret_cast<const char*>(S) + o * 12;
+        c.n = o + step < nS ? step : nS - o;
+        c.row_base = o;
+        CK(radix_probe(&ctx, &t, c, HJ3D_PROBE_UNIQUE | HJ3D_PROBE_EMIT, out + o, c.n, res, 0));
+      }
+    }, nS * 28.0);
+  }
   const RelView v = view_of(rs);
   timeit("floor: read tuple, write pair", [&] { hipLaunchKernelGGL(k_stream_pairs, dim3(1024), dim3(1024), 0, 0, v, pairs); },
          nS * 20.0);
