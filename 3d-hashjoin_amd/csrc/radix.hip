@@ -472,29 +472,41 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
       const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = i < r.n ? r.key(i) : 0u;
     }
-    for (uint32_t k0 = 0; k0 < m; k0 += BLOCK) {
-      const uint32_t k = k0 + threadIdx.x;
-      const bool v = k < m;
-      uint2 e = make_uint2(0, 0);
-      uint32_t o = 0, p = 0;
-      if (v) {
-        e = stage[k];
-        if (IMPLICIT) {
-          p = e.y >> 16;
-          e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
-        } else {
-          p = fw.div(fm.mod(e.x) - lo);
-        }
-        o = cur[p] + (k - loc[p]);
-        if (o < cap) region[(gbase + p) * cap + o] = e;  // plain stores: L2 merges the partial lines of a run
+    // kOutU staged pairs per thread and step: their LDS reads and stores are independent, so the
+    // step exposes kOutU-way parallelism instead of one dependent LDS -> LDS -> store chain
+    constexpr int kOutU = 4;
+    for (uint32_t k0 = 0; k0 < m; k0 += kOutU * BLOCK) {
+      uint2 e[kOutU];
+      uint32_t o[kOutU], p[kOutU];
+#pragma unroll
+      for (int u = 0; u < kOutU; ++u) {
+        const uint32_t k = k0 + u * BLOCK + threadIdx.x;
+        e[u] = k < m ? stage[k] : make_uint2(0, 0);
       }
-      const uint64_t spill = __ballot(v && o >= cap);
-      if (spill) {  // wave-aggregated append to the overflow list
-        const int leader = __ffsll((unsigned long long)spill) - 1;
-        unsigned long long b0 = 0;
-        if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
-        b0 = __shfl(b0, leader, kWave);
-        if (v && o >= cap) ovf[b0 + __popcll(spill & lt)] = e;
+#pragma unroll
+      for (int u = 0; u < kOutU; ++u) {
+        const uint32_t k = k0 + u * BLOCK + threadIdx.x;
+        if (IMPLICIT) {
+          p[u] = e[u].y >> 16;
+          e[u].y = uint32_t(r.row_base + base) + (e[u].y & 0xFFFFu);
+        } else {
+          p[u] = fw.div(fm.mod(e[u].x) - lo);
+        }
+        o[u] = k < m ? cur[p[u]] + (k - loc[p[u]]) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < kOutU; ++u) {
+        const uint32_t k = k0 + u * BLOCK + threadIdx.x;
+        const bool v = k < m;
+        if (v && o[u] < cap) region[(gbase + p[u]) * cap + o[u]] = e[u];  // plain stores: L2 merges a run's partial lines
+        const uint64_t spill = __ballot(v && o[u] >= cap);
+        if (spill) {  // wave-aggregated append to the overflow list
+          const int leader = __ffsll((unsigned long long)spill) - 1;
+          unsigned long long b0 = 0;
+          if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
+          b0 = __shfl(b0, leader, kWave);
+          if (v && o[u] >= cap) ovf[b0 + __popcll(spill & lt)] = e[u];
+        }
       }
     }
     __syncthreads();
