@@ -231,6 +231,7 @@ hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
   hipError_t e = hipMemsetAsync(t->off.p, 0, (uint64_t(t->nb_local) + 1) * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(t->counts.p, 0, 4 * sizeof(uint64_t), ctx->stream);
   t->n_build = 0;
+  t->n_mains = 0;
   return from_hip(ctx, e, "hj3d_table_clear");
 }
 
@@ -251,6 +252,12 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
                                                   : hipErrorNotSupported;
     if (e == hipErrorNotSupported) e = nested_build(ctx, t, *build, ctx->stream);
+    // the partitioned probe sizes its LDS slices by the number of main records
+    t->n_mains = 0;
+    if (e == hipSuccess)
+      e = hipMemcpyAsync(&t->n_mains, t->counts.as<uint64_t>() + 1, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                         ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   }
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");
@@ -287,6 +294,8 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
     e = hipErrorNotSupported;
     if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n))
       e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);  // times its own kernels
+    else if (radix_nested_applicable(ctx, t, probe->n))
+      e = radix_nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
     if (e == hipErrorNotSupported) {
       PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
       e = (t->desc.kind == HJ3D_CHAIN) ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)

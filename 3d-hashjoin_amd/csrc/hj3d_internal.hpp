@@ -78,6 +78,7 @@ struct hj3d_table {
   uint32_t nb_local = 0;  // bucket_hi - bucket_lo
   hj3d::FastMod fm{};
   uint64_t n_build = 0;   // tuples in the last build (host-known)
+  uint64_t n_mains = 0;   // nested: main records (distinct keys) of the last build (host-known)
   bool built = false;
   // chaining: off[nb_local+1] (u32 CSR offsets), ent[n] = {hash, row}
   // nested:   off[nb_local+1] over mains, main[d] = {hash, first_row, sub_off, sub_len},
@@ -105,6 +106,20 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                        uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+// The probe side partitioned by bucket range for a table slice of W buckets per partition
+// (k_rp_part1 + output-slot scan; layout in radix_seg.hpp). Output slots: regions first
+// (seg[P * G] of them), then the overflow list (*novf pairs). Uses scratch kScrPairs,
+// kScrPHist, kScrSortV. hipErrorNotSupported: more than 2048 partitions.
+struct ProbeParts {
+  uint32_t W = 0, P = 0, G = 0, cap = 0, splits = 1;
+  const uint2* region = nullptr;
+  const uint32_t* counts = nullptr;
+  const uint32_t* seg = nullptr;  // seg[P * G] = slots taken by the regions
+  const uint2* ovf = nullptr;
+  const unsigned long long* novf = nullptr;
+};
+hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
+                                 hipStream_t s);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
@@ -117,6 +132,10 @@ bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t 
 hipError_t nested_build_radix(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                         uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+// partitioned nested probe (every mode of nested_probe); needs t->n_mains
+bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
+hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                              uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // exp4.hip
 hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel& r, uint32_t flags,
                   void* out, uint64_t out_cap, uint64_t* res_dev, hipStream_t s);

@@ -14,7 +14,7 @@
 // Probe: as chaining, over main records. Unnest (AlgUnnestHt, algebra.hh:510-541): light
 // matches (<= kInline rows) are expanded by the probing thread; heavy ones (Zipf hot keys)
 // are queued and expanded by whole workgroups, so one hot key cannot serialize a thread.
-#include "hj3d_internal.hpp"
+#include "radix_seg.hpp"
 
 namespace hj3d {
 namespace {
@@ -243,17 +243,36 @@ __global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict
   block_flush<kProbeFields, 1>(acc, res);
 }
 
-// Materialised unnest. Output slots of probe tuple i are [ooff[i], ooff[i+1]) (exclusive scan of
-// the per-probe output counts). One workgroup per 256 consecutive probe tuples: their light
-// outputs (<= kHeavyOut per probe) are enumerated p = 0..L-1 by consecutive threads, each
-// finding its probe tuple by a binary search over the 256 local offsets in LDS, so the stores
-// of a workgroup form one (nearly) contiguous, coalesced range. Heavier probes are queued and
-// written by k_expand_heavy_write with all workgroups.
+// Materialised unnest. Output slots of probe slot i are [ooff[i], ooff[i+1]) (exclusive scan of
+// the per-slot output counts). A slot is a probe tuple (direct probe: its main mid[i], its row
+// r.row(i)) or a partitioned pair (radix probe: sub_off zo[i] and probe row po[i] written by the
+// probe, so the expansion reads no main record). One workgroup per 256 consecutive slots: their
+// light outputs (<= kHeavyOut per slot) are enumerated p = 0..L-1 by consecutive threads, each
+// finding its slot by a binary search over the 256 local offsets in LDS, so the stores of a
+// workgroup form one (nearly) contiguous, coalesced range. Heavier slots are queued and written
+// by k_expand_heavy_flat with all workgroups.
 constexpr uint32_t kHeavyOut = 8192;
 
-__global__ __launch_bounds__(kBlock) void k_expand_light(RelView r, const uint64_t* __restrict__ ooff,
-                                                         const uint32_t* __restrict__ mid,
-                                                         const uint4* __restrict__ mains,
+struct SlotSrc {
+  RelView r;                   // direct: probe relation (row of slot i = r.row(i))
+  const uint32_t* mid;         // direct: matched main of slot i
+  const uint4* mains;
+  const uint32_t* zo;          // radix: sub_off of slot i
+  const uint32_t* po;          // radix: probe row of slot i
+  template <bool SLOTS>
+  __device__ __forceinline__ void get(uint64_t i, uint32_t& z, uint32_t& pr) const {
+    if (SLOTS) {
+      z = zo[i];
+      pr = po[i];
+    } else {
+      z = mains[mid[i]].z;
+      pr = r.row(i);
+    }
+  }
+};
+
+template <bool SLOTS>
+__global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t nslots, const uint64_t* __restrict__ ooff,
                                                          const uint32_t* __restrict__ sub, uint2* __restrict__ out,
                                                          uint64_t out_cap, uint32_t* __restrict__ heavy,
                                                          uint32_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
@@ -266,12 +285,11 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(RelView r, const uint64
   const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
   uint32_t c = 0, z = 0, pr = 0;
   uint64_t pos = 0;
-  if (i < r.n) {
+  if (i < nslots) {
     pos = ooff[i];
     const uint64_t cc = ooff[i + 1] - pos;
     if (cc) {
-      z = mains[mid[i]].z;
-      pr = r.row(i);
+      src.get<SLOTS>(i, z, pr);
       if (cc > kHeavyOut) heavy[atomicAdd(nheavy, 1u)] = uint32_t(i);
       else c = uint32_t(cc);
     }
@@ -296,7 +314,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(RelView r, const uint64
   lpos[threadIdx.x] = pos;
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < tot; p += kBlock) {
-    uint32_t lo = 0, hi = kBlock;  // largest t with loff[t] <= p (probes with c = 0 are skipped over)
+    uint32_t lo = 0, hi = kBlock;  // largest t with loff[t] <= p (slots with c = 0 are skipped over)
 #pragma unroll
     for (int step = 0; step < 8; ++step) {
       const uint32_t md = (lo + hi) >> 1;
@@ -315,32 +333,296 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(RelView r, const uint64
   block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
 }
 
-__global__ __launch_bounds__(kBlock) void k_expand_heavy_write(RelView r, const uint64_t* __restrict__ ooff,
-                                                               const uint32_t* __restrict__ mid,
-                                                               const uint4* __restrict__ mains,
-                                                               const uint32_t* __restrict__ sub,
-                                                               const uint32_t* __restrict__ heavy,
-                                                               const uint32_t* __restrict__ nheavy,
-                                                               uint2* __restrict__ out, uint64_t out_cap,
-                                                               uint64_t* __restrict__ res) {
+// hoff[q] = first flattened output of heavy slot q (exclusive scan of their counts, one workgroup;
+// there are at most total outputs / kHeavyOut heavy slots).
+__global__ __launch_bounds__(1024) void k_heavy_offsets(const uint32_t* __restrict__ heavy,
+                                                        const uint32_t* __restrict__ nheavy,
+                                                        const uint64_t* __restrict__ ooff, uint64_t* __restrict__ hoff) {
+  __shared__ uint64_t wsum[1024 / kWave];
+  __shared__ uint64_t carry_s;
+  const uint32_t nh = *nheavy;
+  if (threadIdx.x == 0) carry_s = 0;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (uint32_t base = 0; base < nh; base += 1024) {
+    const uint32_t q = base + threadIdx.x;
+    uint64_t v = 0;
+    if (q < nh) {
+      const uint32_t i = heavy[q];
+      v = ooff[i + 1] - ooff[i];
+    }
+    uint64_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint64_t y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint64_t wpre = 0, tot = 0;
+    for (int w = 0; w < 1024 / kWave; ++w) {
+      const uint64_t t = wsum[w];
+      if (w < wid) wpre += t;
+      tot += t;
+    }
+    const uint64_t carry = carry_s;
+    if (q < nh) hoff[q] = carry + wpre + x - v;
+    __syncthreads();
+    if (threadIdx.x == 0) carry_s = carry + tot;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) hoff[nh] = carry_s;
+}
+
+// Heavy outputs flattened over all queued slots: wave w writes the kHeavySpan consecutive
+// flattened outputs [w * kHeavySpan, ...), lane l every 64th of them, so stores and sub reads are
+// coalesced and a lane binary-searches hoff only once (a heavy slot spans >= kHeavyOut outputs).
+constexpr uint32_t kHeavySpan = 64 * 16;
+
+template <bool SLOTS>
+__global__ __launch_bounds__(kBlock) void k_expand_heavy_flat(SlotSrc src, const uint64_t* __restrict__ ooff,
+                                                              const uint32_t* __restrict__ sub,
+                                                              const uint32_t* __restrict__ heavy,
+                                                              const uint32_t* __restrict__ nheavy,
+                                                              const uint64_t* __restrict__ hoff, uint2* __restrict__ out,
+                                                              uint64_t out_cap, uint64_t* __restrict__ res) {
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   const uint32_t nh = *nheavy;
-  for (uint32_t q = 0; q < nh; ++q) {
-    const uint32_t i = heavy[q];
-    const uint64_t base = ooff[i], cnt = ooff[i + 1] - base;
-    const uint32_t z = mains[mid[i]].z, prow = r.row(i);
-    for (uint64_t k = uint64_t(blockIdx.x) * kBlock + threadIdx.x; k < cnt; k += uint64_t(gridDim.x) * kBlock) {
+  const uint64_t total = hoff[nh];
+  const int lane = threadIdx.x & 63;
+  const uint64_t nwaves = uint64_t(gridDim.x) * (kBlock / kWave);
+  for (uint64_t w = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) / kWave; w * kHeavySpan < total; w += nwaves) {
+    const uint64_t f0 = w * kHeavySpan + lane;
+    if (f0 >= total) continue;
+    uint32_t lo = 0, hi = nh;  // largest q with hoff[q] <= f0
+    while (hi - lo > 1) {
+      const uint32_t md = (lo + hi) >> 1;
+      if (hoff[md] <= f0) lo = md; else hi = md;
+    }
+    uint32_t q = lo;
+    uint64_t qb = hoff[q], qe = hoff[q + 1];
+    uint32_t i = heavy[q], z, pr;
+    src.get<SLOTS>(i, z, pr);
+    uint64_t ob = ooff[i];
+    for (uint64_t f = f0; f < total && f < (w + 1) * kHeavySpan; f += kWave) {
+      while (f >= qe) {  // next heavy slot
+        ++q;
+        qb = qe;
+        qe = hoff[q + 1];
+        i = heavy[q];
+        src.get<SLOTS>(i, z, pr);
+        ob = ooff[i];
+      }
+      const uint64_t k = f - qb;
       const uint32_t br = sub[z + k];
-      if (base + k < out_cap)
-        __builtin_nontemporal_store((uint64_t(br) << 32) | prow, reinterpret_cast<uint64_t*>(out + base + k));
-      acc[4] += prow;
+      if (ob + k < out_cap)
+        __builtin_nontemporal_store((uint64_t(br) << 32) | pr, reinterpret_cast<uint64_t*>(out + ob + k));
+      acc[4] += pr;
       acc[5] += br;
-      const uint64_t ph = pair_hash(prow, br);
+      const uint64_t ph = pair_hash(pr, br);
       acc[7] += ph;
       acc[8] ^= ph;
     }
   }
   block_flush<kProbeFields, 1>(acc, res);
+}
+
+// ---- partitioned probe (radix_seg.hpp): the probe side is partitioned by bucket range and
+// each partition's slice of the directory and main records is staged in LDS ----
+
+// Probe of one tuple (hash h, row pr) against main records M[s .. s+n) of its bucket; mg0 =
+// global index of M[0] (the slice start in LDS, 0 in HBM). Same counters as k_nested_probe.
+template <int MODE, typename MT>
+__device__ __forceinline__ void nested_bucket(uint32_t h, uint32_t pr, const MT* M, uint32_t s, uint32_t n,
+                                              uint32_t mg0, uint64_t (&acc)[kProbeFields], uint64_t i,
+                                              uint2* __restrict__ out, uint64_t out_cap, uint64_t* __restrict__ cnt,
+                                              uint32_t* __restrict__ zo, uint32_t* __restrict__ po,
+                                              const uint32_t* __restrict__ sub, Heavy* __restrict__ heavy,
+                                              uint64_t* __restrict__ nheavy) {
+  acc[0] += 1;
+  uint32_t found = kInvalid;
+  uint4 F = make_uint4(0, 0, 0, 0);
+  for (uint32_t k = s; k < s + n; ++k) {
+    const uint4 c = M[k];
+    if (c.x == h) {
+      found = k;
+      F = c;
+      break;
+    }
+  }
+  if (found == kInvalid) {
+    acc[3] += n;
+  } else {
+    uint32_t before = 0;  // mains of this bucket inserted before the matching one
+    for (uint32_t k = s; k < s + n; ++k) before += M[k].y < F.y;
+    acc[3] += 1 + before;
+    acc[1] += 1;
+  }
+  if (MODE == kAggNU || MODE == kDenseNU) {
+    if (found != kInvalid) {
+      acc[2] += 1;
+      acc[4] += pr;
+      acc[5] += F.y;
+      const uint64_t ph = pair_hash(pr, F.y);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+    if (MODE == kDenseNU && i < out_cap) out[i] = make_uint2(pr, found == kInvalid ? kInvalid : F.y);
+  } else if (MODE == kAggUN) {
+    if (found != kInvalid) {
+      acc[2] += F.w;
+      if (F.w <= kInline) {
+        for (uint32_t q = 0; q < F.w; ++q) {
+          const uint32_t br = sub[F.z + q];
+          acc[4] += pr;
+          acc[5] += br;
+          const uint64_t ph = pair_hash(pr, br);
+          acc[7] += ph;
+          acc[8] ^= ph;
+        }
+      } else {
+        const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
+        heavy[slot] = Heavy{pr, mg0 + found};
+      }
+    }
+  } else {  // kCountUN: the slot's output count, sub_off and probe row for the expansion
+    acc[2] += found != kInvalid ? F.w : 0u;
+    cnt[i] = found != kInvalid ? F.w : 0u;
+    if (found != kInvalid) {
+      zo[i] = F.z;
+      po[i] = pr;
+    }
+  }
+}
+
+// Directory words (start << 16 | count, relative to the slice) then the main records of buckets
+// [b0, b0 + nbs); every thread keeps kStage loads in flight before writing LDS.
+__device__ __forceinline__ void stage_nested(const uint32_t* __restrict__ off, const uint4* __restrict__ mains,
+                                             uint32_t b0, uint32_t nbs, uint32_t m0, uint32_t nm, uint32_t* ldir,
+                                             uint4* lmain) {
+  constexpr int kStage = 8;
+  for (uint32_t k0 = threadIdx.x; k0 < nbs; k0 += kJBlock * kStage) {
+    uint32_t v[kStage], w[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      v[u] = k < nbs ? off[b0 + k] : 0u;
+      w[u] = k < nbs ? off[b0 + k + 1] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      if (k < nbs) ldir[k] = ((v[u] - m0) << 16) | (w[u] - v[u]);
+    }
+  }
+  for (uint32_t k0 = threadIdx.x; k0 < nm; k0 += kJBlock * kStage) {
+    uint4 v[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      v[u] = k < nm ? mains[m0 + k] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kJBlock;
+      if (k < nm) lmain[k] = v[u];
+    }
+  }
+}
+
+template <int MODE, bool FITS>
+__global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restrict__ region,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
+                                                          const uint32_t* __restrict__ off,
+                                                          const uint4* __restrict__ mains,
+                                                          const uint32_t* __restrict__ sub, FastMod fm, uint32_t lo,
+                                                          uint32_t nbl, uint32_t W, uint32_t P, uint32_t splits,
+                                                          uint2* __restrict__ out, uint64_t out_cap,
+                                                          uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
+                                                          uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
+                                                          uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
+  __shared__ uint32_t lds[kProbeLdsWords];
+  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, nbl - b0);
+  const uint32_t m0 = off[b0], nm = off[b0 + nbs] - m0;
+  const uint32_t dirw = (nbs + 4) & ~3u;  // main records 16-B aligned after the directory
+  const bool fits = dirw + 4ull * nm <= kProbeLdsWords;
+  if (fits != FITS) {  // the other kernel takes this partition; keep this block's partial row zero
+    if (FITS && threadIdx.x < kProbeFields) partials[uint64_t(blockIdx.x) * kProbeFields + threadIdx.x] = 0;
+    return;
+  }
+  uint32_t* ldir = lds;
+  uint4* lmain = reinterpret_cast<uint4*>(lds + dirw);
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  seg_walk(region, counts, seg, G, cap, P, p, splits, sp,
+           [&] { if (FITS) stage_nested(off, mains, b0, nbs, m0, nm, ldir, lmain); },
+           [&](uint32_t hv, uint32_t row, uint64_t i) {
+             const uint32_t bl = fm.mod(hv) - lo - b0;
+             if (FITS) {
+               const uint32_t d = ldir[bl];
+               nested_bucket<MODE>(hv, row, lmain, d >> 16, d & 0xFFFFu, m0, acc, i, out, out_cap, cnt, zo, po, sub,
+                                   heavy, nheavy);
+             } else {
+               const uint32_t s = off[b0 + bl];
+               nested_bucket<MODE>(hv, row, mains, s, off[b0 + bl + 1] - s, 0u, acc, i, out, out_cap, cnt, zo, po,
+                                   sub, heavy, nheavy);
+             }
+           });
+  if (FITS) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+  else block_flush<kProbeFields, 1>(acc, partials + uint64_t(gridDim.x) * kProbeFields);  // extra row (atomics)
+}
+
+// Overflow pairs (runs that did not fit their region), probed against the table in HBM; their
+// slots follow the regions' (base = seg[P * G]).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_rn_probe_ovf(const uint2* __restrict__ ovf,
+                                                         const unsigned long long* __restrict__ novf,
+                                                         const uint32_t* __restrict__ base_slot,
+                                                         const uint32_t* __restrict__ off, const uint4* __restrict__ mains,
+                                                         const uint32_t* __restrict__ sub, FastMod fm, uint32_t lo,
+                                                         uint2* __restrict__ out, uint64_t out_cap,
+                                                         uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
+                                                         uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
+                                                         uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  const uint64_t n = *novf, b = *base_slot;
+  for (uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += uint64_t(gridDim.x) * kBlock) {
+    const uint2 e = ovf[j];
+    const uint32_t bl = fm.mod(e.x) - lo;
+    const uint32_t s = off[bl];
+    nested_bucket<MODE>(e.x, e.y, mains, s, off[bl + 1] - s, 0u, acc, b + j, out, out_cap, cnt, zo, po, sub, heavy,
+                        nheavy);
+  }
+  block_flush<kProbeFields, 1>(acc, res);
+}
+
+}  // namespace
+
+namespace {
+
+// Light expansion (one workgroup per 256 slots, partials per workgroup) then the heavy slots
+// flattened over the chip (hoff in kScrD).
+hipError_t expand(hj3d_ctx* ctx, const SlotSrc& src, bool slots, uint64_t nslots, const uint64_t* ooff,
+                  const uint32_t* sub, uint2* out, uint64_t out_cap, uint32_t* heavy, uint32_t* nheavy,
+                  uint64_t* partials, uint64_t* res, hipStream_t s) {
+  const uint32_t nblk = uint32_t((nslots + kBlock - 1) / kBlock);
+  uint64_t* hoff = ctx->scratch[kScrD].as<uint64_t>();
+  if (slots)
+    hipLaunchKernelGGL(k_expand_light<true>, dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
+                       heavy, nheavy, partials);
+  else
+    hipLaunchKernelGGL(k_expand_light<false>, dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
+                       heavy, nheavy, partials);
+  hipLaunchKernelGGL(k_heavy_offsets, dim3(1), dim3(1024), 0, s, heavy, nheavy, ooff, hoff);
+  if (slots)
+    hipLaunchKernelGGL(k_expand_heavy_flat<true>, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub, heavy,
+                       nheavy, hoff, out, out_cap, res);
+  else
+    hipLaunchKernelGGL(k_expand_heavy_flat<false>, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub, heavy,
+                       nheavy, hoff, out, out_cap, res);
+  return hipGetLastError();
 }
 
 }  // namespace
@@ -437,6 +719,7 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
   const uint32_t nblk = uint32_t((r.n + kBlock - 1) / kBlock);
   if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrC].ensure(2 * r.n * sizeof(uint32_t) + 64)) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrD].ensure((r.n + 2) * sizeof(uint64_t))) != hipSuccess) return e;  // hoff
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblk) * kProbeFields * sizeof(uint64_t))) != hipSuccess) return e;
   uint64_t* cnt = ctx->scratch[kScrA].as<uint64_t>();
   uint32_t* nheavy = ctx->scratch[kScrC].as<uint32_t>();
@@ -447,11 +730,100 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
   hipLaunchKernelGGL(k_nested_probe<kCountUN>, dim3(g), dim3(kBlock), 0, s, v, t->fm, lo, nbl, off, mains, sub,
                      nullptr, 0, cnt, mid, nullptr, nullptr, res);
   if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_expand_light, dim3(nblk), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, o, out_cap, heavy,
-                     nheavy, partials);
-  hipLaunchKernelGGL(k_expand_heavy_write, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, v, cnt, mid, mains, sub, heavy,
-                     nheavy, o, out_cap, res);
+  SlotSrc src{v, mid, mains, nullptr, nullptr};
+  if ((e = expand(ctx, src, false, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess) return e;
+  return reduce_partials(partials, nblk, kProbeFields, 1, res, s);
+}
+
+bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe) {
+  return t->desc.kind == HJ3D_NESTED && !ctx->force_direct && n_probe >= ctx->radix_min && t->nb_local >= 64 &&
+         n_probe < (1ull << 32) && t->n_mains > 0;
+}
+
+hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                              uint64_t out_cap, uint64_t* res, hipStream_t s) {
+  hipError_t e;
+  const uint32_t lo = uint32_t(t->desc.bucket_lo), nbl = t->nb_local;
+  // slice width: 80% of the LDS budget at the mean number of main records per bucket (a
+  // directory word + a 4-word main record per bucket at fill 1)
+  const double fill = double(t->n_mains) / double(nbl);
+  ProbeParts pp;
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill)), &pp, s)) !=
+      hipSuccess)
+    return e;
+  const uint32_t nblocks = pp.P * pp.splits;
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+    return e;
+  uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  if ((e = hipMemsetAsync(partials + uint64_t(nblocks) * kProbeFields, 0, kProbeFields * sizeof(uint64_t), s)) !=
+      hipSuccess)
+    return e;
+  uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
+  if ((e = hipMemcpyAsync(base0, res, sizeof(uint64_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+  const bool unnest = flags & HJ3D_PROBE_UNNEST;
+  const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
+  const uint32_t* off = t->off.as<const uint32_t>();
+  const uint4* mains = t->main.as<const uint4>();
+  const uint32_t* sub = t->sub.as<const uint32_t>();
+  uint2* o = static_cast<uint2*>(out);
+  uint64_t* cnt = nullptr;
+  uint32_t *zo = nullptr, *po = nullptr;
+  Heavy* hq = nullptr;
+  uint64_t* nhq = nullptr;
+  const int mode = !unnest ? (emit ? kDenseNU : kAggNU) : (emit ? kCountUN : kAggUN);
+  if (mode == kCountUN) {
+    if ((e = ctx->scratch[kScrA].ensure((r.n + 1) * sizeof(uint64_t))) != hipSuccess) return e;
+    if ((e = ctx->scratch[kScrC].ensure(3 * r.n * sizeof(uint32_t) + 64)) != hipSuccess) return e;
+    cnt = ctx->scratch[kScrA].as<uint64_t>();
+    zo = ctx->scratch[kScrC].as<uint32_t>() + 16;
+    po = zo + r.n;
+    if ((e = hipMemsetAsync(cnt, 0, (r.n + 1) * sizeof(uint64_t), s)) != hipSuccess) return e;
+  } else if (mode == kAggUN) {
+    if ((e = ctx->scratch[kScrC].ensure(r.n * sizeof(Heavy) + 16)) != hipSuccess) return e;
+    nhq = ctx->scratch[kScrC].as<uint64_t>();
+    hq = reinterpret_cast<Heavy*>(nhq + 2);
+    if ((e = hipMemsetAsync(nhq, 0, sizeof(uint64_t), s)) != hipSuccess) return e;
+  }
+  {
+    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+    auto launch = [&](auto mode_c) {
+      constexpr int M = decltype(mode_c)::value;
+      hipLaunchKernelGGL((k_rn_probe_seg<M, true>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
+                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, o, out_cap, cnt, zo, po,
+                         hq, nhq, partials);
+      hipLaunchKernelGGL((k_rn_probe_seg<M, false>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
+                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, o, out_cap, cnt, zo, po,
+                         hq, nhq, partials);
+      hipLaunchKernelGGL((k_rn_probe_ovf<M>), dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf,
+                         pp.seg + uint64_t(pp.G) * pp.P, off, mains, sub, t->fm, lo, o, out_cap, cnt, zo, po, hq, nhq,
+                         res);
+    };
+    switch (mode) {
+      case kAggNU: launch(std::integral_constant<int, kAggNU>{}); break;
+      case kDenseNU: launch(std::integral_constant<int, kDenseNU>{}); break;
+      case kAggUN: launch(std::integral_constant<int, kAggUN>{}); break;
+      default: launch(std::integral_constant<int, kCountUN>{}); break;
+    }
+    if (mode == kAggUN)
+      hipLaunchKernelGGL(k_expand_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, hq, nhq, mains, sub, res);
+  }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
+  if ((e = reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n, base0)) != hipSuccess) return e;
+  if (mode != kCountUN) return hipSuccess;
+  // expansion over the slots: regions' then overflow pairs' (unused slots have count 0)
+  if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
+  const uint32_t nblk = uint32_t((r.n + kBlock - 1) / kBlock);
+  // heavy slots: at most one per slot (many probe tuples may match one hot key)
+  if ((e = ctx->scratch[kScrSortK].ensure((r.n + 64) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrD].ensure((r.n + 2) * sizeof(uint64_t))) != hipSuccess) return e;  // hoff
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblk) * kProbeFields * sizeof(uint64_t))) != hipSuccess) return e;
+  uint32_t* nheavy = ctx->scratch[kScrSortK].as<uint32_t>();
+  uint32_t* heavy = nheavy + 64;
+  partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+  SlotSrc src{view_of(r), nullptr, mains, zo, po};
+  if ((e = expand(ctx, src, true, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess) return e;
   return reduce_partials(partials, nblk, kProbeFields, 1, res, s);
 }
 

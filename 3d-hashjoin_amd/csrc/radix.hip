@@ -17,7 +17,7 @@
 // statistics) untouched: every counter is computed per bucket exactly as in chain.hip.
 #include <cmath>
 
-#include "hj3d_internal.hpp"
+#include "radix_seg.hpp"
 
 namespace hj3d {
 namespace {
@@ -27,9 +27,7 @@ constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
-constexpr int kJBlock = 1024;                    // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
-constexpr uint32_t kProbeLdsWords = 36864;       // 144 KB LDS table slice per probe workgroup
 constexpr uint32_t kSortedMax = 32;             // buckets up to this size are kept sorted by row
 
 struct FastDiv {  // exact floor(a / d) for u32 a, 1 <= d < 2^32
@@ -526,13 +524,11 @@ __global__ void k_transpose_counts(const uint32_t* __restrict__ counts, uint32_t
   }
 }
 
-// Probe of one partition's regions (one per partitioning workgroup): the table slice is staged in
-// LDS, then wave w walks regions g = g_lo + w, g_lo + w + 16, ... in chunks of 64 * kSegItems
-// pairs, the next chunk in flight while the current one is probed. The output slot of a pair is
-// seg[p * G + g] + its position in the region (dense over all regions, partition-major).
-// FITS: the kernel handles only the partitions whose slice fits LDS (the common case, a tight
-// loop over LDS), or only the others (reads the slice through L2); both are launched.
-constexpr int kSegItems = 8;
+// Probe of one partition's regions (seg_walk, radix_seg.hpp) against its table slice in LDS.
+// The output slot of a pair is seg[p * G + g] + its position in the region (dense over all
+// regions, partition-major). FITS: the kernel handles only the partitions whose slice fits LDS
+// (the common case, a tight loop over LDS), or only the others (reads the slice through L2);
+// both are launched.
 template <bool UNIQUE, int MODE, bool CK, bool FITS>
 __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restrict__ region,
                                                           const uint32_t* __restrict__ counts,
@@ -555,70 +551,19 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
   }
   uint32_t* loff = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr int kWaves = kJBlock / kWave;
-  const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
-  constexpr uint32_t kChunk = 64 * kSegItems;
-  // The regions of wave wid are g = g_lo + wid + kWaves * r; lane r holds region r's pair count and
-  // output base, so the walk below never waits on a global load for its bookkeeping.
-  const uint32_t nr = g_hi > g_lo + wid ? (g_hi - g_lo - wid + kWaves - 1) / kWaves : 0u;  // <= 64 (G <= 1024)
-  uint32_t my_len = 0, my_seg = 0;
-  if (uint32_t(lane) < nr) {
-    const uint32_t gg = g_lo + wid + kWaves * lane;
-    my_len = counts[uint64_t(gg) * P + p];
-    my_seg = seg[uint64_t(p) * G + gg];
-  }
-  // wave-uniform cursor: region index r, offset q
-  uint32_t r = 0, q = 0;
-  uint32_t len = __shfl(my_len, 0, kWave);
-  while (r < nr && len == 0) {
-    ++r;
-    len = __shfl(my_len, int(r & 63), kWave);
-  }
-  auto load = [&](uint64_t (&v)[kSegItems], uint32_t rr, uint32_t qq, uint32_t ll) {
-    const uint2* src = region + (uint64_t(g_lo + wid + kWaves * rr) * P + p) * cap;
-#pragma unroll
-    for (int j = 0; j < kSegItems; ++j) {
-      const uint32_t k = qq + j * 64 + lane;
-      v[j] = (rr < nr && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
-    }
-  };
-  uint64_t cur[kSegItems];
-  load(cur, r, q, len);
-  if (FITS) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent);
-  __syncthreads();
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  while (r < nr) {
-    uint32_t nr_ = r, nq = q + kChunk, nl = len;
-    while (nr_ < nr && nq >= nl) {
-      ++nr_;
-      nq = 0;
-      nl = __shfl(my_len, int(nr_ & 63), kWave);
-    }
-    uint64_t nxt[kSegItems];
-    load(nxt, nr_, nq, nl);
-    const uint64_t obase = uint64_t(__shfl(my_seg, int(r & 63), kWave)) + q;
-#pragma unroll
-    for (int j = 0; j < kSegItems; ++j) {
-      const uint32_t k = q + j * 64 + lane;
-      if (k >= len) continue;
-      const uint32_t hv = uint32_t(cur[j]), row = uint32_t(cur[j] >> 32);
-      const uint32_t bl = fm.mod(hv) - lo - b0;
-      const uint64_t i = obase + j * 64 + lane;
-      if (FITS) {
-        const uint32_t d = loff[bl];
-        probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, d >> 16, d & 0xFFFFu, acc, i, out, out_cap, cnt);
-      } else {
-        const uint32_t s = off[b0 + bl];
-        probe_bucket<UNIQUE, MODE, CK>(hv, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
-      }
-    }
-    r = nr_;
-    q = nq;
-    len = nl;
-#pragma unroll
-    for (int j = 0; j < kSegItems; ++j) cur[j] = nxt[j];
-  }
+  seg_walk(region, counts, seg, G, cap, P, p, splits, sp,
+           [&] { if (FITS) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent); },
+           [&](uint32_t hv, uint32_t row, uint64_t i) {
+             const uint32_t bl = fm.mod(hv) - lo - b0;
+             if (FITS) {
+               const uint32_t d = loff[bl];
+               probe_bucket<UNIQUE, MODE, CK>(hv, row, lent, d >> 16, d & 0xFFFFu, acc, i, out, out_cap, cnt);
+             } else {
+               const uint32_t s = off[b0 + bl];
+               probe_bucket<UNIQUE, MODE, CK>(hv, row, ent, s, off[b0 + bl + 1] - s, acc, i, out, out_cap, cnt);
+             }
+           });
   if (MODE != kWrite) {
     if (FITS) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
     else block_flush<kProbeFields, 1>(acc, partials + uint64_t(gridDim.x) * kProbeFields);  // extra row (atomics)
@@ -797,30 +742,24 @@ void launch_seg_any(const SegLaunch& L, bool unique, bool ck, uint2* out, uint64
 
 }  // namespace
 
-hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                       uint64_t out_cap, uint64_t* res, hipStream_t s) {
+hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
+                                 hipStream_t s) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;
-  // slice width: 80% of the LDS slice budget at the table's mean bucket fill
-  const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
-  uint32_t W = uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill));
   if (W < 64) W = 64;
   // more than kMaxParts slices: wider slices that no longer fit LDS (probed through L2 by the
   // non-fitting kernel, still one bucket range per workgroup)
   if ((uint64_t(nbl) + W - 1) / W > kMaxParts) W = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
-  SegLaunch L;
-  L.t = t;
-  L.pl = plan_for(nbl, W, r.n);
-  const uint32_t P = L.pl.P;
+  const Plan pl = plan_for(nbl, W, r.n);
+  const uint32_t P = pl.P;
   if (P > kMaxParts) return hipErrorNotSupported;
-  L.G = L.pl.ntiles < uint32_t(ctx->num_cus) ? L.pl.ntiles : uint32_t(ctx->num_cus);
+  const uint32_t G = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
   // region capacity: expected pairs per (workgroup, partition) + 8 sigma + slack, 128-B multiple
-  const uint64_t per_g = uint64_t((L.pl.ntiles + L.G - 1) / L.G) * kPTile;
+  const uint64_t per_g = uint64_t((pl.ntiles + G - 1) / G) * kPTile;
   const double ex = double(per_g < r.n ? per_g : r.n) / P;
   uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
   cap = (cap + 15) & ~uint64_t(15);
-  L.cap = uint32_t(cap);
-  const uint64_t nreg = uint64_t(L.G) * P;
+  const uint64_t nreg = uint64_t(G) * P;
   if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPHist].ensure((3 * nreg + 2) * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2) + 64)) != hipSuccess) return e;
@@ -829,17 +768,60 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   uint32_t* seg = counts + nreg;  // nreg + 1 (transposed counts, scanned in place)
   unsigned long long* novf = ctx->scratch[kScrSortV].as<unsigned long long>();
   uint2* ovf = reinterpret_cast<uint2*>(ctx->scratch[kScrSortV].as<char>() + 64);
-  L.region = region;
-  L.counts = counts;
-  L.seg = seg;
-  L.ovf = ovf;
-  L.novf = novf;
-  L.ovf_grid = ctx->num_cus;
-  L.splits = 1;
+  if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  const RelView v = view_of(r);
+  {
+    PhaseTimer tm(ctx, HJ3D_T_SCATTER);
+    if (r.row_off == HJ3D_ROW_IMPLICIT)
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm,
+                         uint32_t(t->desc.bucket_lo), nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf,
+                         novf);
+    else
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm,
+                         uint32_t(t->desc.bucket_lo), nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf,
+                         novf);
+  }
+  hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, G, P, seg);
+  if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
+  pp->W = pl.W;
+  pp->P = P;
+  pp->G = G;
+  pp->cap = uint32_t(cap);
+  // two probe workgroups per CU's worth of partitions at least: small P splits its regions
   const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
-  if (P < want_blocks) L.splits = (want_blocks + P - 1) / P;
-  if (L.splits > L.G) L.splits = L.G;
-  const uint32_t nblocks = P * L.splits;
+  pp->splits = P < want_blocks ? (want_blocks + P - 1) / P : 1u;
+  if (pp->splits > G) pp->splits = G;
+  pp->region = region;
+  pp->counts = counts;
+  pp->seg = seg;
+  pp->ovf = ovf;
+  pp->novf = novf;
+  return hipGetLastError();
+}
+
+hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                       uint64_t out_cap, uint64_t* res, hipStream_t s) {
+  hipError_t e;
+  // slice width: 80% of the LDS slice budget at the table's mean bucket fill
+  const double fill = t->n_build ? double(t->n_build) / double(t->nb_local) : 0.0;
+  ProbeParts pp;
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s)) !=
+      hipSuccess)
+    return e;
+  SegLaunch L;
+  L.t = t;
+  L.pl.W = pp.W;
+  L.pl.P = pp.P;
+  L.G = pp.G;
+  L.cap = pp.cap;
+  L.splits = pp.splits;
+  L.region = pp.region;
+  L.counts = pp.counts;
+  L.seg = pp.seg;
+  L.ovf = pp.ovf;
+  L.novf = pp.novf;
+  L.ovf_grid = ctx->num_cus;
+  const uint32_t nblocks = pp.P * pp.splits;
   // one row per probe workgroup + one extra row accumulated with atomics by the non-fitting kernel
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
@@ -850,19 +832,6 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   // n_probe of earlier accumulated probes (the reduction below sets res[0] = that + r.n)
   uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
   if ((e = hipMemcpyAsync(base0, res, sizeof(uint64_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
-  const RelView v = view_of(r);
-  {
-    PhaseTimer tm(ctx, HJ3D_T_SCATTER);
-    if (r.row_off == HJ3D_ROW_IMPLICIT)
-      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
-                         uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
-    else
-      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, false>), dim3(L.G), dim3(kPBlock), 0, s, v, t->fm,
-                         uint32_t(t->desc.bucket_lo), nbl, L.pl.fw, P, L.pl.ntiles, L.cap, region, counts, ovf, novf);
-  }
-  hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, L.G, P, seg);
-  if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
   const bool unique = flags & HJ3D_PROBE_UNIQUE;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;

@@ -1,0 +1,82 @@
+// radix_seg.hpp — device side of the partitioned probe shared by the chaining probe (radix.hip)
+// and the nested probe (nested.hip): the walk of one partition's regions.
+//
+// k_rp_part1 (radix.hip) leaves, for every partitioning workgroup g and partition p, a region of
+// counts[g * P + p] (hash, row) pairs at region[(g * P + p) * cap]; seg[p * G + g] is the dense
+// output slot of the region's first pair (exclusive scan, partition-major). A probe workgroup
+// owns partition p (or one of `splits` shares of its regions) and stages the partition's table
+// slice in LDS before probing.
+#pragma once
+
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+
+constexpr int kJBlock = 1024;               // build / probe workgroups (16 waves, 1 per CU)
+constexpr uint32_t kProbeLdsWords = 36864;  // 144 KB LDS table slice per probe workgroup
+constexpr int kSegItems = 8;                // pairs per lane and step of the region walk
+
+// Walks the regions of partition p assigned to share sp (of `splits`): wave w takes regions
+// g = g_lo + w, g_lo + w + 16, ... in chunks of 64 * kSegItems pairs, the next chunk in flight
+// while the current one is probed. Lane r of a wave holds region r's pair count and output base,
+// so the walk never waits on a global load for its bookkeeping. `stage()` runs once after the
+// first chunk's loads are issued (table slice -> LDS) and is followed by a barrier;
+// `probe(hash, row, slot)` is called for every pair.
+template <class Stage, class Probe>
+__device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const uint32_t* __restrict__ counts,
+                                         const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap, uint32_t P,
+                                         uint32_t p, uint32_t splits, uint32_t sp, Stage&& stage, Probe&& probe) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kJBlock / kWave;
+  const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
+  constexpr uint32_t kChunk = 64 * kSegItems;
+  const uint32_t nr = g_hi > g_lo + wid ? (g_hi - g_lo - wid + kWaves - 1) / kWaves : 0u;  // <= 64 (G <= 1024)
+  uint32_t my_len = 0, my_seg = 0;
+  if (uint32_t(lane) < nr) {
+    const uint32_t gg = g_lo + wid + kWaves * lane;
+    my_len = counts[uint64_t(gg) * P + p];
+    my_seg = seg[uint64_t(p) * G + gg];
+  }
+  // wave-uniform cursor: region index r, offset q
+  uint32_t r = 0, q = 0;
+  uint32_t len = __shfl(my_len, 0, kWave);
+  while (r < nr && len == 0) {
+    ++r;
+    len = __shfl(my_len, int(r & 63), kWave);
+  }
+  auto load = [&](uint64_t (&v)[kSegItems], uint32_t rr, uint32_t qq, uint32_t ll) {
+    const uint2* src = region + (uint64_t(g_lo + wid + kWaves * rr) * P + p) * cap;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = qq + j * 64 + lane;
+      v[j] = (rr < nr && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
+    }
+  };
+  uint64_t cur[kSegItems];
+  load(cur, r, q, len);
+  stage();
+  __syncthreads();
+  while (r < nr) {
+    uint32_t nr_ = r, nq = q + kChunk, nl = len;
+    while (nr_ < nr && nq >= nl) {
+      ++nr_;
+      nq = 0;
+      nl = __shfl(my_len, int(nr_ & 63), kWave);
+    }
+    uint64_t nxt[kSegItems];
+    load(nxt, nr_, nq, nl);
+    const uint64_t obase = uint64_t(__shfl(my_seg, int(r & 63), kWave)) + q;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) {
+      const uint32_t k = q + j * 64 + lane;
+      if (k < len) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), obase + j * 64 + lane);
+    }
+    r = nr_;
+    q = nq;
+    len = nl;
+#pragma unroll
+    for (int j = 0; j < kSegItems; ++j) cur[j] = nxt[j];
+  }
+}
+
+}  // namespace hj3d

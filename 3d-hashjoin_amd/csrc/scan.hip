@@ -95,27 +95,43 @@ __global__ __launch_bounds__(1024) void k_scan_sums(T* sums, uint64_t m) {
   if (threadIdx.x == 0) sums[m] = carry_s;
 }
 
-// Per-tile exclusive scan. Thread t owns the kScanItems consecutive elements
-// [base + t*kScanItems, ...) so the scan order is the element order.
+// Per-tile exclusive scan. The tile is loaded and stored coalesced (lane-strided) and
+// transposed through LDS so that thread t scans the kScanItems consecutive elements
+// [t*kScanItems, ...) of the tile; one pad word per kScanItems keeps the transposed LDS
+// accesses free of bank conflicts.
+constexpr int kScanPad = kTile + kTile / kScanItems;
+__device__ __forceinline__ uint32_t scan_slot(uint32_t i) { return i + i / kScanItems; }
+
 template <typename T>
 __global__ __launch_bounds__(kBlock) void k_scan_tiles(const T* in, T* out, uint64_t n, const T* __restrict__ sums) {
   __shared__ T lds[kBlock / kWave];
-  const uint64_t base = uint64_t(blockIdx.x) * kTile + uint64_t(threadIdx.x) * kScanItems;
+  __shared__ T tile[kScanPad];
+  const uint64_t base = uint64_t(blockIdx.x) * kTile;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
+    tile[scan_slot(k)] = base + k < n ? in[base + k] : T(0);
+  }
+  __syncthreads();
   T v[kScanItems];
   T local = 0;
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
-    const uint64_t i = base + j;
-    v[j] = i < n ? in[i] : T(0);
+    v[j] = tile[scan_slot(threadIdx.x * kScanItems + j)];
     local += v[j];
   }
   T total;
   T pre = block_excl_scan(local, lds, &total) + sums[blockIdx.x];
 #pragma unroll
   for (int j = 0; j < kScanItems; ++j) {
-    const uint64_t i = base + j;
-    if (i < n) out[i] = pre;
+    tile[scan_slot(threadIdx.x * kScanItems + j)] = pre;
     pre += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
+    if (base + k < n) out[base + k] = tile[scan_slot(k)];
   }
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = sums[gridDim.x];
 }
