@@ -112,6 +112,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
 // kScrPHist, kScrSortV. hipErrorNotSupported: more than 2048 partitions.
 struct ProbeParts {
   uint32_t W = 0, P = 0, G = 0, cap = 0, splits = 1;
+  bool flat = false;  // short regions: walk them as one flattened stream (radix_seg.hpp)
   const uint2* region = nullptr;
   const uint32_t* counts = nullptr;
   const uint32_t* seg = nullptr;  // seg[P * G] = slots taken by the regions

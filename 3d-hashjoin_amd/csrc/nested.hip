@@ -538,7 +538,7 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
                                                           const uint4* __restrict__ mains,
                                                           const uint32_t* __restrict__ sub, FastMod fm, uint32_t lo,
                                                           uint32_t nbl, uint32_t W, uint32_t P, uint32_t splits,
-                                                          uint2* __restrict__ out, uint64_t out_cap,
+                                                          bool flat, uint2* __restrict__ out, uint64_t out_cap,
                                                           uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
                                                           uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
                                                           uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
   uint32_t* ldir = lds;
   uint4* lmain = reinterpret_cast<uint4*>(lds + dirw);
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  seg_walk(region, counts, seg, G, cap, P, p, splits, sp,
+  seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
            [&] { if (FITS) stage_nested(off, mains, b0, nbs, m0, nm, ldir, lmain); },
            [&](uint32_t hv, uint32_t row, uint64_t i) {
              const uint32_t bl = fm.mod(hv) - lo - b0;
@@ -789,11 +789,11 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
     auto launch = [&](auto mode_c) {
       constexpr int M = decltype(mode_c)::value;
       hipLaunchKernelGGL((k_rn_probe_seg<M, true>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
-                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, o, out_cap, cnt, zo, po,
-                         hq, nhq, partials);
+                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
+                         zo, po, hq, nhq, partials);
       hipLaunchKernelGGL((k_rn_probe_seg<M, false>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
-                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, o, out_cap, cnt, zo, po,
-                         hq, nhq, partials);
+                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
+                         zo, po, hq, nhq, partials);
       hipLaunchKernelGGL((k_rn_probe_ovf<M>), dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf,
                          pp.seg + uint64_t(pp.G) * pp.P, off, mains, sub, t->fm, lo, o, out_cap, cnt, zo, po, hq, nhq,
                          res);

@@ -535,8 +535,9 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
                                                           const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
                                                           const uint32_t* __restrict__ off, const uint2* __restrict__ ent,
                                                           FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
-                                                          uint32_t splits, uint2* __restrict__ out, uint64_t out_cap,
-                                                          uint64_t* __restrict__ cnt, uint64_t* __restrict__ partials) {
+                                                          uint32_t splits, bool flat, uint2* __restrict__ out,
+                                                          uint64_t out_cap, uint64_t* __restrict__ cnt,
+                                                          uint64_t* __restrict__ partials) {
   __shared__ uint32_t lds[kProbeLdsWords];
   const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
   const uint32_t b0 = p * W;
@@ -552,7 +553,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
   uint32_t* loff = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  seg_walk(region, counts, seg, G, cap, P, p, splits, sp,
+  seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
            [&] { if (FITS) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent); },
            [&](uint32_t hv, uint32_t row, uint64_t i) {
              const uint32_t bl = fm.mod(hv) - lo - b0;
@@ -704,6 +705,7 @@ struct SegLaunch {
   const hj3d_table* t;
   Plan pl;
   uint32_t G, cap, splits;
+  bool flat;
   const uint2* region;
   const uint32_t* counts;
   const uint32_t* seg;
@@ -718,11 +720,12 @@ void launch_seg(const SegLaunch& L, uint2* out, uint64_t cap, uint64_t* cnt, uin
   const hj3d_table* t = L.t;
   hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK, true>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s, L.region,
                      L.counts, L.seg, L.G, L.cap, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
-                     uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, out, cap, cnt, partials);
+                     uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, L.flat, out, cap, cnt,
+                     partials);
   hipLaunchKernelGGL((k_rp_probe_seg<UNIQUE, MODE, CK, false>), dim3(L.pl.P * L.splits), dim3(kJBlock), 0, s,
                      L.region, L.counts, L.seg, L.G, L.cap, t->off.as<const uint32_t>(), t->ent.as<const uint2>(),
-                     t->fm, uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, out, cap, cnt,
-                     partials);
+                     t->fm, uint32_t(t->desc.bucket_lo), t->nb_local, L.pl.W, L.pl.P, L.splits, L.flat, out, cap,
+                     cnt, partials);
   hipLaunchKernelGGL((k_probe_ovf<UNIQUE, MODE, CK>), dim3(L.ovf_grid), dim3(kBlock), 0, s, L.ovf, L.novf,
                      L.seg + uint64_t(L.G) * L.pl.P, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), t->fm,
                      uint32_t(t->desc.bucket_lo), out, cap, cnt, res);
@@ -791,6 +794,7 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
   pp->splits = P < want_blocks ? (want_blocks + P - 1) / P : 1u;
   if (pp->splits > G) pp->splits = G;
+  pp->flat = double(r.n) / double(nreg) < 256.0;
   pp->region = region;
   pp->counts = counts;
   pp->seg = seg;
@@ -815,6 +819,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   L.G = pp.G;
   L.cap = pp.cap;
   L.splits = pp.splits;
+  L.flat = pp.flat;
   L.region = pp.region;
   L.counts = pp.counts;
   L.seg = pp.seg;

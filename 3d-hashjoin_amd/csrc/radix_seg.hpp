@@ -17,15 +17,20 @@ constexpr uint32_t kProbeLdsWords = 36864;  // 144 KB LDS table slice per probe 
 constexpr int kSegItems = 8;                // pairs per lane and step of the region walk
 
 // Walks the regions of partition p assigned to share sp (of `splits`): wave w takes regions
-// g = g_lo + w, g_lo + w + 16, ... in chunks of 64 * kSegItems pairs, the next chunk in flight
-// while the current one is probed. Lane r of a wave holds region r's pair count and output base,
-// so the walk never waits on a global load for its bookkeeping. `stage()` runs once after the
-// first chunk's loads are issued (table slice -> LDS) and is followed by a barrier;
-// `probe(hash, row, slot)` is called for every pair.
+// g = g_lo + w, g_lo + w + 16, ... (at most 64; lane r holds region r's pair count and output
+// base) in chunks of 64 * kSegItems pairs, the next chunk in flight while the current one is
+// probed. `stage()` runs once after the first chunk's loads are issued (table slice -> LDS) and
+// is followed by a barrier; `probe(hash, row, slot)` is called for every pair.
+// Long regions (a large probe side) are walked one region at a time. Short ones (`flat`: a small
+// probe side leaves a few dozen pairs per region) are walked as ONE flattened stream so that
+// every lane stays busy; the region of each 64-item block is then found with wave-uniform steps
+// only (readlane of the lane holding region r): the block's first region advances
+// monotonically and the region starts inside a block are few.
 template <class Stage, class Probe>
 __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const uint32_t* __restrict__ counts,
                                          const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap, uint32_t P,
-                                         uint32_t p, uint32_t splits, uint32_t sp, Stage&& stage, Probe&& probe) {
+                                         uint32_t p, uint32_t splits, uint32_t sp, bool flat, Stage&& stage,
+                                         Probe&& probe) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   constexpr int kWaves = kJBlock / kWave;
   const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
@@ -36,6 +41,52 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
     const uint32_t gg = g_lo + wid + kWaves * lane;
     my_len = counts[uint64_t(gg) * P + p];
     my_seg = seg[uint64_t(p) * G + gg];
+  }
+  if (flat) {
+    uint32_t total;
+    const uint32_t my_pre = wave_excl_scan(my_len, &total);  // stream offset of region `lane`
+    auto pre_at = [&](uint32_t r) { return uint32_t(__builtin_amdgcn_readlane(int(my_pre), int(r))); };
+    auto seg_at = [&](uint32_t r) { return uint32_t(__builtin_amdgcn_readlane(int(my_seg), int(r))); };
+    uint32_t rb = 0;  // wave-uniform: last region starting at or before the current block
+    auto load = [&](uint64_t (&v)[kSegItems], uint32_t (&slot)[kSegItems], uint32_t f0) {
+  #pragma unroll
+      for (int j = 0; j < kSegItems; ++j) {
+        const uint32_t b = f0 + j * 64, f = b + lane;
+        while (rb + 1 < nr && pre_at(rb + 1) <= b) ++rb;
+        uint32_t r = rb, pr = pre_at(rb), sg = seg_at(rb);
+        for (uint32_t t = rb + 1; t < nr; ++t) {  // region starts inside the block
+          const uint32_t pt = pre_at(t);
+          if (pt > b + 63) break;
+          if (pt <= f) {
+            r = t;
+            pr = pt;
+            sg = seg_at(t);
+          }
+        }
+        const uint2* src = region + (uint64_t(g_lo + wid + kWaves * r) * P + p) * cap;
+        v[j] = f < total ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + (f - pr))) : 0ull;
+        slot[j] = sg + (f - pr);
+      }
+    };
+    uint64_t cur[kSegItems];
+    uint32_t cslot[kSegItems];
+    load(cur, cslot, 0);
+    stage();
+    __syncthreads();
+    for (uint32_t f0 = 0; f0 < total; f0 += kChunk) {
+      uint64_t nxt[kSegItems];
+      uint32_t nslot[kSegItems];
+      if (f0 + kChunk < total) load(nxt, nslot, f0 + kChunk);
+  #pragma unroll
+      for (int j = 0; j < kSegItems; ++j)
+        if (f0 + j * 64 + lane < total) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), uint64_t(cslot[j]));
+  #pragma unroll
+      for (int j = 0; j < kSegItems; ++j) {
+        cur[j] = nxt[j];
+        cslot[j] = nslot[j];
+      }
+    }
+    return;
   }
   // wave-uniform cursor: region index r, offset q
   uint32_t r = 0, q = 0;

@@ -339,7 +339,7 @@ int main(int argc, char** argv) {
     timeit(nm, [&] {
       hipLaunchKernelGGL((k_rp_probe_seg<true, kDense, false, true>), dim3(P * splits), dim3(kJBlock), 0, 0, region, counts,
                          seg, G, uint32_t(cap), t.off.as<const uint32_t>(), t.ent.as<const uint2>(), t.fm, 0u, nR,
-                         pl0.W, P, splits, out, nS, nullptr, partials);
+                         pl0.W, P, splits, false, out, nS, nullptr, partials);
     }, nS * 16.0 + nR * 12.0);
   };
   variant("1024x16 (1/CU)", k_rp_part1<1024, 16, 2048, true>, 1024, 16384, 1);
