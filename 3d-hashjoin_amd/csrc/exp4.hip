@@ -12,7 +12,7 @@
 //        c_probe_rt = top += mS*mT
 // Triples are enumerated only for the checksums; products above kInline2 are handed to whole
 // workgroups (heavy queue), as in nested.hip.
-#include "hj3d_internal.hpp"
+#include "radix_seg.hpp"
 
 namespace hj3d {
 namespace {
@@ -44,22 +44,31 @@ struct NTab {  // nested table view
   FastMod fm;
   uint32_t lo, nbl;
   // returns main index or kInvalid; adds the reference's comparison count to *cmps
-  __device__ __forceinline__ uint32_t find(uint32_t h, uint64_t* cmps, uint4* M) const {
-    const uint32_t b = fm.mod(h) - lo;
-    if (b >= nbl) return kInvalid;
-    const uint32_t s = off[b], e = off[b + 1];
-    uint32_t found = kInvalid;
-    for (uint32_t k = s; k < e; ++k) {
-      const uint4 c = mains[k];
-      if (c.x == h) { found = k; *M = c; break; }
-    }
-    if (found == kInvalid) { *cmps += e - s; return kInvalid; }
-    uint32_t before = 0;
-    for (uint32_t k = s; k < e; ++k) before += mains[k].y < M->y;
-    *cmps += 1 + before;
-    return found;
-  }
+  __device__ __forceinline__ uint32_t find(uint32_t h, uint64_t* cmps, uint4* M) const;
 };
+
+// Main record of hash h among M[s .. s+n) (one bucket), or kInvalid; adds the reference's
+// comparison count (findMainNodeByOther, ht_nested.hh:354-382) to *cmps. M: HBM or LDS.
+template <typename MT>
+__device__ __forceinline__ uint32_t nfind(uint32_t h, const MT* M, uint32_t s, uint32_t n, uint64_t* cmps, uint4* F) {
+  uint32_t found = kInvalid;
+  for (uint32_t k = s; k < s + n; ++k) {
+    const uint4 c = M[k];
+    if (c.x == h) { found = k; *F = c; break; }
+  }
+  if (found == kInvalid) { *cmps += n; return kInvalid; }
+  uint32_t before = 0;
+  for (uint32_t k = s; k < s + n; ++k) before += M[k].y < F->y;
+  *cmps += 1 + before;
+  return found;
+}
+
+__device__ __forceinline__ uint32_t NTab::find(uint32_t h, uint64_t* cmps, uint4* M) const {
+  const uint32_t b = fm.mod(h) - lo;
+  if (b >= nbl) return kInvalid;
+  const uint32_t s = off[b];
+  return nfind(h, mains, s, off[b + 1] - s, cmps, M);
+}
 
 struct CTab {  // chaining table view
   const uint32_t* off;
@@ -74,33 +83,104 @@ struct CTab {  // chaining table view
   }
 };
 
+// Ndu for one probe tuple after its two lookups (ms / mt: global main indices or kInvalid).
+__device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const NTab& S, const NTab& T, uint32_t ms,
+                                         const uint4& MS, uint32_t mt, const uint4& MT, Heavy2* __restrict__ heavy,
+                                         uint64_t* __restrict__ nheavy) {
+  a[2] += 1;
+  a[4] += MT.w;
+  const uint64_t prod = uint64_t(MS.w) * MT.w;
+  a[5] += prod;
+  a[6] += prod;
+  if (prod <= kInline2) {
+    for (uint32_t q = 0; q < MT.w; ++q) {
+      const uint32_t tr = T.sub[MT.z + q];
+      for (uint32_t p = 0; p < MS.w; ++p) add_triple(a, pr, S.sub[MS.z + p], tr);
+    }
+  } else {
+    const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
+    heavy[slot] = Heavy2{pr, ms, mt, 0};
+  }
+}
+
+// AlgNestJoinProbe(S) -> AlgNestJoinProbe(T) -> unnest both, for one probe tuple (HBM tables).
+__device__ __forceinline__ void ndu_probe(uint64_t (&a)[kF], uint32_t h, uint32_t pr, const NTab& S, const NTab& T,
+                                          Heavy2* __restrict__ heavy, uint64_t* __restrict__ nheavy) {
+  uint4 MS, MT;
+  const uint32_t ms = S.find(h, &a[1], &MS);
+  if (ms == kInvalid) return;
+  a[0] += 1;
+  const uint32_t mt = T.find(h, &a[3], &MT);
+  if (mt == kInvalid) return;
+  ndu_tail(a, pr, S, T, ms, MS, mt, MT, heavy, nheavy);
+}
+
 __global__ __launch_bounds__(kBlock) void k_ndu(RelView r, NTab S, NTab T, Heavy2* __restrict__ heavy,
                                                 uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
   uint64_t a[kF] = {0};
-  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock) {
-    const uint32_t h = murmur32(r.key(i));
-    const uint32_t pr = r.row(i);
-    uint4 MS, MT;
-    const uint32_t ms = S.find(h, &a[1], &MS);
-    if (ms == kInvalid) continue;
-    a[0] += 1;
-    const uint32_t mt = T.find(h, &a[3], &MT);
-    if (mt == kInvalid) continue;
-    a[2] += 1;
-    a[4] += MT.w;
-    const uint64_t prod = uint64_t(MS.w) * MT.w;
-    a[5] += prod;
-    a[6] += prod;
-    if (prod <= kInline2) {
-      for (uint32_t q = 0; q < MT.w; ++q) {
-        const uint32_t tr = T.sub[MT.z + q];
-        for (uint32_t p = 0; p < MS.w; ++p) add_triple(a, pr, S.sub[MS.z + p], tr);
-      }
-    } else {
-      const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
-      heavy[slot] = Heavy2{pr, ms, mt, 0};
-    }
-  }
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock)
+    ndu_probe(a, murmur32(r.key(i)), r.row(i), S, T, heavy, nheavy);
+  block_flush<kF, 1>(a, res);
+}
+
+// Partitioned Ndu (S and T tables with the same bucket function): the probe side is
+// partitioned by bucket range (radix_partition_probe) and each partition's slices of BOTH
+// tables (directories + main records) are staged in LDS; the lookups of both joins then run
+// against LDS. FITS as in k_rp_probe_seg (false: the slices are read through L2).
+template <bool FITS>
+__global__ __launch_bounds__(kJBlock) void k_ndu_seg(const uint2* __restrict__ region, const uint32_t* __restrict__ counts,
+                                                     const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap, NTab S,
+                                                     NTab T, uint32_t W, uint32_t P, uint32_t splits, bool flat,
+                                                     Heavy2* __restrict__ heavy, uint64_t* __restrict__ nheavy,
+                                                     uint64_t* __restrict__ res) {
+  __shared__ uint32_t lds[kProbeLdsWords];
+  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const uint32_t b0 = p * W;
+  const uint32_t nbs = min(W, S.nbl - b0);
+  const uint32_t s0 = S.off[b0], ns = S.off[b0 + nbs] - s0;
+  const uint32_t t0 = T.off[b0], nt = T.off[b0 + nbs] - t0;
+  const uint32_t dirw = (2 * nbs + 4) & ~3u;  // both directories, then 16-B aligned main records
+  const bool fits = dirw + 4ull * (ns + nt) <= kProbeLdsWords;
+  if (fits != FITS) return;
+  uint32_t* ldS = lds;
+  uint32_t* ldT = lds + nbs;
+  uint4* lmS = reinterpret_cast<uint4*>(lds + dirw);
+  uint4* lmT = lmS + ns;
+  uint64_t a[kF] = {0};
+  seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
+           [&] {
+             if (FITS) {
+               stage_nested(S.off, S.mains, b0, nbs, s0, ns, ldS, lmS);
+               stage_nested(T.off, T.mains, b0, nbs, t0, nt, ldT, lmT);
+             }
+           },
+           [&](uint32_t h, uint32_t pr, uint64_t) {
+             if (!FITS) {
+               ndu_probe(a, h, pr, S, T, heavy, nheavy);
+               return;
+             }
+             const uint32_t bl = S.fm.mod(h) - S.lo - b0;
+             uint4 MS, MT;
+             const uint32_t ds = ldS[bl];
+             const uint32_t ms = nfind(h, lmS, ds >> 16, ds & 0xFFFFu, &a[1], &MS);
+             if (ms == kInvalid) return;
+             a[0] += 1;
+             const uint32_t dt = ldT[bl];
+             const uint32_t mt = nfind(h, lmT, dt >> 16, dt & 0xFFFFu, &a[3], &MT);
+             if (mt == kInvalid) return;
+             ndu_tail(a, pr, S, T, s0 + ms, MS, t0 + mt, MT, heavy, nheavy);
+           });
+  block_flush<kF, 1>(a, res);
+}
+
+// Overflow pairs of the partition (runs that did not fit their region), against the HBM tables.
+__global__ __launch_bounds__(kBlock) void k_ndu_ovf(const uint2* __restrict__ ovf, const unsigned long long* __restrict__ novf,
+                                                    NTab S, NTab T, Heavy2* __restrict__ heavy,
+                                                    uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+  uint64_t a[kF] = {0};
+  const uint64_t n = *novf;
+  for (uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += uint64_t(gridDim.x) * kBlock)
+    ndu_probe(a, ovf[j].x, ovf[j].y, S, T, heavy, nheavy);
   block_flush<kF, 1>(a, res);
 }
 
@@ -203,7 +283,28 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
            uint32_t(ts->desc.bucket_lo), ts->nb_local};
     NTab T{tt->off.as<const uint32_t>(), tt->main.as<const uint4>(), tt->sub.as<const uint32_t>(), tt->fm,
            uint32_t(tt->desc.bucket_lo), tt->nb_local};
-    hipLaunchKernelGGL(k_ndu, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res);
+    // partitioned when both tables share the bucket function (and their main counts are known)
+    const bool same = ts->desc.num_buckets == tt->desc.num_buckets && ts->desc.bucket_lo == tt->desc.bucket_lo &&
+                      ts->nb_local == tt->nb_local;
+    e = hipErrorNotSupported;
+    if (same && radix_nested_applicable(ctx, ts, r.n) && radix_nested_applicable(ctx, tt, r.n)) {
+      const double fill = double(ts->n_mains + tt->n_mains) / double(ts->nb_local);
+      ProbeParts pp;
+      e = radix_partition_probe(ctx, ts, r, uint32_t(0.8 * kProbeLdsWords / (2.0 + 4.0 * fill)), &pp, s);
+      if (e == hipSuccess) {
+        const uint32_t nblocks = pp.P * pp.splits;
+        hipLaunchKernelGGL(k_ndu_seg<true>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,
+                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res);
+        hipLaunchKernelGGL(k_ndu_seg<false>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,
+                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res);
+        hipLaunchKernelGGL(k_ndu_ovf, dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf, S, T, heavy, nheavy,
+                           res);
+      }
+    }
+    if (e == hipErrorNotSupported)
+      hipLaunchKernelGGL(k_ndu, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res);
+    else if (e != hipSuccess)
+      return e;
     hipLaunchKernelGGL(k_ndu_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res);
   } else {
     CTab S{ts->off.as<const uint32_t>(), ts->ent.as<const uint2>(), ts->fm, uint32_t(ts->desc.bucket_lo),

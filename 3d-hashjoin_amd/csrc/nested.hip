@@ -495,41 +495,6 @@ __device__ __forceinline__ void nested_bucket(uint32_t h, uint32_t pr, const MT*
   }
 }
 
-// Directory words (start << 16 | count, relative to the slice) then the main records of buckets
-// [b0, b0 + nbs); every thread keeps kStage loads in flight before writing LDS.
-__device__ __forceinline__ void stage_nested(const uint32_t* __restrict__ off, const uint4* __restrict__ mains,
-                                             uint32_t b0, uint32_t nbs, uint32_t m0, uint32_t nm, uint32_t* ldir,
-                                             uint4* lmain) {
-  constexpr int kStage = 8;
-  for (uint32_t k0 = threadIdx.x; k0 < nbs; k0 += kJBlock * kStage) {
-    uint32_t v[kStage], w[kStage];
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      v[u] = k < nbs ? off[b0 + k] : 0u;
-      w[u] = k < nbs ? off[b0 + k + 1] : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      if (k < nbs) ldir[k] = ((v[u] - m0) << 16) | (w[u] - v[u]);
-    }
-  }
-  for (uint32_t k0 = threadIdx.x; k0 < nm; k0 += kJBlock * kStage) {
-    uint4 v[kStage];
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      v[u] = k < nm ? mains[m0 + k] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      if (k < nm) lmain[k] = v[u];
-    }
-  }
-}
-
 template <int MODE, bool FITS>
 __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restrict__ region,
                                                           const uint32_t* __restrict__ counts,

@@ -156,8 +156,11 @@ def test_nested_many_keys_per_bucket(ctx, nb, path):
         ctx.nested_radix(False)
 
 
+@pytest.mark.parametrize("path", ["default", "partitioned"])
 @pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
-def test_exp4_plans_bit_exact(ctx, name, g):
+def test_exp4_plans_bit_exact(ctx, name, g, path):
+    """Experiment 4 against the reference's fixtures; `partitioned` lowers HJ3D_OPT_RADIX_MIN so
+    even these small probe sides take the partitioned Ndu kernels (LDS slices of both tables)."""
     import hj3d
     log2R, a, A, b, B = g["generator_args"][1:6]
     Sa, Ta = O.gen_exp4(log2R, a, A, b, B)
@@ -165,6 +168,16 @@ def test_exp4_plans_bit_exact(ctx, name, g):
     R = dev(O.tuples2(np.arange(cardR, dtype=np.uint32), np.zeros(cardR, np.uint32)))
     S = dev(O.tuples2(np.arange(n, dtype=np.uint32), Sa))
     T = dev(O.tuples2(np.arange(n, dtype=np.uint32), Ta))
+    if path == "partitioned":
+        ctx.radix_min(1 << 6)
+    try:
+        _exp4_check(ctx, g, R, S, T)
+    finally:
+        ctx.radix_min(1 << 20)
+
+
+def _exp4_check(ctx, g, R, S, T):
+    import hj3d
     for plan in ("Ndu", "Chj"):
         got = hj3d.exp4_plan(ctx, plan, R, S, T, g["nb"])
         ref = g["plans"][plan]
