@@ -83,6 +83,31 @@ struct CTab {  // chaining table view
   }
 };
 
+// Triples of one light match (|S(k)| x |T(k)| <= kInline2): the sub rows are loaded in blocks
+// of 8 into registers before they are combined, so a match costs one or two memory latencies
+// instead of one per sub row.
+__device__ __forceinline__ void light_triples(uint64_t (&a)[kF], uint32_t pr, const NTab& S, const NTab& T, uint32_t zs,
+                                              uint32_t ws, uint32_t zt, uint32_t wt) {
+  constexpr uint32_t kB = 8;
+  for (uint32_t qb = 0; qb < wt; qb += kB) {
+    uint32_t tv[kB];
+#pragma unroll
+    for (uint32_t u = 0; u < kB; ++u) tv[u] = qb + u < wt ? T.sub[zt + qb + u] : 0u;
+    for (uint32_t pb = 0; pb < ws; pb += kB) {
+      uint32_t sv[kB];
+#pragma unroll
+      for (uint32_t u = 0; u < kB; ++u) sv[u] = pb + u < ws ? S.sub[zs + pb + u] : 0u;
+#pragma unroll
+      for (uint32_t qu = 0; qu < kB; ++qu) {
+        if (qb + qu >= wt) break;
+#pragma unroll
+        for (uint32_t pu = 0; pu < kB; ++pu)
+          if (pb + pu < ws) add_triple(a, pr, sv[pu], tv[qu]);
+      }
+    }
+  }
+}
+
 // Ndu for one probe tuple after its two lookups (ms / mt: global main indices or kInvalid).
 __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const NTab& S, const NTab& T, uint32_t ms,
                                          const uint4& MS, uint32_t mt, const uint4& MT, Heavy2* __restrict__ heavy,
@@ -93,10 +118,7 @@ __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const N
   a[5] += prod;
   a[6] += prod;
   if (prod <= kInline2) {
-    for (uint32_t q = 0; q < MT.w; ++q) {
-      const uint32_t tr = T.sub[MT.z + q];
-      for (uint32_t p = 0; p < MS.w; ++p) add_triple(a, pr, S.sub[MS.z + p], tr);
-    }
+    light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w);
   } else {
     const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
     heavy[slot] = Heavy2{pr, ms, mt, 0};
