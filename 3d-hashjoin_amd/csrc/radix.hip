@@ -371,37 +371,30 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
 
 // Copy the table slice of buckets [b0, b0 + nbs) into LDS: directory word k = (start of bucket k
 // relative to the slice) << 16 | (its entry count) (both < 2^16: a slice holds < 18432 entries),
-// then the entries. Every thread keeps kStage loads in flight before writing LDS.
+// then the entries. Every load of a batch of kStage rounds (directory AND entries: a whole
+// typical slice) is issued before the first LDS write, so staging costs one memory latency
+// rather than one per round.
 __device__ __forceinline__ void stage_slice(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
                                             uint32_t nbs, uint32_t e0, uint32_t ne, uint32_t* ldir, uint2* lent) {
-  constexpr int kStage = 8;
-  for (uint32_t k0 = threadIdx.x; k0 < nbs; k0 += kJBlock * kStage) {
+  constexpr int kStage = 12;
+  const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(lent);
+  const uint32_t nmax = max(nbs, ne);
+  for (uint32_t k0 = threadIdx.x; k0 < nmax; k0 += kJBlock * kStage) {
     uint32_t v[kStage], w[kStage];
+    uint64_t x[kStage];
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
       v[u] = k < nbs ? off[b0 + k] : 0u;
       w[u] = k < nbs ? off[b0 + k + 1] : 0u;
+      x[u] = k < ne ? src[k] : 0ull;
     }
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
       if (k < nbs) ldir[k] = ((v[u] - e0) << 16) | (w[u] - v[u]);
-    }
-  }
-  const uint64_t* src = reinterpret_cast<const uint64_t*>(ent + e0);
-  uint64_t* dst = reinterpret_cast<uint64_t*>(lent);
-  for (uint32_t k0 = threadIdx.x; k0 < ne; k0 += kJBlock * kStage) {
-    uint64_t v[kStage];
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      v[u] = k < ne ? src[k] : 0ull;
-    }
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      if (k < ne) dst[k] = v[u];
+      if (k < ne) dst[k] = x[u];
     }
   }
 }

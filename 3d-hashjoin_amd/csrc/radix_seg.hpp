@@ -131,36 +131,27 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
 }
 
 // Directory words (start << 16 | count, relative to the slice) then the main records of buckets
-// [b0, b0 + nbs); every thread keeps kStage loads in flight before writing LDS.
+// [b0, b0 + nbs); all loads of a batch of kStage rounds are issued before the first LDS write.
 __device__ __forceinline__ void stage_nested(const uint32_t* __restrict__ off, const uint4* __restrict__ mains,
                                              uint32_t b0, uint32_t nbs, uint32_t m0, uint32_t nm, uint32_t* ldir,
                                              uint4* lmain) {
   constexpr int kStage = 8;
-  for (uint32_t k0 = threadIdx.x; k0 < nbs; k0 += kJBlock * kStage) {
+  const uint32_t nmax = max(nbs, nm);
+  for (uint32_t k0 = threadIdx.x; k0 < nmax; k0 += kJBlock * kStage) {
     uint32_t v[kStage], w[kStage];
+    uint4 x[kStage];
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
       v[u] = k < nbs ? off[b0 + k] : 0u;
       w[u] = k < nbs ? off[b0 + k + 1] : 0u;
+      x[u] = k < nm ? mains[m0 + k] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < kStage; ++u) {
       const uint32_t k = k0 + u * kJBlock;
       if (k < nbs) ldir[k] = ((v[u] - m0) << 16) | (w[u] - v[u]);
-    }
-  }
-  for (uint32_t k0 = threadIdx.x; k0 < nm; k0 += kJBlock * kStage) {
-    uint4 v[kStage];
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      v[u] = k < nm ? mains[m0 + k] : make_uint4(0, 0, 0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * kJBlock;
-      if (k < nm) lmain[k] = v[u];
+      if (k < nm) lmain[k] = x[u];
     }
   }
 }
