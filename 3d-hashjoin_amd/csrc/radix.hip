@@ -25,6 +25,7 @@ namespace {
 constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
 constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
+constexpr int kPRoundsR = 8;                     // k_rp_part1r: 8192-tuple tiles
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
@@ -507,6 +508,179 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
   for (uint32_t p = threadIdx.x; p < P; p += BLOCK) counts[gbase + p] = min(cur[p], cap);
 }
 
+// Wave-aggregated append of the lanes with spill_me set to the overflow list.
+__device__ __forceinline__ void ovf_append(bool spill_me, uint2 e, uint2* __restrict__ ovf,
+                                           unsigned long long* __restrict__ novf) {
+  const uint64_t spill = __ballot(spill_me);
+  if (!spill) return;
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const int leader = __ffsll((unsigned long long)spill) - 1;
+  unsigned long long b0 = 0;
+  if (lane == leader) b0 = atomicAdd(novf, (unsigned long long)__popcll(spill));
+  b0 = __shfl(b0, leader, kWave);
+  if (spill_me) ovf[b0 + __popcll(spill & lt)] = e;
+}
+
+// k_rp_part1 that writes every region in whole, aligned 64-B segments (8 pairs), each by one
+// store instruction. A tile's run of partition p is short (tile / P pairs), so with plain
+// write-out nearly every run starts and ends inside a segment, and the two halves of such a
+// segment reach the L2 from different tiles microseconds apart: the S stream has evicted the
+// first half by then and the segment goes to HBM as partial writes. Here the pairs of a run
+// that do not complete a segment are CARRIED: thread p keeps partition p's <= 7 leftover pairs
+// in registers and puts them in front of p's next run. Runs are staged in LDS at 8-aligned
+// (padded) starts, so a segment never straddles two wave-instructions; segp maps a staged
+// segment to its partition. One partition per thread: P <= BLOCK. The carries are flushed at
+// the end. Stage capacity 2 * TILE holds the padded runs (TILE + 14 P pairs at worst); a tile
+// that would not fit first flushes the carries.
+template <int BLOCK, int ROUNDS, bool IMPLICIT>
+__global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                     uint32_t P, uint32_t ntiles, uint32_t cap,
+                                                     uint2* __restrict__ region, uint32_t* __restrict__ counts,
+                                                     uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
+  constexpr int TILE = BLOCK * ROUNDS;
+  constexpr int TBITS = __builtin_ctz(TILE);
+  constexpr uint32_t SCAP = 2 * TILE;  // stage capacity (pairs)
+  constexpr uint32_t kSeg = 8;         // pairs per 64-B segment
+  static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 15), "tile must be a power of two");
+  __shared__ uint2 stage[SCAP];
+  __shared__ uint32_t loc[BLOCK];      // tile counts (rank atomics)
+  __shared__ uint32_t sbase[BLOCK];    // stage index of the run's first new pair (padded start + carry)
+  // per run: {region offset - stage index, stage end of its whole segments, stage index of its
+  // first new (not yet converted) pair}
+  __shared__ uint4 pinfo[BLOCK];
+  __shared__ uint16_t segp[SCAP / kSeg];  // partition of each staged segment
+  __shared__ uint32_t wsum[BLOCK / kWave];
+  const uint32_t me = threadIdx.x;  // the partition this thread carries for (me < P)
+  const uint64_t gbase = uint64_t(blockIdx.x) * P;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint2 creg[kSeg - 1];
+  uint32_t my_kc = 0, my_cur = 0;
+#pragma unroll
+  for (int j = 0; j < int(kSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
+  uint32_t h[ROUNDS];
+#pragma unroll
+  for (int j = 0; j < ROUNDS; ++j) {
+    const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
+    h[j] = i < r.n ? r.key(i) : 0u;
+  }
+  auto flush_carry = [&]() {  // thread me writes its carry at its cursor (a partial segment)
+#pragma unroll
+    for (int j = 0; j < int(kSeg) - 1; ++j) {
+      const bool v = me < P && uint32_t(j) < my_kc;
+      const uint32_t o = my_cur + j;
+      if (v && o < cap) region[(gbase + me) * cap + o] = creg[j];
+      ovf_append(v && o >= cap, creg[j], ovf, novf);
+    }
+    my_cur += my_kc;
+    my_kc = 0;
+  };
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    if (me < P) loc[me] = 0;
+    const uint64_t base = uint64_t(tile) * TILE;
+    uint32_t rk[ROUNDS];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
+      h[j] = murmur32(h[j]);
+      const uint32_t bl = fm.mod(h[j]) - lo;
+      if (i < r.n && bl < nbl) {
+        const uint32_t part = fw.div(bl);
+        rk[j] = (part << TBITS) | atomicAdd(&loc[part], 1u);
+      } else {
+        rk[j] = kInvalid;
+      }
+    }
+    __syncthreads();
+    const uint32_t my_c = me < P ? loc[me] : 0u;
+    // padded run sizes -> exclusive scan over the threads (one partition per thread)
+    auto scan = [&](uint32_t v, uint32_t* total) {
+      uint32_t x = v;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, kWave);
+        if (lane >= o) x += y;
+      }
+      if (lane == 63) wsum[wid] = x;
+      __syncthreads();
+      uint32_t pre = 0, tot = 0;
+#pragma unroll
+      for (int w = 0; w < BLOCK / kWave; ++w) {
+        const uint32_t t = wsum[w];
+        if (w < wid) pre += t;
+        tot += t;
+      }
+      __syncthreads();
+      *total = tot;
+      return pre + x - v;
+    };
+    uint32_t total;
+    uint32_t my_loc = scan((my_kc + my_c + kSeg - 1) & ~(kSeg - 1), &total);
+    if (total > SCAP) {  // pathological padding: flush the carries (unpadded fill then fits)
+      flush_carry();
+      my_loc = scan((my_c + kSeg - 1) & ~(kSeg - 1), &total);
+    }
+    const uint32_t my_len = my_kc + my_c;
+    if (me < P) {
+      sbase[me] = my_loc + my_kc;
+      pinfo[me] = make_uint4(my_cur - my_loc, my_loc + (my_len & ~(kSeg - 1)), my_loc + my_kc, 0u);
+#pragma unroll
+      for (int j = 0; j < int(kSeg) - 1; ++j)
+        if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
+      for (uint32_t sg = my_loc / kSeg; sg < (my_loc + my_len + kSeg - 1) / kSeg; ++sg) segp[sg] = uint16_t(me);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint32_t part = rk[j] >> TBITS;
+      const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
+      const uint32_t y = IMPLICIT ? ((part << 16) | li) : r.row(base + li);
+      stage[sbase[part] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
+    }
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;  // next tile: loads in flight
+#pragma unroll
+    for (int j = 0; j < ROUNDS; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
+      h[j] = i < r.n ? r.key(i) : 0u;
+    }
+    __syncthreads();
+    // whole segments of every run: stage index k of run p -> region offset k + pinfo[p].x
+    for (uint32_t k = threadIdx.x; k < total; k += BLOCK) {
+      const uint32_t p = segp[k / kSeg];
+      const uint4 pi = pinfo[p];
+      const bool v = k < pi.y;  // padding and the tail (the next carry) are not written
+      uint2 e = make_uint2(0, 0);
+      uint32_t o = 0;
+      if (v) {
+        e = stage[k];
+        if (IMPLICIT && k >= pi.z) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+        o = k + pi.x;
+        if (o < cap) region[(gbase + p) * cap + o] = e;
+      }
+      ovf_append(v && o >= cap, e, ovf, novf);
+    }
+    // the run's tail (< one segment) becomes the partition's carry
+    if (me < P) {
+      const uint32_t F = my_len & ~(kSeg - 1);
+#pragma unroll
+      for (int j = 0; j < int(kSeg) - 1; ++j) {
+        if (uint32_t(j) < my_len - F) {
+          uint2 e = stage[my_loc + F + j];
+          if (IMPLICIT && F + j >= my_kc) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+          creg[j] = e;
+        }
+      }
+      my_cur += F;
+      my_kc = my_len - F;
+    }
+    __syncthreads();
+  }
+  flush_carry();
+  if (me < P) counts[gbase + me] = min(my_cur, cap);
+}
+
 // cnt_pm[p * G + g] = counts[g * P + p]: partition-major order for the output-slot scan.
 __global__ void k_transpose_counts(const uint32_t* __restrict__ counts, uint32_t G, uint32_t P,
                                    uint32_t* __restrict__ cnt_pm) {
@@ -746,12 +920,16 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   // more than kMaxParts slices: wider slices that no longer fit LDS (probed through L2 by the
   // non-fitting kernel, still one bucket range per workgroup)
   if ((uint64_t(nbl) + W - 1) / W > kMaxParts) W = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
-  const Plan pl = plan_for(nbl, W, r.n);
+  Plan pl = plan_for(nbl, W, r.n);
   const uint32_t P = pl.P;
   if (P > kMaxParts) return hipErrorNotSupported;
+  // up to one partition per thread: the whole-segment partitioner and its 8192-tuple tiles
+  const bool seg_writes = P <= uint32_t(kPBlock);
+  const uint32_t tile = seg_writes ? uint32_t(kPBlock * kPRoundsR) : uint32_t(kPTile);
+  pl.ntiles = uint32_t((r.n + tile - 1) / tile);
   const uint32_t G = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
   // region capacity: expected pairs per (workgroup, partition) + 8 sigma + slack, 128-B multiple
-  const uint64_t per_g = uint64_t((pl.ntiles + G - 1) / G) * kPTile;
+  const uint64_t per_g = uint64_t((pl.ntiles + G - 1) / G) * tile;
   const double ex = double(per_g < r.n ? per_g : r.n) / P;
   uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
   cap = (cap + 15) & ~uint64_t(15);
@@ -768,14 +946,22 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   const RelView v = view_of(r);
   {
     PhaseTimer tm(ctx, HJ3D_T_SCATTER);
-    if (r.row_off == HJ3D_ROW_IMPLICIT)
-      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm,
-                         uint32_t(t->desc.bucket_lo), nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf,
-                         novf);
-    else
-      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm,
-                         uint32_t(t->desc.bucket_lo), nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf,
-                         novf);
+    const uint32_t lo = uint32_t(t->desc.bucket_lo);
+    const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
+    if (seg_writes) {
+      if (imp)
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
+                           pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
+      else
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
+                           pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
+    } else if (imp) {
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo,
+                         nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
+    } else {
+      hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo,
+                         nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
+    }
   }
   hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, G, P, seg);
   if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;

@@ -343,6 +343,7 @@ int main(int argc, char** argv) {
     }, nS * 16.0 + nR * 12.0);
   };
   variant("1024x16 (1/CU)", k_rp_part1<1024, 16, 2048, true>, 1024, 16384, 1);
+  variant("regcarry 1024x8 (1/CU)", k_rp_part1r<1024, 8, true>, 1024, 8192, 1);
   {
     const uint32_t ntiles = uint32_t((nS + 16383) / 16384), G = 256;
     const uint32_t cap = 576;
