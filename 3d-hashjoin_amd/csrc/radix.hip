@@ -546,10 +546,8 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
   __shared__ uint2 stage[SCAP];
   __shared__ uint32_t loc[BLOCK];      // tile counts (rank atomics)
   __shared__ uint32_t sbase[BLOCK];    // stage index of the run's first new pair (padded start + carry)
-  // per run: {region offset - stage index, stage end of its whole segments, stage index of its
-  // first new (not yet converted) pair}
-  __shared__ uint4 pinfo[BLOCK];
-  __shared__ uint16_t segp[SCAP / kSeg];  // partition of each staged segment
+  __shared__ uint2 pinfo[BLOCK];       // per run: {region offset - stage index, stage index of its first new pair}
+  __shared__ uint32_t segfull[SCAP / kSeg];  // the whole segments to write: stage segment | partition << 16
   __shared__ uint32_t wsum[BLOCK / kWave];
   const uint32_t me = threadIdx.x;  // the partition this thread carries for (me < P)
   const uint64_t gbase = uint64_t(blockIdx.x) * P;
@@ -615,20 +613,26 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       *total = tot;
       return pre + x - v;
     };
-    uint32_t total;
-    uint32_t my_loc = scan((my_kc + my_c + kSeg - 1) & ~(kSeg - 1), &total);
-    if (total > SCAP) {  // pathological padding: flush the carries (unpadded fill then fits)
+    // one scan for both: padded segments << 16 | whole segments (both sums < 2^16)
+    auto seg_counts = [&]() {
+      const uint32_t L = my_kc + my_c;
+      return (((L + kSeg - 1) / kSeg) << 16) | (L / kSeg);
+    };
+    uint32_t tot;
+    uint32_t pre = scan(seg_counts(), &tot);
+    if ((tot >> 16) * kSeg > SCAP) {  // pathological padding: flush the carries (the fill then fits)
       flush_carry();
-      my_loc = scan((my_c + kSeg - 1) & ~(kSeg - 1), &total);
+      pre = scan(seg_counts(), &tot);
     }
+    const uint32_t my_loc = (pre >> 16) * kSeg, my_fseg = pre & 0xFFFFu, nfull = tot & 0xFFFFu;
     const uint32_t my_len = my_kc + my_c;
     if (me < P) {
       sbase[me] = my_loc + my_kc;
-      pinfo[me] = make_uint4(my_cur - my_loc, my_loc + (my_len & ~(kSeg - 1)), my_loc + my_kc, 0u);
+      pinfo[me] = make_uint2(my_cur - my_loc, my_loc + my_kc);
 #pragma unroll
       for (int j = 0; j < int(kSeg) - 1; ++j)
         if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
-      for (uint32_t sg = my_loc / kSeg; sg < (my_loc + my_len + kSeg - 1) / kSeg; ++sg) segp[sg] = uint16_t(me);
+      for (uint32_t sg = 0; sg < my_len / kSeg; ++sg) segfull[my_fseg + sg] = (my_loc / kSeg + sg) | (me << 16);
     }
     __syncthreads();
 #pragma unroll
@@ -646,20 +650,17 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       h[j] = i < r.n ? r.key(i) : 0u;
     }
     __syncthreads();
-    // whole segments of every run: stage index k of run p -> region offset k + pinfo[p].x
-    for (uint32_t k = threadIdx.x; k < total; k += BLOCK) {
-      const uint32_t p = segp[k / kSeg];
-      const uint4 pi = pinfo[p];
-      const bool v = k < pi.y;  // padding and the tail (the next carry) are not written
-      uint2 e = make_uint2(0, 0);
-      uint32_t o = 0;
-      if (v) {
-        e = stage[k];
-        if (IMPLICIT && k >= pi.z) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
-        o = k + pi.x;
-        if (o < cap) region[(gbase + p) * cap + o] = e;
-      }
-      ovf_append(v && o >= cap, e, ovf, novf);
+    // the whole segments: stage index k of run p -> region offset k + pinfo[p].x (padding and
+    // each run's tail, the next carry, are not visited)
+    for (uint32_t kk = threadIdx.x; kk < nfull * kSeg; kk += BLOCK) {
+      const uint32_t sf = segfull[kk / kSeg];
+      const uint32_t p = sf >> 16, k = (sf & 0xFFFFu) * kSeg + (kk % kSeg);
+      const uint2 pi = pinfo[p];
+      uint2 e = stage[k];
+      if (IMPLICIT && k >= pi.y) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+      const uint32_t o = k + pi.x;
+      if (o < cap) region[(gbase + p) * cap + o] = e;
+      ovf_append(o >= cap, e, ovf, novf);
     }
     // the run's tail (< one segment) becomes the partition's carry
     if (me < P) {
