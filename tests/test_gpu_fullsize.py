@@ -268,3 +268,30 @@ def test_nested_partitioned_probe_vs_direct(ctx, build_side):
             assert a == b, (unnest, emit)
             if emit:
                 assert torch.equal(oa, ob), (unnest, emit)
+
+
+def test_explicit_row_ids_partitioned(ctx):
+    """Probe sides whose row ids are a column (row_word, as the multi-GPU exchange delivers
+    them) rather than implicit: the partitioners' explicit-row forms give the counters and
+    checksums of the implicit form. S.k holds the row id (S.k = i), so both forms name the
+    same rows; chaining (Csr, unique) and nested (Nsr, unnested materialised) probes."""
+    import torch
+    import hj3d
+    nR, nS = 2_000_000, 12_000_000
+    R, S = make_rel(ctx, nR, nS)
+    assert torch.equal(S[:1000, 0], torch.arange(1000, dtype=torch.int32, device="cuda"))
+    t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nR)
+    t.build(hj3d.Rel(R, 0))
+    imp = ctx.probe(t, hj3d.Rel(S, 1), unique=True)
+    exp_ = ctx.probe(t, hj3d.Rel(S, 1, row_word=0), unique=True)
+    assert imp == exp_ and imp.n_out == nS
+    tn = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nR)
+    tn.build(hj3d.Rel(R, 0))
+    out_a = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    out_b = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    a = ctx.probe(tn, hj3d.Rel(S, 1), unnest=True, out=out_a)
+    b = ctx.probe(tn, hj3d.Rel(S, 1, row_word=0), unnest=True, out=out_b)
+    assert a == b and a.n_out == nS
+    ka = ((out_a[:, 0].long() << 32) | (out_a[:, 1].long() & 0xFFFFFFFF)).sort().values
+    kb = ((out_b[:, 0].long() << 32) | (out_b[:, 1].long() & 0xFFFFFFFF)).sort().values
+    assert torch.equal(ka, kb)
