@@ -15,6 +15,7 @@ import argparse
 import json
 import os
 import sys
+import subprocess
 import threading
 import time
 
@@ -64,9 +65,53 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _host_cpu():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+REF_BIN = os.path.join(ROOT, "oracle", "_ref", "ref_golden.out")
+
+
+def cpu_baseline_reference(nR, nS, reps):
+    """The reference's own Csr plan (main_experiment1.cc:636-699, compiled from /root/reference
+    into oracle/_ref/ by oracle/Makefile) on a bounded uniform key/FK sample, run as a child
+    process pinned to one core. None when the binary is absent (then the oracle port runs)."""
+    if not os.path.exists(REF_BIN):
+        return None
+    core = sorted(os.sched_getaffinity(0))[-1]
+    p = subprocess.run([REF_BIN, "time_csr", str(nR), str(nS), str(reps)], capture_output=True, text=True,
+                       timeout=600, preexec_fn=lambda: os.sched_setaffinity(0, {core}))
+    if p.returncode != 0:
+        log(f"reference CPU baseline failed (rc={p.returncode}): {p.stderr[-500:]}")
+        return None
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["c_top"] == nS, r  # every FK finds its key
+    return {
+        "value": nS / (r["probe_ns"] * 1e-9),
+        "unit": "probe tuples/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": (f"the reference's Csr plan (AlgHashJoinBuild/AlgHashJoinProbe<unique>, HtChaining1) "
+                   f"compiled from the reference sources (oracle/_ref/ref_golden.out time_csr): build {nR} R "
+                   f"tuples, probe {nS} uniform-FK S tuples (reference generator, mt19937 seed 5489), "
+                   f"{reps} reps, clear_ht between reps, 1 pinned core"),
+        "build_ms": r["build_ns"] * 1e-6,
+        "probe_ms": r["probe_ns"] * 1e-6,
+        "host_cpu": _host_cpu(),
+        "nproc": os.cpu_count(),
+    }
+
+
 def cpu_baseline(R_host, S_host, nb, reps):
     """The oracle's single-thread port of the reference Csr plan on a bounded sample, pinned
-    to one core (reported baseline, not the target)."""
+    to one core (reported baseline, not the target). Used when oracle/_ref is absent."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O  # CPU baseline leg only
 
@@ -85,15 +130,7 @@ def cpu_baseline(R_host, S_host, nb, reps):
     th.start()
     th.join()
     r = out["res"]
-    cpu_model = "unknown"
-    try:
-        with open("/proc/cpuinfo") as f:
-            for line in f:
-                if line.startswith("model name"):
-                    cpu_model = line.split(":", 1)[1].strip()
-                    break
-    except OSError:
-        pass
+    cpu_model = _host_cpu()
     return {
         "value": len(S_host) / (r.probe_ns * 1e-9),
         "unit": "probe tuples/s",
@@ -345,9 +382,11 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         m = min(args.cpu_sample, nS)
-        R_host = R.cpu().numpy().view("uint32")
-        S_host = S[:m].cpu().numpy().view("uint32")
-        line["cpu_baseline"] = cpu_baseline(R_host, S_host, nb, args.cpu_reps)
+        line["cpu_baseline"] = cpu_baseline_reference(nR, m, args.cpu_reps)
+        if line["cpu_baseline"] is None:
+            R_host = R.cpu().numpy().view("uint32")
+            S_host = S[:m].cpu().numpy().view("uint32")
+            line["cpu_baseline"] = cpu_baseline(R_host, S_host, nb, args.cpu_reps)
     else:
         line["cpu_baseline"] = None
     s = json.dumps(line)

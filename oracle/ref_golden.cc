@@ -21,12 +21,14 @@
 // Usage:
 //   ref_golden exp1 <nR> <nS> <skew 0|1> <theta> <t> <b> [dump]
 //   ref_golden exp4 <log2R> <alpha> <multA> <beta> <multB> [dump]
+//   ref_golden time_csr <nR> <nS> <reps>      (CPU baseline timing of the reference Csr plan)
 // Prints one JSON object on stdout. With "dump", the generated key columns are
 // also emitted (small sizes only; used for generator known-answer fixtures).
 
 #include "util/standard_includes.hh"
 
 #include <algorithm>
+#include <chrono>
 #include <cinttypes>
 #include <cstdio>
 #include <cstring>
@@ -266,6 +268,54 @@ int run(size_t nR, size_t nS, bool skew, double theta, uint32_t t, uint32_t b, b
   std::printf("}}\n");
   return 0;
 }
+
+// CPU baseline (bench.py cpu_baseline, kind "reference"): the reference's own Csr plan
+// (main_experiment1.cc:636-699: AlgScan(R) -> AlgHashJoinBuild, AlgScan(S) -> AlgHashJoinProbe
+// unique -> counting AlgTop, clear_ht between repetitions) timed on a uniform key/FK input of
+// |R| = nR, |S| = nS generated as in main_experiment1.cc:415-457. Build and probe are timed
+// separately with steady_clock, averaged over `reps` repetitions.
+int timeCsr(size_t nR, size_t nS, int reps) {
+  std::mt19937 rng;
+  std::vector<uint32_t> keysR(nR);
+  for (size_t i = 0; i < nR; ++i) keysR[i] = static_cast<uint32_t>(i);
+  std::shuffle(keysR.begin(), keysR.end(), rng);
+  std::vector<uint32_t> fk;
+  GenRandIntVec griv;
+  GenRandIntVec::param_t p(GenRandIntVec::dist_t::kUni, static_cast<uint32_t>(nR), 0, 0.0, 0, -1);
+  griv.generate(fk, static_cast<uint>(nS), p, rng);
+  RelationRS<Tup> R, S;
+  R._tuples.resize(nR);
+  for (size_t i = 0; i < nR; ++i) R._tuples[i] = Tup{keysR[i], 0, 0};
+  S._tuples.resize(nS);
+  for (size_t i = 0; i < nS; ++i) S._tuples[i] = Tup{static_cast<uint32_t>(i), fk[i], 0};
+
+  using build_t = AlgHashJoinBuild<HashK, EqK, GS>;
+  using top_t = AlgTop<Pair, GS>;
+  using probe_t = AlgHashJoinProbe<top_t, build_t, HashA, PredAK, CatPair, true>;
+  GS gs;
+  build_t opBuild(std::max<size_t>(nR, 1), 10);
+  AlgScan<build_t> scanB(&opBuild, &R);
+  top_t top(gNull, false);
+  probe_t opProbe(&top, &opBuild);
+  AlgScan<probe_t> scanP(&opProbe, &S);
+  using clk = std::chrono::steady_clock;
+  std::chrono::nanoseconds tb{0}, tp{0};
+  for (int r = 0; r < reps; ++r) {
+    if (r) opBuild.clear_ht();
+    const auto t0 = clk::now();
+    scanB.run(&gs);
+    const auto t1 = clk::now();
+    scanP.run(&gs);
+    const auto t2 = clk::now();
+    tb += t1 - t0;
+    tp += t2 - t1;
+  }
+  std::printf("{\"plan\":\"Csr\",\"nR\":%zu,\"nS\":%zu,\"reps\":%d,\"build_ns\":%.1f,\"probe_ns\":%.1f,"
+              "\"c_probe\":%" PRIu64 ",\"c_cmp\":%" PRIu64 ",\"c_top\":%" PRIu64 "}\n",
+              nR, nS, reps, double(tb.count()) / reps, double(tp.count()) / reps, opProbe.count(),
+              opProbe.numCmps(), top.count());
+  return 0;
+}
 }  // namespace e1
 
 // =============================== experiment 4 ===================================
@@ -456,6 +506,8 @@ int main(int argc, char** argv) {
     return e4::run(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                    std::atoi(argv[6]), dump);
   }
+  if (argc >= 5 && std::strcmp(argv[1], "time_csr") == 0)
+    return e1::timeCsr(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]));
   std::fprintf(stderr, "usage: ref_golden exp1 nR nS skew theta t b [dump] | exp4 log2R a A b B [dump]\n");
   return 2;
 }

@@ -5,6 +5,7 @@ generate_canonical + the reference's Zipf sampler and vec_permute), and every co
 statistic and output checksum of the six experiment-1 plans and the two experiment-4 plans.
 CPU only.
 """
+import os
 import numpy as np
 import pytest
 
@@ -103,3 +104,21 @@ def test_empty_and_tiny_relations():
     assert (r.c_probe, r.c_cmp, r.c_top) == (0, 0, 0)
     r = O.nested_plan(S, 1, R, 0, 1, True)
     assert (r.c_probe, r.c_cmp, r.c_top, r.stats["empty"]) == (0, 0, 0, 1)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")),
+                    reason="reference harness not built")
+def test_reference_cpu_baseline_timer_counts():
+    """bench.py's cpu_baseline (kind "reference") runs the reference Csr plan through
+    oracle/_ref/ref_golden.out time_csr; its counters must be those of the oracle's Csr plan on
+    the same generator sequence (uniform key/FK: every probe matches once)."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")
+    out = subprocess.run([exe, "time_csr", "4096", "20000", "2"], capture_output=True, text=True, check=True)
+    r = json.loads(out.stdout)
+    Rk, Sa, _ = O.gen_exp1(4096, 20000, False, 0.0, 0)
+    exp = O.chain_plan(O.tuples3(Rk, np.zeros_like(Rk)), 0, O.tuples3(np.arange(20000, dtype=np.uint32), Sa), 1,
+                       4096, True)
+    assert (r["c_probe"], r["c_cmp"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_top)
+    assert r["reps"] == 2 and r["probe_ns"] > 0
