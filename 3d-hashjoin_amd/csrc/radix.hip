@@ -26,6 +26,7 @@ constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
 constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
 constexpr int kPRoundsR = 8;                     // k_rp_part1r: 8192-tuple tiles
+constexpr int kPSeg = 16;                        // k_rp_part1r: 128-B region segments
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
@@ -522,32 +523,34 @@ __device__ __forceinline__ void ovf_append(bool spill_me, uint2 e, uint2* __rest
   if (spill_me) ovf[b0 + __popcll(spill & lt)] = e;
 }
 
-// k_rp_part1 that writes every region in whole, aligned 64-B segments (8 pairs), each by one
-// store instruction. A tile's run of partition p is short (tile / P pairs), so with plain
+// k_rp_part1 that writes every region in whole, aligned SEG-pair segments (SEG = 16: 128 B), each
+// by one store instruction. A tile's run of partition p is short (tile / P pairs), so with plain
 // write-out nearly every run starts and ends inside a segment, and the two halves of such a
 // segment reach the L2 from different tiles microseconds apart: the S stream has evicted the
 // first half by then and the segment goes to HBM as partial writes. Here the pairs of a run
-// that do not complete a segment are CARRIED: thread p keeps partition p's <= 7 leftover pairs
-// in registers and puts them in front of p's next run. Runs are staged in LDS at 8-aligned
-// (padded) starts, so a segment never straddles two wave-instructions; segp maps a staged
-// segment to its partition. One partition per thread: P <= BLOCK. The carries are flushed at
-// the end. Stage capacity 2 * TILE holds the padded runs (TILE + 14 P pairs at worst); a tile
-// that would not fit first flushes the carries.
-template <int BLOCK, int ROUNDS, bool IMPLICIT>
+// that do not complete a segment are CARRIED: thread p keeps partition p's <= SEG-1 leftover
+// pairs in registers and puts them in front of p's next run in the LDS stage. The whole
+// segments of the tile are listed (segfull: stage start | partition << 16) and enumerated SEG
+// lanes per segment, so one wave-instruction stores 64 / SEG complete segments; the stage itself
+// needs no alignment (runs are packed). One partition per thread: P <= BLOCK. The carries are
+// flushed at the end. A tile whose runs plus carries exceed the stage first flushes the carries.
+template <int BLOCK, int ROUNDS, int SEG, bool IMPLICIT>
 __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                      uint32_t P, uint32_t ntiles, uint32_t cap,
                                                      uint2* __restrict__ region, uint32_t* __restrict__ counts,
                                                      uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
   constexpr int TILE = BLOCK * ROUNDS;
   constexpr int TBITS = __builtin_ctz(TILE);
-  constexpr uint32_t SCAP = 2 * TILE;  // stage capacity (pairs)
-  constexpr uint32_t kSeg = 8;         // pairs per 64-B segment
+  constexpr uint32_t kSeg = SEG;
+  // stage capacity (pairs): the tile + the carries (expected (SEG-1)/2 per partition)
+  constexpr uint32_t SCAP = 2 * TILE + (SEG > 8 ? 1024u : 0u);
   static_assert((TILE & (TILE - 1)) == 0 && TILE <= (1 << 15), "tile must be a power of two");
+  static_assert(SCAP + BLOCK * (SEG - 1) < (1u << 16), "stage starts are packed into 16 bits");
   __shared__ uint2 stage[SCAP];
   __shared__ uint32_t loc[BLOCK];      // tile counts (rank atomics)
-  __shared__ uint32_t sbase[BLOCK];    // stage index of the run's first new pair (padded start + carry)
-  __shared__ uint2 pinfo[BLOCK];       // per run: {region offset - stage index, stage index of its first new pair}
-  __shared__ uint32_t segfull[SCAP / kSeg];  // the whole segments to write: stage segment | partition << 16
+  __shared__ uint32_t sbase[BLOCK];    // stage index of the run's first new pair (start + carry)
+  __shared__ uint2 pinfo[BLOCK];       // per run: {region offset - stage index, sbase}
+  __shared__ uint32_t segfull[SCAP / kSeg];  // the whole segments to write: stage start | partition << 16
   __shared__ uint32_t wsum[BLOCK / kWave];
   const uint32_t me = threadIdx.x;  // the partition this thread carries for (me < P)
   const uint64_t gbase = uint64_t(blockIdx.x) * P;
@@ -592,7 +595,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
     }
     __syncthreads();
     const uint32_t my_c = me < P ? loc[me] : 0u;
-    // padded run sizes -> exclusive scan over the threads (one partition per thread)
+    // run lengths -> exclusive scan over the threads (one partition per thread)
     auto scan = [&](uint32_t v, uint32_t* total) {
       uint32_t x = v;
 #pragma unroll
@@ -613,18 +616,18 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       *total = tot;
       return pre + x - v;
     };
-    // one scan for both: padded segments << 16 | whole segments (both sums < 2^16)
+    // one scan for both: run length (carry + new) << 16 | whole segments (both sums < 2^16)
     auto seg_counts = [&]() {
       const uint32_t L = my_kc + my_c;
-      return (((L + kSeg - 1) / kSeg) << 16) | (L / kSeg);
+      return (L << 16) | (L / kSeg);
     };
     uint32_t tot;
     uint32_t pre = scan(seg_counts(), &tot);
-    if ((tot >> 16) * kSeg > SCAP) {  // pathological padding: flush the carries (the fill then fits)
+    if ((tot >> 16) > SCAP) {  // too many carried pairs: flush them (the tile alone then fits)
       flush_carry();
       pre = scan(seg_counts(), &tot);
     }
-    const uint32_t my_loc = (pre >> 16) * kSeg, my_fseg = pre & 0xFFFFu, nfull = tot & 0xFFFFu;
+    const uint32_t my_loc = pre >> 16, my_fseg = pre & 0xFFFFu, nfull = tot & 0xFFFFu;
     const uint32_t my_len = my_kc + my_c;
     if (me < P) {
       sbase[me] = my_loc + my_kc;
@@ -632,7 +635,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
 #pragma unroll
       for (int j = 0; j < int(kSeg) - 1; ++j)
         if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
-      for (uint32_t sg = 0; sg < my_len / kSeg; ++sg) segfull[my_fseg + sg] = (my_loc / kSeg + sg) | (me << 16);
+      for (uint32_t sg = 0; sg < my_len / kSeg; ++sg) segfull[my_fseg + sg] = (my_loc + sg * kSeg) | (me << 16);
     }
     __syncthreads();
 #pragma unroll
@@ -640,7 +643,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       if (rk[j] == kInvalid) continue;
       const uint32_t part = rk[j] >> TBITS;
       const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
-      const uint32_t y = IMPLICIT ? ((part << 16) | li) : r.row(base + li);
+      const uint32_t y = IMPLICIT ? li : r.row(base + li);
       stage[sbase[part] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
     }
     const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;  // next tile: loads in flight
@@ -650,26 +653,27 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       h[j] = i < r.n ? r.key(i) : 0u;
     }
     __syncthreads();
-    // the whole segments: stage index k of run p -> region offset k + pinfo[p].x (padding and
-    // each run's tail, the next carry, are not visited)
+    // the whole segments: stage index k of run p -> region offset k + pinfo[p].x (each run's
+    // tail, the next carry, is not visited)
+    const uint32_t rb = uint32_t(r.row_base + base);
     for (uint32_t kk = threadIdx.x; kk < nfull * kSeg; kk += BLOCK) {
       const uint32_t sf = segfull[kk / kSeg];
-      const uint32_t p = sf >> 16, k = (sf & 0xFFFFu) * kSeg + (kk % kSeg);
+      const uint32_t p = sf >> 16, k = (sf & 0xFFFFu) + (kk % kSeg);
       const uint2 pi = pinfo[p];
       uint2 e = stage[k];
-      if (IMPLICIT && k >= pi.y) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+      if (IMPLICIT && k >= pi.y) e.y = rb + e.y;
       const uint32_t o = k + pi.x;
       if (o < cap) region[(gbase + p) * cap + o] = e;
       ovf_append(o >= cap, e, ovf, novf);
     }
     // the run's tail (< one segment) becomes the partition's carry
     if (me < P) {
-      const uint32_t F = my_len & ~(kSeg - 1);
+      const uint32_t F = my_len - my_len % kSeg;
 #pragma unroll
       for (int j = 0; j < int(kSeg) - 1; ++j) {
         if (uint32_t(j) < my_len - F) {
           uint2 e = stage[my_loc + F + j];
-          if (IMPLICIT && F + j >= my_kc) e.y = uint32_t(r.row_base + base) + (e.y & 0xFFFFu);
+          if (IMPLICIT && F + j >= my_kc) e.y = rb + e.y;
           creg[j] = e;
         }
       }
@@ -951,10 +955,10 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
     const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
     if (seg_writes) {
       if (imp)
-        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, kPSeg, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
                            pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
       else
-        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, kPSeg, false>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
                            pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
     } else if (imp) {
       hipLaunchKernelGGL((k_rp_part1<kPBlock, kPRounds, kMaxParts, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo,
