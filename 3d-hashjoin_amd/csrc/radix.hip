@@ -371,6 +371,118 @@ __device__ __forceinline__ void probe_bucket(uint32_t h, uint32_t pr, const EntT
   }
 }
 
+// probe_bucket for the kSegItems pairs of one lane at once (unique probe against an LDS slice,
+// the hot path of config B): the directory words of all items are read together, then walk
+// position c = 0, 1, 2 of every item still unmatched (sorted index 0, n-1, n-2) as one batch of
+// independent LDS reads per position, so a chunk costs a few LDS latencies instead of one
+// dependent chain per item. Positions >= 3 (buckets of >= 4 entries) and unsorted long buckets
+// (> kSortedMax) finish per item. Counters identical to probe_bucket<true, MODE, CK>.
+template <int MODE, bool CK, int NG>
+__device__ __forceinline__ void probe_group_unique(const uint64_t (&v)[kSegItems], const uint64_t (&slot)[kSegItems],
+                                                   uint32_t valid, int g, const uint32_t* loff, const uint2* lent,
+                                                   FastMod fm, uint32_t lob0, uint64_t (&acc)[kProbeFields],
+                                                   uint2* __restrict__ out, uint64_t out_cap) {
+  static_assert(MODE == kDense || MODE == kAgg, "unique dense / aggregate forms only");
+  // branch-free: every lane reads LDS (absent items read word 0) and selects afterwards
+  uint32_t d[NG], match[NG], cmps[NG];
+  bool live[NG];
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const bool ok = (valid >> (g + j)) & 1u;
+    const uint32_t w = loff[ok ? fm.mod(uint32_t(v[g + j])) - lob0 : 0u];
+    d[j] = ok ? w : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const uint32_t n = d[j] & 0xFFFFu;
+    match[j] = kInvalid;
+    cmps[j] = n;
+    live[j] = n != 0 && n <= kSortedMax;
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < 3; ++c) {
+    uint2 e[NG];
+#pragma unroll
+    for (int j = 0; j < NG; ++j) {
+      const uint32_t n = d[j] & 0xFFFFu;
+      const bool ok = live[j] && c < n;
+      e[j] = lent[ok ? (d[j] >> 16) + (c == 0 ? 0u : n - c) : 0u];
+      const bool hit = ok && e[j].x == uint32_t(v[g + j]);
+      match[j] = hit ? e[j].y : match[j];
+      cmps[j] = hit ? c + 1 : cmps[j];
+      live[j] = live[j] && !hit;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const uint32_t h = uint32_t(v[g + j]), n = d[j] & 0xFFFFu, s = d[j] >> 16;
+    if (live[j] && n > 3) {
+      for (uint32_t c = 3; c < n; ++c) {
+        const uint2 e = lent[s + n - c];
+        if (e.x == h) {
+          cmps[j] = c + 1;
+          match[j] = e.y;
+          break;
+        }
+      }
+    } else if (n > kSortedMax) {  // order-free form of probe_bucket
+      uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, nm = 0;
+      for (uint32_t k = s; k < s + n; ++k) {
+        const uint2 e = lent[k];
+        minrow = min(minrow, e.y);
+        if (e.x == h) {
+          ++nm;
+          lo_m = min(lo_m, e.y);
+          hi_m = max(hi_m, e.y);
+        }
+      }
+      if (nm != 0 && lo_m == minrow) {
+        cmps[j] = 1;
+        match[j] = lo_m;
+      } else if (nm != 0) {
+        uint32_t gt = 0;
+        for (uint32_t k = s; k < s + n; ++k) gt += lent[k].y > hi_m;
+        cmps[j] = 2 + gt;
+        match[j] = hi_m;
+      }
+    }
+  }
+  uint32_t nv = 0, nm = 0, sc = 0;  // per-group sums, folded into the u64 accumulators once
+#pragma unroll
+  for (int j = 0; j < NG; ++j) {
+    const bool ok = (valid >> (g + j)) & 1u;
+    const uint32_t pr = uint32_t(v[g + j] >> 32);
+    nv += ok;
+    sc += cmps[j];  // 0 for absent items (d = 0)
+    const bool m = match[j] != kInvalid;
+    nm += m;
+    if (MODE == kDense && ok && slot[g + j] < out_cap)
+      __builtin_nontemporal_store((uint64_t(match[j]) << 32) | pr, reinterpret_cast<uint64_t*>(out + slot[g + j]));
+    if (CK && m) {
+      acc[4] += pr;
+      acc[5] += match[j];
+      const uint64_t ph = pair_hash(pr, match[j]);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+  }
+  acc[0] += nv;
+  acc[1] += nm;
+  acc[2] += nm;
+  acc[3] += sc;
+}
+
+// Items are taken in groups of NG (register pressure: 4 independent lookups per LDS round).
+template <int MODE, bool CK, int NG = 4>
+__device__ __forceinline__ void probe_chunk_unique(const uint64_t (&v)[kSegItems], const uint64_t (&slot)[kSegItems],
+                                                   uint32_t valid, const uint32_t* loff, const uint2* lent,
+                                                   FastMod fm, uint32_t lob0, uint64_t (&acc)[kProbeFields],
+                                                   uint2* __restrict__ out, uint64_t out_cap) {
+  static_assert(kSegItems % NG == 0, "groups of NG items");
+#pragma unroll
+  for (int g = 0; g < kSegItems; g += NG)
+    probe_group_unique<MODE, CK, NG>(v, slot, valid, g, loff, lent, fm, lob0, acc, out, out_cap);
+}
 // Copy the table slice of buckets [b0, b0 + nbs) into LDS: directory word k = (start of bucket k
 // relative to the slice) << 16 | (its entry count) (both < 2^16: a slice holds < 18432 entries),
 // then the entries. Every load of a batch of kStage rounds (directory AND entries: a whole
@@ -491,7 +603,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
       for (int u = 0; u < kOutU; ++u) {
         const uint32_t k = k0 + u * BLOCK + threadIdx.x;
         const bool v = k < m;
-        if (v && o[u] < cap) region[(gbase + p[u]) * cap + o[u]] = e[u];  // plain stores: L2 merges a run's partial lines
+        if (v && o[u] < cap) region[region_idx(blockIdx.x, p[u], gridDim.x, P) * cap + o[u]] = e[u];  // plain stores: L2 merges a run's partial lines
         const uint64_t spill = __ballot(v && o[u] >= cap);
         if (spill) {  // wave-aggregated append to the overflow list
           const int leader = __ffsll((unsigned long long)spill) - 1;
@@ -570,7 +682,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
     for (int j = 0; j < int(kSeg) - 1; ++j) {
       const bool v = me < P && uint32_t(j) < my_kc;
       const uint32_t o = my_cur + j;
-      if (v && o < cap) region[(gbase + me) * cap + o] = creg[j];
+      if (v && o < cap) region[region_idx(blockIdx.x, me, gridDim.x, P) * cap + o] = creg[j];
       ovf_append(v && o >= cap, creg[j], ovf, novf);
     }
     my_cur += my_kc;
@@ -663,7 +775,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       uint2 e = stage[k];
       if (IMPLICIT && k >= pi.y) e.y = rb + e.y;
       const uint32_t o = k + pi.x;
-      if (o < cap) region[(gbase + p) * cap + o] = e;
+      if (o < cap) region[region_idx(blockIdx.x, p, gridDim.x, P) * cap + o] = e;
       ovf_append(o >= cap, e, ovf, novf);
     }
     // the run's tail (< one segment) becomes the partition's carry
@@ -725,6 +837,15 @@ __global__ __launch_bounds__(kJBlock) void k_rp_probe_seg(const uint2* __restric
   uint32_t* loff = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (FITS && UNIQUE && (MODE == kDense || MODE == kAgg)) {  // batched LDS lookups
+    seg_walk<true>(region, counts, seg, G, cap, P, p, splits, sp, flat,
+                   [&] { stage_slice(off, ent, b0, nbs, e0, ne, loff, lent); },
+                   [&](const uint64_t (&v)[kSegItems], const uint64_t (&sl)[kSegItems], uint32_t valid) {
+                     probe_chunk_unique<MODE, CK>(v, sl, valid, loff, lent, fm, lo + b0, acc, out, out_cap);
+                   });
+    block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+    return;
+  }
   seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
            [&] { if (FITS) stage_slice(off, ent, b0, nbs, e0, ne, loff, lent); },
            [&](uint32_t hv, uint32_t row, uint64_t i) {

@@ -12,9 +12,15 @@
 
 namespace hj3d {
 
+// Index of region (partitioning workgroup g, partition p) among the G * P regions: g-major, so a
+// partitioning workgroup's regions are contiguous (a partition-major layout measured the same).
+__host__ __device__ __forceinline__ uint64_t region_idx(uint32_t g, uint32_t p, uint32_t G, uint32_t P) {
+  return uint64_t(g) * P + p;
+}
+
 constexpr int kJBlock = 1024;               // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kProbeLdsWords = 36864;  // 144 KB LDS table slice per probe workgroup
-constexpr int kSegItems = 8;                // pairs per lane and step of the region walk
+constexpr int kSegItems = 8;                // pairs per lane and step of the region walk (4, 12, 16: slower)
 
 // Walks the regions of partition p assigned to share sp (of `splits`): wave w takes regions
 // g = g_lo + w, g_lo + w + 16, ... (at most 64; lane r holds region r's pair count and output
@@ -26,7 +32,10 @@ constexpr int kSegItems = 8;                // pairs per lane and step of the re
 // every lane stays busy; the region of each 64-item block is then found with wave-uniform steps
 // only (readlane of the lane holding region r): the block's first region advances
 // monotonically and the region starts inside a block are few.
-template <class Stage, class Probe>
+// CHUNK: `probe(v, slot, valid)` is called once per chunk with all kSegItems items of the lane
+// (pair v[j], output slot slot[j], item j present iff bit j of valid), so that the probe can
+// batch its LDS lookups across items.
+template <bool CHUNK = false, class Stage, class Probe>
 __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const uint32_t* __restrict__ counts,
                                          const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap, uint32_t P,
                                          uint32_t p, uint32_t splits, uint32_t sp, bool flat, Stage&& stage,
@@ -63,7 +72,7 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
             sg = seg_at(t);
           }
         }
-        const uint2* src = region + (uint64_t(g_lo + wid + kWaves * r) * P + p) * cap;
+        const uint2* src = region + region_idx(g_lo + wid + kWaves * r, p, G, P) * cap;
         v[j] = f < total ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + (f - pr))) : 0ull;
         slot[j] = sg + (f - pr);
       }
@@ -77,9 +86,20 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
       uint64_t nxt[kSegItems];
       uint32_t nslot[kSegItems];
       if (f0 + kChunk < total) load(nxt, nslot, f0 + kChunk);
+      if constexpr (CHUNK) {
+        uint64_t sl[kSegItems];
+        uint32_t vm = 0;
   #pragma unroll
-      for (int j = 0; j < kSegItems; ++j)
-        if (f0 + j * 64 + lane < total) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), uint64_t(cslot[j]));
+        for (int j = 0; j < kSegItems; ++j) {
+          sl[j] = cslot[j];
+          vm |= uint32_t(f0 + j * 64 + lane < total) << j;
+        }
+        probe(cur, sl, vm);
+      } else {
+  #pragma unroll
+        for (int j = 0; j < kSegItems; ++j)
+          if (f0 + j * 64 + lane < total) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), uint64_t(cslot[j]));
+      }
   #pragma unroll
       for (int j = 0; j < kSegItems; ++j) {
         cur[j] = nxt[j];
@@ -96,7 +116,7 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
     len = __shfl(my_len, int(r & 63), kWave);
   }
   auto load = [&](uint64_t (&v)[kSegItems], uint32_t rr, uint32_t qq, uint32_t ll) {
-    const uint2* src = region + (uint64_t(g_lo + wid + kWaves * rr) * P + p) * cap;
+    const uint2* src = region + region_idx(g_lo + wid + kWaves * rr, p, G, P) * cap;
 #pragma unroll
     for (int j = 0; j < kSegItems; ++j) {
       const uint32_t k = qq + j * 64 + lane;
@@ -117,10 +137,21 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
     uint64_t nxt[kSegItems];
     load(nxt, nr_, nq, nl);
     const uint64_t obase = uint64_t(__shfl(my_seg, int(r & 63), kWave)) + q;
+    if constexpr (CHUNK) {
+      uint64_t sl[kSegItems];
+      uint32_t vm = 0;
 #pragma unroll
-    for (int j = 0; j < kSegItems; ++j) {
-      const uint32_t k = q + j * 64 + lane;
-      if (k < len) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), obase + j * 64 + lane);
+      for (int j = 0; j < kSegItems; ++j) {
+        sl[j] = obase + j * 64 + lane;
+        vm |= uint32_t(q + j * 64 + lane < len) << j;
+      }
+      probe(cur, sl, vm);
+    } else {
+#pragma unroll
+      for (int j = 0; j < kSegItems; ++j) {
+        const uint32_t k = q + j * 64 + lane;
+        if (k < len) probe(uint32_t(cur[j]), uint32_t(cur[j] >> 32), obase + j * 64 + lane);
+      }
     }
     r = nr_;
     q = nq;
