@@ -378,6 +378,16 @@ hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t nb, uint
   return from_hip(ctx, partition(ctx, *rel, nb, parts, out_pairs, counts, ctx->stream), "hj3d_partition");
 }
 
+hj3d_status hj3d_key_bitmap(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t domain, void* bitmap, void* outside) {
+  if (!ctx || !rel_ok(rel) || domain == 0 || domain > (1ull << 32) || !bitmap) return HJ3D_EINVAL;
+  return from_hip(ctx, key_bitmap(ctx, *rel, domain, bitmap, outside, ctx->stream), "hj3d_key_bitmap");
+}
+
+hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t rows, uint64_t words, void* count) {
+  if (!ctx || !count || (words && rows && !bitmaps)) return HJ3D_EINVAL;
+  return from_hip(ctx, bitmap_or_popcount(ctx, bitmaps, rows, words, count, ctx->stream), "hj3d_bitmap_or_popcount");
+}
+
 hj3d_status hj3d_gen_keys(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
                           uint64_t row_base, uint64_t n_keys, uint64_t seed) {
   if (!ctx || (n && !tuples) || stride == 0 || (stride & 3) || (key_off & 3) || key_off + 4 > stride)

@@ -145,6 +145,9 @@ hipError_t table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out, hipS
 // part.hip
 hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t nparts, void* out_pairs,
                      void* counts, hipStream_t s);
+hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s);
+hipError_t bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t rows, uint64_t words, void* count,
+                              hipStream_t s);
 hipError_t gen_keys(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base,
                     uint64_t n_keys, uint64_t seed, hipStream_t s);
 hipError_t gen_fk(void* tuples, uint64_t n, uint32_t stride, uint32_t key_off, uint64_t row_base, uint32_t fk_max,

@@ -243,6 +243,43 @@ __global__ __launch_bounds__(kBlock) void k_expect_gen(RelView p, Feistel f, boo
   block_flush<5, 1>(a, res);
 }
 
+// ---- #dv pre-pass: the reference counts the distinct FK values of S.a with
+// an unordered_set (main_experiment1.cc:453-454) to size the Crs / Nrs / NrsNU tables. Across
+// GPUs: every rank sets the bits of its keys in a bitmap over the key domain, the ranks exchange
+// bitmap slices (all-to-all: rank r receives slice r of every bitmap), OR + popcount their slice,
+// and sum the counts. ----
+
+// bit k of bm for every key k < domain; keys >= domain are counted in *outside (u64).
+__global__ __launch_bounds__(kBlock) void k_key_bitmap(RelView r, uint64_t domain, uint32_t* __restrict__ bm,
+                                                       unsigned long long* __restrict__ outside) {
+  uint32_t nout = 0;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t k = r.key(i);
+    if (k < domain) {
+      const uint32_t bit = 1u << (k & 31);
+      uint32_t* w = bm + (k >> 5);
+      if (!(*w & bit)) atomicOr(w, bit);  // skip the atomic when the bit is already visible
+    } else {
+      ++nout;
+    }
+  }
+  const uint64_t t = wave_sum(uint64_t(nout));
+  if (outside && (threadIdx.x & 63) == 0 && t) atomicAdd(outside, (unsigned long long)t);
+}
+
+// *count += popcount(OR over rows of bm[row * words + w]) over w < words.
+__global__ __launch_bounds__(kBlock) void k_or_popcount(const uint32_t* __restrict__ bm, uint32_t rows, uint64_t words,
+                                                        unsigned long long* __restrict__ count) {
+  uint64_t c = 0;
+  for (uint64_t w = uint64_t(blockIdx.x) * kBlock + threadIdx.x; w < words; w += uint64_t(gridDim.x) * kBlock) {
+    uint32_t x = 0;
+    for (uint32_t q = 0; q < rows; ++q) x |= bm[uint64_t(q) * words + w];
+    c += __popc(x);
+  }
+  const uint64_t t = wave_sum(c);
+  if ((threadIdx.x & 63) == 0 && t) atomicAdd(count, (unsigned long long)t);
+}
+
 }  // namespace
 
 hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n_keys, uint64_t seed, bool swap,
@@ -313,6 +350,21 @@ hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel
   if (probe.n)
     hipLaunchKernelGGL(k_expect, dim3(grid_for(ctx, probe.n, kBlock * 4)), dim3(kBlock), 0, s, p, n_keys, inv,
                        swap, static_cast<uint64_t*>(res));
+  return hipGetLastError();
+}
+
+hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s) {
+  if (r.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_key_bitmap, dim3(grid_for(ctx, r.n, kBlock * 4)), dim3(kBlock), 0, s, view_of(r), domain,
+                     static_cast<uint32_t*>(bitmap), static_cast<unsigned long long*>(outside));
+  return hipGetLastError();
+}
+
+hipError_t bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t rows, uint64_t words, void* count,
+                              hipStream_t s) {
+  if (words == 0 || rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_or_popcount, dim3(grid_for(ctx, words, kBlock * 4)), dim3(kBlock), 0, s,
+                     static_cast<const uint32_t*>(bitmaps), rows, words, static_cast<unsigned long long*>(count));
   return hipGetLastError();
 }
 

@@ -105,6 +105,8 @@ def lib():
         "hj3d_probe2_result": (st, [p, C.POINTER(_Probe2Res)]),
         "hj3d_partition": (st, [p, R, u64, u32, p, p]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
+        "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
+        "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
         "hj3d_gen_keys": (st, [p, p, u64, u32, u32, u64, u64, u64]),
         "hj3d_gen_fk": (st, [p, p, u64, u32, u32, u64, u32, u64]),
         "hj3d_gen_zipf": (st, [p, p, u64, u32, u32, u64, u32, C.c_double, u64]),
@@ -273,6 +275,35 @@ class Context:
     def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts):
         self._check(lib().hj3d_partition(self.h, C.byref(rel.c), num_buckets, parts, out_pairs.data_ptr(),
                                          counts.data_ptr()), "hj3d_partition")
+
+    def key_bitmap(self, rel: Rel, domain: int, bitmap, outside=None):
+        """Set bit k of `bitmap` (int32 device tensor of >= ceil(domain/32) words, zeroed) for every
+        key k < domain of rel; `outside` (int64[1] device tensor) += keys >= domain."""
+        if bitmap.numel() * 32 < domain:
+            raise ValueError("bitmap too small for the domain")
+        self._check(lib().hj3d_key_bitmap(self.h, C.byref(rel.c), domain, bitmap.data_ptr(),
+                                          outside.data_ptr() if outside is not None else None), "hj3d_key_bitmap")
+
+    def bitmap_or_popcount(self, bitmaps, count):
+        """count (int64[1] device tensor) += popcount of the OR over the rows of `bitmaps`
+        ((rows, words) int32 device tensor)."""
+        rows, words = bitmaps.shape
+        self._check(lib().hj3d_bitmap_or_popcount(self.h, bitmaps.data_ptr(), rows, words, count.data_ptr()),
+                    "hj3d_bitmap_or_popcount")
+
+    def num_distinct(self, rel: Rel, domain: int) -> int:
+        """#dv of rel's keys (all < domain) on this GPU; synchronous."""
+        torch = _torch()
+        dev = f"cuda:{self.device}"
+        bm = torch.zeros((1, (domain + 31) // 32), dtype=torch.int32, device=dev)
+        cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+        self.key_bitmap(rel, domain, bm, cnt[1:])
+        self.bitmap_or_popcount(bm, cnt[:1])
+        self.sync()
+        c, out = cnt.tolist()
+        if out:
+            raise ValueError(f"{out} keys outside [0, {domain})")
+        return c
 
     def gen_keys(self, tensor, key_word: int, row_base: int, n_keys: int, seed: int):
         """n_keys == 0: identity (k = global row id); else a seeded permutation of [0, n_keys)."""

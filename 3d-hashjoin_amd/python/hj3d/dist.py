@@ -68,6 +68,54 @@ def exchange_async(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf
     return out, work
 
 
+def num_distinct(bitmap: torch.Tensor, or_popcount, group=None) -> int:
+    """Global number of distinct keys (the #dv pre-pass of SURVEY §8e step 1; the reference sizes
+    its build-on-S.a tables by #dv(S.a), main_experiment1.cc:453-454).
+
+    bitmap: this rank's key bitmap (int32 words, bit k set for every local key k; the word count
+    a multiple of the world size), e.g. from Context.key_bitmap. The bitmap is all-to-all'ed in
+    world equal slices, so rank r receives slice r of every rank's bitmap (1/world of the domain,
+    not the whole map as an all-gather would); `or_popcount((world, words/world) tensor) -> int`
+    ORs the received slices and counts their bits (Context.bitmap_or_popcount on the GPU); the
+    per-rank counts are summed. RCCL has no bitwise-OR reduction, hence the exchange."""
+    world = dist.get_world_size(group)
+    words = bitmap.numel()
+    if words % world:
+        raise ValueError(f"bitmap words ({words}) must be a multiple of the world size ({world})")
+    src = bitmap.reshape(-1)
+    if _host_staged(group) and src.is_cuda:
+        src = src.cpu()
+    recv = torch.empty_like(src)
+    dist.all_to_all_single(recv, src, group=group)
+    c = int(or_popcount(recv.view(world, words // world)))
+    t = torch.tensor([c], dtype=torch.int64, device="cpu" if _host_staged(group) else bitmap.device)
+    dist.all_reduce(t, group=group)
+    return int(t.item())
+
+
+def num_distinct_rel(ctx, rel, domain: int, group=None) -> int:
+    """num_distinct over the keys (< domain) of every rank's slice `rel`, bitmaps built and
+    popcounted by the engine (hj3d_key_bitmap / hj3d_bitmap_or_popcount)."""
+    world = dist.get_world_size(group)
+    words = (domain + 31) // 32
+    words = (words + world - 1) // world * world
+    dev = rel.tensor.device
+    bm = torch.zeros(words, dtype=torch.int32, device=dev)
+    cnt = torch.zeros(2, dtype=torch.int64, device=dev)
+    ctx.key_bitmap(rel, domain, bm, cnt[1:])
+
+    def or_popcount(slices):
+        c = torch.zeros(1, dtype=torch.int64, device=dev)
+        ctx.bitmap_or_popcount(slices.to(dev).contiguous(), c)
+        return int(c.item())
+
+    n = num_distinct(bm, or_popcount, group)
+    outside = allreduce_sum_u64([int(cnt[1].item())], dev)[0]
+    if outside:
+        raise ValueError(f"{outside} keys outside [0, {domain})")
+    return n
+
+
 def allreduce_sum_u64(values: list[int], device) -> list[int]:
     """Sum u64 counters over ranks (mod 2^64, as the reference's u64 counters would wrap)."""
     device = "cpu" if _host_staged() else device

@@ -205,6 +205,21 @@ hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t num_buck
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
 
+/* ---- #dv pre-pass (the number of distinct join-attribute values sizes the build-on-S.a plans:
+ * NB = #dv(S.a) / b, main_experiment1.cc:453-454 counts it with an unordered_set, 875, 1001,
+ * 1214 use it). One GPU: key_bitmap + or_popcount with rows = 1. Multi-GPU (SURVEY §8e step 1,
+ * hj3d/dist.py num_distinct): each rank builds the bitmap of its slice, the ranks all-to-all
+ * the bitmap in nranks equal slices, each ORs the slices it received (rows = nranks) and
+ * popcounts, and the counts are summed. ----
+ * hj3d_key_bitmap: sets bit k of bitmap_dev (u32 words, ceil(domain / 32) of them, zeroed by the
+ * caller) for every key k < domain of rel; outside_dev (u64, may be NULL) += #keys >= domain. */
+hj3d_status hj3d_key_bitmap(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t domain, void* bitmap_dev,
+                            void* outside_dev);
+/* count_dev (u64) += popcount of the OR of `rows` bitmaps of `words` u32 words each, stored
+ * back to back at bitmaps_dev. */
+hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps_dev, uint32_t rows, uint64_t words,
+                                    void* count_dev);
+
 /* ---- synthetic key/FK relations generated on the device (bench / full-size checks) ----
  * R.k = a seeded bijective permutation of [0, n_keys) (keys for global rows
  * [row_base, row_base+n)), written into tuple word key_off of an AoS buffer;

@@ -6,6 +6,8 @@ exchanges (key, row) pairs with hj3d.dist.exchange (all_to_all), and joins its r
 with the oracle over the full bucket space (only its own buckets are populated). The per-rank
 counters, all-reduced with hj3d.dist, must equal the single-table oracle on the whole relations:
 join cardinality, c_htProbeCmp, unnest counts, output checksums and the table statistics.
+#dv(S.a), which sizes the build-on-S.a plans, comes from the distributed pre-pass
+(hj3d.dist.num_distinct: bitmap slices all-to-all'ed, OR + popcount, summed).
 That is the property the device path relies on (bucket ranges keep per-bucket chain order when
 received segments are concatenated in source-rank order)."""
 import os
@@ -39,6 +41,19 @@ def partition(keys, rows, nb, parts):
     return pairs, counts
 
 
+def bitmap_np(keys, words):
+    """Bit k set for every key k (hj3d_key_bitmap restated)."""
+    bm = np.zeros(words, dtype=np.uint32)
+    np.bitwise_or.at(bm, keys >> 5, np.left_shift(np.uint32(1), (keys & 31).astype(np.uint32)))
+    return bm
+
+
+def or_popcount_np(slices):
+    """popcount of the OR over the rows (hj3d_bitmap_or_popcount restated)."""
+    x = np.bitwise_or.reduce(slices.numpy().view(np.uint32), axis=0)
+    return int(np.unpackbits(x.view(np.uint8)).sum())
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -59,7 +74,13 @@ def _worker(rank, port, case, q):
     try:
         nR, nS, skew = case
         Rk, Sa, _ = O.gen_exp1(nR, nS, skew, 1.0, 0)
-        dv = O.num_distinct(Sa)
+        # the #dv pre-pass: bitmaps of the local S.a slices, all-to-all'ed slices, OR + popcount
+        lo_s, hi_s = rank * nS // WORLD, (rank + 1) * nS // WORLD
+        words = -(-nR // 32)
+        words = -(-words // WORLD) * WORLD
+        bm = bitmap_np(Sa[lo_s:hi_s], words)
+        dv = hdist.num_distinct(torch.from_numpy(bm.view(np.int32)), or_popcount_np)
+        assert dv == O.num_distinct(Sa)
         out = {}
         for plan, (bkeys, pkeys, nb) in {
             "Csr": (Rk, Sa, nR), "Nsr": (Rk, Sa, nR), "Crs": (Sa, Rk, dv), "Nrs": (Sa, Rk, dv),
