@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--rehearse", action="store_true",
                    help="N>1 on ONE GPU: every rank on cuda:0, gloo exchange staged through host memory "
                         "(checks the multi-GPU code path; the numbers are not a scaling measurement)")
+    p.add_argument("--plan", default="Csr", choices=["Csr", "Nsr", "Nrs"],
+                   help="workload B plan: Csr chaining build R / probe S (the headline); Nsr 3D table on R.k, "
+                        "probe S + unnest; Nrs 3D table on S.a (NB = #dv(S.a) from the distributed pre-pass), "
+                        "probe R + unnest (config D's per-GPU 3D join)")
     p.add_argument("--workload", default="B", choices=["B", "C", "E"],
                    help="B: the headline key/FK chaining join (default); C: 3D table on Zipf(0.8) S.a, Nrs plan; "
                         "E: experiment-4 deferred unnesting (Ndu)")
@@ -174,7 +178,7 @@ def main():
 
     nR, nS = args.nR, args.nS
     nR_tot = nR * world
-    nb = max(nR_tot // args.b, 1)
+    plan = args.plan
     emit = not args.no_emit
     ctx = hj3d.Context(local)
     ctx.timing(True)
@@ -187,26 +191,41 @@ def main():
     ctx.gen_fk(S, 1, rank * nS, nR_tot, SEED_S)       # S.a ~ U[0, |R|)
     relR = hj3d.Rel(R, key_word=0, row_base=rank * nR)
     relS = hj3d.Rel(S, key_word=1, row_base=rank * nS)
+    # plan: build side, probe side, table kind (main_experiment1.cc: Csr 623-848, Nrs 969-1076,
+    # Nsr 1078-1185); every S tuple has exactly one partner, so each plan outputs |S| pairs
+    if plan == "Nrs":
+        # NB = #dv(S.a) / b: the pre-pass (bitmaps, all-to-all'ed slices, OR + popcount) outside
+        # the timed region, as the reference counts numDvSa at generation time
+        dv = hdist.num_distinct_rel(ctx, relS, nR_tot) if world > 1 else ctx.num_distinct(relS, nR_tot)
+        nb = max(dv // args.b, 1)
+        bT, pT, bRel, pRel, nB, nP, pkw, prow0 = S, R, relS, relR, nS, nR, 0, rank * nR
+    else:
+        dv = None
+        nb = max(nR_tot // args.b, 1)
+        bT, pT, bRel, pRel, nB, nP, pkw, prow0 = R, S, relR, relS, nR, nS, 1, rank * nS
+    kind = hj3d.HJ3D_CHAIN if plan == "Csr" else hj3d.HJ3D_NESTED
+    unique, unnest = plan == "Csr", plan != "Csr"
+    n_out_local = nS  # output pairs of this rank's share (uniform FKs: |S| per rank)
 
     if world == 1:
-        table = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nb)
-        table.reserve(nR)
-        out = torch.empty((nS, 2), dtype=torch.int32, device=dev) if emit else None
+        table = hj3d.Table(ctx, kind, nb)
+        table.reserve(nB)
+        out = torch.empty((n_out_local, 2), dtype=torch.int32, device=dev) if emit else None
     else:
         lo, hi = hj3d.part_range(nb, world, rank)
-        table = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nb, lo, hi)
+        table = hj3d.Table(ctx, kind, nb, lo, hi)
         slack = 1.05
-        table.reserve(int(nR * slack) + 4096)
-        sendR = torch.empty((nR, 2), dtype=torch.int32, device=dev)
-        sendS = torch.empty((nS, 2), dtype=torch.int32, device=dev)
-        cntR = torch.zeros(world, dtype=torch.int64, device=dev)
+        table.reserve(int(nB * slack) + 4096)
+        sendB = torch.empty((nB, 2), dtype=torch.int32, device=dev)
+        sendP = torch.empty((nP, 2), dtype=torch.int32, device=dev)
+        cntB = torch.zeros(world, dtype=torch.int64, device=dev)
         C = max(1, args.chunks)
-        sb = [nS * c // C for c in range(C + 1)]
-        relS_c = [hj3d.Rel(S[sb[c]:sb[c + 1]], key_word=1, row_base=rank * nS + sb[c]) for c in range(C)]
-        cntS = torch.zeros((C, world), dtype=torch.int64, device=dev)
-        recvR = torch.empty((int(nR * slack) + 4096, 2), dtype=torch.int32, device=dev)
-        recvS = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev)
-        out = torch.empty((int(nS * slack) + 4096, 2), dtype=torch.int32, device=dev) if emit else None
+        sb = [nP * c // C for c in range(C + 1)]
+        pRel_c = [hj3d.Rel(pT[sb[c]:sb[c + 1]], key_word=pkw, row_base=prow0 + sb[c]) for c in range(C)]
+        cntP = torch.zeros((C, world), dtype=torch.int64, device=dev)
+        recvB = torch.empty((int(nB * slack) + 4096, 2), dtype=torch.int32, device=dev)
+        recvP = torch.empty((int(nP * slack) + 4096, 2), dtype=torch.int32, device=dev)
+        out = torch.empty((int(n_out_local * slack) + 4096, 2), dtype=torch.int32, device=dev) if emit else None
     torch.cuda.synchronize()
 
     state = {}
@@ -216,28 +235,30 @@ def main():
         if work is not None:
             work.wait()
         n = rS.shape[0]
-        ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=True,
-                  out=out[ooff:ooff + n] if out is not None else None, fetch=False,
+        o = out[ooff:] if out is not None else None
+        ctx.probe(table, hj3d.Rel(rS, key_word=0, row_word=1), unique=unique, unnest=unnest, out=o, fetch=False,
                   checksum=state.get("ck", False), accumulate=not first)
-        return ooff + n
+        # outputs of this chunk: one per probe tuple (unique chaining probe, dense slots), else the
+        # unnest count so far (read back: the next chunk's slots follow)
+        return ooff + n if unique else ctx.probe_result().n_out
 
     def step(ev):
         ev[0].record()
         if world == 1:
-            table.build(relR)
+            table.build(bRel)
             ev[1].record()
-            ctx.probe(table, relS, unique=True, out=out, fetch=False, checksum=state.get("ck", False))
+            ctx.probe(table, pRel, unique=unique, unnest=unnest, out=out, fetch=False, checksum=state.get("ck", False))
         else:
-            ctx.partition(relR, nb, world, sendR, cntR)
-            rR = hdist.exchange(sendR, cntR, recvR)
-            table.build(hj3d.Rel(rR, key_word=0, row_word=1))
+            ctx.partition(bRel, nb, world, sendB, cntB)
+            rB = hdist.exchange(sendB, cntB, recvB)
+            table.build(hj3d.Rel(rB, key_word=0, row_word=1))
             ev[1].record()
-            # S in C chunks: partition chunk c, start its all-to-all, then probe chunk c-1 while
-            # chunk c is in flight (results accumulate into one probe strand)
+            # the probe side in C chunks: partition chunk c, start its all-to-all, then probe
+            # chunk c-1 while chunk c is in flight (results accumulate into one probe strand)
             roff, ooff, pend, first = 0, 0, None, True
             for c in range(C):
-                ctx.partition(relS_c[c], nb, world, sendS[sb[c]:sb[c + 1]], cntS[c])
-                rS, work = hdist.exchange_async(sendS[sb[c]:sb[c + 1]], cntS[c], recvS[roff:])
+                ctx.partition(pRel_c[c], nb, world, sendP[sb[c]:sb[c + 1]], cntP[c])
+                rS, work = hdist.exchange_async(sendP[sb[c]:sb[c + 1]], cntP[c], recvP[roff:])
                 roff += rS.shape[0]
                 if pend is not None:
                     ooff = probe_chunk(pend, ooff, first)
@@ -269,7 +290,8 @@ def main():
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     # per-kernel averages over the timed steps (HIP events on the engine's stream)
     kern_avg = {}
-    for name, ph in (("k_rp_probe_seg", hj3d.T_PROBE_KERNEL), ("k_rp_part1", hj3d.T_SCATTER)):
+    kprobe = "k_rp_probe_seg" if unique else "k_rn_probe_seg"
+    for name, ph in ((kprobe, hj3d.T_PROBE_KERNEL), ("k_rp_part1", hj3d.T_SCATTER)):
         ms, cnt = ctx.timer(ph)
         kern_avg[name] = ms / cnt if cnt else None
     # verification step (outside the timed region): the same step once more with the
@@ -279,11 +301,11 @@ def main():
     torch.cuda.synchronize()
     res = ctx.probe_result()
     wall_ms = wall * 1e3 / args.steps
-    probe_n_local = state.get("probe_n", nS)
+    probe_n_local = state.get("probe_n", nP)
 
     # ---- verification of the last step (bit-exact, size-independent) ----
     expd = torch.zeros(8, dtype=torch.int64, device=dev)
-    ctx.expected_fk_join_gen(relS, nR_tot, SEED_R, swap=False, res=expd)
+    ctx.expected_fk_join_gen(relS, nR_tot, SEED_R, swap=plan == "Nrs", res=expd)
     torch.cuda.synchronize()
     exp_local = [int(x) & hj3d.MASK64 for x in expd.cpu().tolist()[:5]]
     got_local = [res.n_out, res.sum_a, res.sum_b, res.sum_h]
@@ -317,10 +339,20 @@ def main():
     launches = 1 if world == 1 else max(1, args.chunks)
     n = probe_n_local / launches  # probe tuples per kernel launch
     tuple_bytes = 12 if world == 1 else 8
-    alg = {
-        "k_rp_part1": n * (tuple_bytes + 8),
-        "k_rp_probe_seg": n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4,
-    }
+    #   k_rn_probe_seg (3D plans, unnest materialised): n * (8 + 16) read the pair, write the slot's
+    #                  output count (8), sub offset and probe row (4 + 4); + the slices (directory +
+    #                  16-B main records) once. The expansion kernels that follow are not in this timer.
+    if unique:
+        alg = {
+            "k_rp_part1": n * (tuple_bytes + 8),
+            kprobe: n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4,
+        }
+    else:
+        n_keys = dv if plan == "Nrs" else nR_tot
+        alg = {
+            "k_rp_part1": n * (tuple_bytes + 8),
+            kprobe: n * (8 + (16 if emit else 0)) + (n_keys // world) * 16 + (nb // world) * 4,
+        }
     kernels = {}
     for k, ms in kern_avg.items():
         if ms:
@@ -329,7 +361,7 @@ def main():
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     traffic = None
     pmc = None
-    if world == 1 and args.pmc_json and os.path.exists(args.pmc_json):
+    if world == 1 and plan == "Csr" and args.pmc_json and os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
@@ -342,13 +374,19 @@ def main():
         for k in kernels:
             if k in pmc:
                 kernels[k]["traffic"] = pmc[k].get("traffic_bytes_per_launch")
-    # the whole probe phase (partition + probe; N > 1: + exchange) against the plan's 28 B per probe
-    phase_alg = probe_n_local * (tuple_bytes + 8 + (8 if emit else 0))
+    # the whole probe phase (partition + probe; N > 1: + exchange) against SURVEY §8(d): 20 B per
+    # probe tuple + per output 8 B (chaining) or 4 + 8 B (unnest: sub row read, pair write)
+    phase_alg = probe_n_local * (tuple_bytes + 8) + nS * ((8 if emit else 0) + (0 if unique else 4))
+    if unique:
+        metric, unit = METRIC, "probe tuples/s"
+    else:
+        metric, unit = (f"unnested output tuples/s (probe + unnest phase), exp1 key/FK plan {plan}",
+                        "output tuples/s")
 
     line = {
-        "metric": METRIC,
-        "value": nS * world / (probe_ms * 1e-3),
-        "unit": "probe tuples/s",
+        "metric": metric,
+        "value": nS * world / (probe_ms * 1e-3),  # |S| probe tuples (Csr) = |S| output pairs (every plan)
+        "unit": unit,
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -359,8 +397,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic (device-generated: R.k = seeded permutation of [0,|R|), S.a ~ U[0,|R|))",
         "config": {
-            "workload": f"exp1 key/FK plan Csr, |R|={nR} |S|={nS} per GPU, uniform FKs, b={args.b}",
-            "plan": "Csr", "R_per_gpu": nR, "S_per_gpu": nS, "num_buckets": nb,
+            "workload": f"exp1 key/FK plan {plan}, |R|={nR} |S|={nS} per GPU, uniform FKs, b={args.b}",
+            "plan": plan, "R_per_gpu": nR, "S_per_gpu": nS, "num_buckets": nb, "num_dv_Sa": dv,
             "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if world > 1 else "single GPU",
             "exchange_chunks": (max(1, args.chunks) if world > 1 else None),
             "rehearsal_one_gpu": bool(args.rehearse),
@@ -380,7 +418,7 @@ def main():
         "counters": {"c_top": got_sum[0], "c_htProbeCmp": cmps},
         "verified_bit_exact": verified,
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and plan == "Csr":
         m = min(args.cpu_sample, nS)
         line["cpu_baseline"] = cpu_baseline_reference(nR, m, args.cpu_reps)
         if line["cpu_baseline"] is None:

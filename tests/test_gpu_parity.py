@@ -284,3 +284,32 @@ def test_bucket_shards_sum_to_single_table(ctx):
         assert tot["n_out"] == ref["out"]["n"], plan
         assert (tot["sum_h"], tot["xor_h"]) == (ref["out"]["sum_h"], ref["out"]["xor_h"]), plan
         assert tot["empty"] == ref["stats"]["empty"] and tot["cc0_max"] == ref["stats"]["cc0_max"], plan
+
+
+@pytest.mark.parametrize("name,g", [x for x in EXP1 if x[1]["nS"] <= 1_100_000], ids=lambda v: v if isinstance(v, str) else "")
+def test_num_distinct_bitmap_matches_reference(ctx, name, g):
+    """#dv(S.a) from the device pre-pass (hj3d_key_bitmap + hj3d_bitmap_or_popcount) equals the
+    reference's numDvSa (unordered_set, main_experiment1.cc:453-454) recorded in the fixture; the
+    same count from two half-bitmaps OR'ed (the multi-GPU form, rows = 2) and the outside count."""
+    import torch
+    import hj3d
+    _, S, _ = exp1_rel(g)
+    nR = g["nR"]
+    relS = hj3d.Rel(dev(S), key_word=1)
+    assert ctx.num_distinct(relS, nR) == g["numDvSa"]
+    n = S.shape[0]
+    words = (nR + 31) // 32
+    bm = torch.zeros((2, words), dtype=torch.int32, device="cuda")
+    out = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.key_bitmap(hj3d.Rel(dev(S[: n // 2]), key_word=1), nR, bm[0], out)
+    ctx.key_bitmap(hj3d.Rel(dev(S[n // 2:]), key_word=1), nR, bm[1], out)
+    cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+    ctx.bitmap_or_popcount(bm, cnt)
+    assert int(cnt.item()) == g["numDvSa"] and int(out.item()) == 0
+    # a domain that excludes the largest keys counts them as outside
+    k = int(S[:, 1].max())
+    if k == 0:
+        return
+    bm2 = torch.zeros((1, (k + 31) // 32), dtype=torch.int32, device="cuda")
+    ctx.key_bitmap(relS, k, bm2[0], out)
+    assert int(out.item()) == int((S[:, 1] >= k).sum())
