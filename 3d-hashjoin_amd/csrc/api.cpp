@@ -112,6 +112,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_FORCE_DIRECT: ctx->force_direct = value != 0; return HJ3D_OK;
     case HJ3D_OPT_RADIX_MIN: ctx->radix_min = value < 0 ? 0 : uint64_t(value); return HJ3D_OK;
     case HJ3D_OPT_NESTED_RADIX: ctx->nested_radix = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_NESTED_SORT: ctx->nested_sort = value != 0; return HJ3D_OK;
     default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
   }
 }
@@ -251,6 +252,7 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   } else {
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
                                                   : hipErrorNotSupported;
+    if (e == hipErrorNotSupported && !ctx->nested_sort) e = nested_build_agg(ctx, t, *build, ctx->stream);
     if (e == hipErrorNotSupported) e = nested_build(ctx, t, *build, ctx->stream);
     // the partitioned probe sizes its LDS slices by the number of main records
     t->n_mains = 0;

@@ -67,6 +67,7 @@ struct hj3d_ctx {
   bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
   uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
   bool nested_radix = false;      // HJ3D_OPT_NESTED_RADIX
+  bool nested_sort = false;       // HJ3D_OPT_NESTED_SORT
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;
@@ -102,6 +103,11 @@ hipError_t radix_sort_pairs(hj3d_ctx* ctx, uint32_t* k0, uint32_t* v0, uint32_t*
 bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
 // rows_sorted (optional): set when the small buckets already come out sorted by row.
 hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, bool* rows_sorted = nullptr);
+// Partition r into (hash, row) pairs by ranges of W local buckets (LDS-histogram pass, scan,
+// LDS-staged scatter): partition p is out[ps[p] .. ps[p+1]), *nparts = ceil(nb_local / W).
+// Uses scratch kScrPHist. hipErrorNotSupported beyond 2048 partitions.
+hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
+                                 uint32_t* ps, uint32_t* nparts, hipStream_t s);
 // after every chaining build: buckets of <= 32 entries sorted by row (single-pass probe order)
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
@@ -127,6 +133,9 @@ hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
                        uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // nested.hip
 hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+// nested_agg.hip: the nested build by bucket-range partition + per-partition LDS aggregation.
+// hipErrorNotSupported when not applicable (small inputs / tables): use nested_build.
+hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 // nested_radix.hip: nested build from the radix-partitioned bucket CSR (large inputs);
 // hipErrorNotSupported when a bucket holds too many distinct keys (use nested_build).
 bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n);

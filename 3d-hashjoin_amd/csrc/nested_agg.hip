@@ -1,0 +1,325 @@
+// nested_agg.hip — build of the nested ("3D") table by bucket-range partition + per-partition
+// aggregation in LDS (the default nested build for large inputs).
+//
+// The nested table (nested.hip) needs, per bucket, one main record per distinct key {hash,
+// first_row, sub_off, sub_len} and every key's rows contiguous in `sub` (HtNested1: a main node
+// per distinct key with its duplicates in a sub-chain, ht_nested.hh:287-311, 386-436). Neither the
+// order of the mains inside a bucket nor the order of the rows inside a key matters: the probe
+// derives the reference's comparison count from first-row ranks and unnest output is order-free.
+// So instead of sorting all tuples by key (3 LSD passes at 16 B/tuple each, nested.hip):
+//   1. partition the build tuples into (hash, row) pairs by ranges of kAggW buckets
+//      (radix_partition_pairs: one histogram pass, one LDS-staged scatter pass);
+//   2. one workgroup per partition inserts the partition's keys into an LDS hash table (count +
+//      min row per key; a hot key's lanes are aggregated per wave first, so Zipf skew costs one
+//      LDS atomic per wave, not per tuple), assigns every key its main slot (bucket order) and
+//      sub range, then reads the pairs again and scatters every row into its key's sub range.
+//      A range whose distinct keys do not fit the table is retried in halves (many keys per
+//      bucket), so the table never overflows; below kAggMinSpan buckets per round the build
+//      gives up (hipErrorNotSupported) and the sort-based build runs instead;
+//   3. the partitions' main records are compacted and the directory offsets rebased (scan of
+//      the per-partition key counts).
+// Traffic: 12 B read (tuple) x 2 + 8 B write + 2 x 8 B read (pairs) + 4 B write (sub) per tuple,
+// + 16 B per distinct key (twice) + 4 B per bucket.
+#include "hj3d_internal.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kAggBlock = 1024;
+constexpr uint32_t kAggW = 6144;     // buckets per partition (one LDS table round at fill <= ~1.3)
+constexpr uint32_t kAggCap = 10240;  // LDS hash table slots
+// new keys are admitted while fewer than this many are in the table: at most kAggBlock inserts
+// race past the test, so the table never fills and every probe sequence ends
+constexpr uint32_t kAggLimit = kAggCap - kAggBlock - 64;
+constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
+constexpr int kAggU = 4;             // pairs per thread in flight per step
+constexpr int kWavesA = kAggBlock / kWave;
+
+__device__ __forceinline__ uint32_t slot_of(uint32_t h) { return __umulhi(h * 0x9E3779B1u, kAggCap); }
+
+// Slot of key h, inserting it if absent (returns kInvalid when the table is at its limit: the
+// caller flags the round as overflowing).
+__device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t* nkeys) {
+  uint32_t s = slot_of(h);
+  for (;;) {
+    const uint32_t k = tkey[s];
+    if (k == h) return s;
+    if (k == empty) {
+      if (*nkeys >= kAggLimit) return kInvalid;
+      const uint32_t old = atomicCAS(&tkey[s], empty, h);
+      if (old == empty) {
+        atomicAdd(nkeys, 1u);
+        return s;
+      }
+      if (old == h) return s;
+    }
+    s = s + 1 == kAggCap ? 0u : s + 1;
+  }
+}
+
+__device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h) {
+  uint32_t s = slot_of(h);
+  while (tkey[s] != h) s = s + 1 == kAggCap ? 0u : s + 1;
+  return s;
+}
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = min(v, uint32_t(__shfl_xor(int(v), o, kWave)));
+  return v;
+}
+
+// Exclusive scan of a[0..n) in LDS by kAggBlock threads (contiguous chunks per thread); returns
+// the total. All threads must call it.
+__device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
+  const uint32_t per = (n + kAggBlock - 1) / kAggBlock;
+  const uint32_t b = threadIdx.x * per, e = min(n, b + per);
+  uint32_t t = 0;
+  for (uint32_t i = b; i < e; ++i) t += a[i];
+  uint32_t wt;
+  const uint32_t wpre = wave_excl_scan(t, &wt);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 63) wsum[wid] = wpre + t;
+  __syncthreads();
+  uint32_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < kWavesA; ++w) {
+    const uint32_t x = wsum[w];
+    if (w < wid) pre += x;
+    tot += x;
+  }
+  pre += wpre;
+  for (uint32_t i = b; i < e; ++i) {
+    const uint32_t x = a[i];
+    a[i] = pre;
+    pre += x;
+  }
+  __syncthreads();
+  return tot;
+}
+
+// One workgroup per partition p (local buckets [b0, b0 + nbs), pairs [ps[p], ps[p+1])).
+// Writes: off[b0 + k] = partition-local main offset of bucket k; mtmp[ps[p] + i] the partition's
+// main records in bucket order (i < its key count, with sub_off global); sub rows; dcount[p].
+__global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                    FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global,
+                                                    uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
+                                                    uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
+                                                    unsigned long long* __restrict__ maxlen,
+                                                    uint32_t* __restrict__ fail) {
+  __shared__ uint32_t tkey[kAggCap];
+  __shared__ uint32_t tcnt[kAggCap];  // count, then the sub cursor
+  __shared__ uint32_t tmin[kAggCap];  // min row, then (after the main records are written) unused
+  __shared__ uint32_t bcnt[kAggW];    // keys per bucket of the round, then their main offsets
+  __shared__ uint32_t wsum[kWavesA];
+  __shared__ uint32_t nkeys, ovf;
+  const uint32_t p = blockIdx.x;
+  const uint32_t b0 = p * kAggW, nbs = min(kAggW, nbl - b0);
+  const uint32_t e0 = ps[p], e1 = ps[p + 1];
+  const int lane = threadIdx.x & 63;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint32_t mrun = 0, srun = 0, mxlen = 0;  // keys and rows of the finished rounds
+  uint32_t c0 = 0, span = nbs;
+  while (c0 < nbs) {
+    const uint32_t c1 = min(nbs, c0 + span);
+    // a hash that no key of this round has: its bucket lies outside [b0 + c0, b0 + c1)
+    const uint32_t empty = uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
+    for (uint32_t s = threadIdx.x; s < kAggCap; s += kAggBlock) {
+      tkey[s] = empty;
+      tcnt[s] = 0;
+      tmin[s] = kInvalid;
+    }
+    for (uint32_t k = threadIdx.x; k < c1 - c0; k += kAggBlock) bcnt[k] = 0;
+    if (threadIdx.x == 0) {
+      nkeys = 0;
+      ovf = 0;
+    }
+    __syncthreads();
+    // ---- pass A: count and min row per key ----
+    for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
+      uint2 v[kAggU];
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        const uint32_t lb = fm.mod(v[u].x) - lo - b0;
+        bool act = i < e1 && lb >= c0 && lb < c1;
+        const uint64_t am = __ballot(act);
+        if (am) {  // the wave's first active key: aggregated (a Zipf hot key fills most lanes)
+          const int leader = __ffsll((unsigned long long)am) - 1;
+          const uint32_t hl = uint32_t(__shfl(int(v[u].x), leader, kWave));
+          const bool mine = act && v[u].x == hl;
+          const uint64_t same = __ballot(mine);
+          const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
+          if (lane == leader) {
+            const uint32_t s = tab_insert(tkey, hl, empty, &nkeys);
+            if (s == kInvalid) {
+              ovf = 1;
+            } else {
+              atomicAdd(&tcnt[s], uint32_t(__popcll(same)));
+              atomicMin(&tmin[s], rmin);
+            }
+          }
+          act = act && !mine;
+        }
+        if (act) {
+          const uint32_t s = tab_insert(tkey, v[u].x, empty, &nkeys);
+          if (s == kInvalid) {
+            ovf = 1;
+          } else {
+            atomicAdd(&tcnt[s], 1u);
+            atomicMin(&tmin[s], v[u].y);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (ovf) {  // too many distinct keys for one round: retry the first half of the range
+      if (c1 - c0 <= kAggMinSpan) {  // > ~24 keys per bucket: the sort-based build instead
+        if (threadIdx.x == 0) atomicOr(fail, 1u);
+        return;
+      }
+      span = (c1 - c0 + 1) / 2;
+      __syncthreads();
+      continue;
+    }
+    // ---- main slots: rank of every key inside its bucket (registers), bucket offsets ----
+    // (empty slots: tkey = empty, tcnt = 0, tmin = kInvalid)
+    uint32_t rank[kAggCap / kAggBlock];
+#pragma unroll
+    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) {
+      const uint32_t s = j * kAggBlock + threadIdx.x;
+      rank[j] = tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t nk = block_scan_lds(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
+    // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
+    uint32_t cnt[kAggCap / kAggBlock];
+#pragma unroll
+    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) cnt[j] = tcnt[j * kAggBlock + threadIdx.x];
+    __syncthreads();
+    const uint32_t nrows = block_scan_lds(tcnt, kAggCap, wsum);
+    // main records (partition-local slots, global sub offsets) and the round's directory words
+#pragma unroll
+    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) {
+      const uint32_t s = j * kAggBlock + threadIdx.x;
+      if (cnt[j]) {
+        const uint32_t h = tkey[s];
+        const uint32_t m = mrun + bcnt[fm.mod(h) - lo - b0 - c0] + rank[j];
+        const uint32_t so = e0 + srun + tcnt[s];
+        mtmp[e0 + m] = make_uint4(h, tmin[s], so, cnt[j]);
+        tcnt[s] = so;  // sub cursor
+        mxlen = max(mxlen, cnt[j]);
+      }
+    }
+    for (uint32_t k = threadIdx.x; k < c1 - c0; k += kAggBlock) off[b0 + c0 + k] = mrun + bcnt[k];
+    __syncthreads();
+    // ---- pass B: rows into their keys' sub ranges ----
+    for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
+      uint2 v[kAggU];
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        const uint32_t lb = fm.mod(v[u].x) - lo - b0;
+        bool act = i < e1 && lb >= c0 && lb < c1;
+        const uint64_t am = __ballot(act);
+        if (am) {
+          const int leader = __ffsll((unsigned long long)am) - 1;
+          const uint32_t hl = uint32_t(__shfl(int(v[u].x), leader, kWave));
+          const bool mine = act && v[u].x == hl;
+          const uint64_t same = __ballot(mine);
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl)], uint32_t(__popcll(same)));
+          base = uint32_t(__shfl(int(base), leader, kWave));
+          if (mine) sub[base + uint32_t(__popcll(same & lt))] = v[u].y;
+          act = act && !mine;
+        }
+        if (act) sub[atomicAdd(&tcnt[tab_find(tkey, v[u].x)], 1u)] = v[u].y;
+      }
+    }
+    mrun += nk;
+    srun += nrows;
+    c0 = c1;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dcount[p] = mrun;
+  const uint64_t wm = wave_max(uint64_t(mxlen));
+  if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+}
+
+// off[b] += first main of b's partition; main records moved to their final slots.
+__global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ off, uint32_t nbl,
+                                                        const uint32_t* __restrict__ mbase) {
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[b / kAggW];
+}
+
+__global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
+                                                       const uint32_t* __restrict__ mbase, uint4* __restrict__ mains) {
+  const uint32_t p = blockIdx.x;
+  const uint32_t n = mbase[p + 1] - mbase[p];
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[mbase[p] + i] = mtmp[ps[p] + i];
+}
+
+__global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t P,
+                              uint32_t nbl, uint32_t* __restrict__ off, uint64_t* __restrict__ counts) {
+  counts[0] = ps[P];
+  counts[1] = mbase[P];
+  off[nbl] = mbase[P];
+}
+
+}  // namespace
+
+hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+  const uint64_t n = r.n;
+  const uint32_t nbl = t->nb_local;
+  // small inputs and tables that one partition would cover (no free bucket for the LDS table's
+  // empty marker) take the sort-based build
+  if (ctx->force_direct || n < (ctx->radix_min >> 4) || n >= (1ull << 31) || nbl <= kAggW ||
+      t->desc.num_buckets >= (1ull << 32))
+    return hipErrorNotSupported;
+  hipError_t e;
+  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->main.ensure(n * sizeof(uint4))) != hipSuccess) return e;
+  if ((e = t->sub.ensure(n * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
+  const uint32_t P = (nbl + kAggW - 1) / kAggW;
+  // scratch: pairs (n uint2) | main records before compaction (n uint4) | starts, key counts
+  if ((e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPStart].ensure((2 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
+  uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
+  uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
+  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
+  uint32_t* dcount = ps + P + 2;  // P + 1 (scanned in place into the main bases)
+  uint32_t np = 0;
+  if ((e = radix_partition_pairs(ctx, t, r, kAggW, pairs, ps, &np, s)) != hipSuccess) return e;
+  if (np != P) return hipErrorNotSupported;
+  uint64_t* counts = t->counts.as<uint64_t>();
+  uint32_t* off = t->off.as<uint32_t>();
+  if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+  uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
+  hipLaunchKernelGGL(k_nagg, dim3(P), dim3(kAggBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
+                     uint32_t(t->desc.num_buckets), off, mtmp, t->sub.as<uint32_t>(), dcount,
+                     reinterpret_cast<unsigned long long*>(counts + 2), fail);
+  uint32_t hfail = 0;
+  if ((e = hipMemcpyAsync(&hfail, fail, sizeof(hfail), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  if (hfail) return hipErrorNotSupported;  // table untouched apart from scratch: the caller sorts
+  if ((e = exclusive_scan_u32(ctx, dcount, dcount, P, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl, dcount);
+  hipLaunchKernelGGL(k_nagg_mains, dim3(P), dim3(kBlock), 0, s, mtmp, ps, dcount, t->main.as<uint4>());
+  hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(1), 0, s, ps, dcount, P, nbl, off, counts);
+  t->n_build = n;
+  return hipGetLastError();
+}
+
+}  // namespace hj3d

@@ -961,6 +961,14 @@ bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n
          t->nb_local >= 64 && n_probe < (1ull << 32);
 }
 
+hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
+                                 uint32_t* ps, uint32_t* nparts, hipStream_t s) {
+  const Plan pl = plan_for(t->nb_local, W, r.n);
+  if (pl.P > kMaxParts) return hipErrorNotSupported;
+  *nparts = pl.P;
+  return partition_pairs(ctx, t, r, pl, out, ps, s);
+}
+
 hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, bool* rows_sorted) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;

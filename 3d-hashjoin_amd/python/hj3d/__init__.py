@@ -25,7 +25,7 @@ HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
-OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX = 1, 2, 3
+OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT = 1, 2, 3, 4
 
 MASK64 = (1 << 64) - 1
 
@@ -224,6 +224,10 @@ class Context:
     def nested_radix(self, on: bool = True):
         """Nested builds from the radix-partitioned bucket CSR instead of the key sort."""
         self.set_option(OPT_NESTED_RADIX, int(on))
+
+    def nested_sort(self, on: bool = True):
+        """Nested builds by the LSD key sort instead of the partition + LDS aggregation build."""
+        self.set_option(OPT_NESTED_SORT, int(on))
 
     def radix_min(self, n: int):
         """Smallest probe side (tuples) that takes the radix-partitioned chaining kernels."""

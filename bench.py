@@ -61,6 +61,9 @@ def parse():
                    help="B: the headline key/FK chaining join (default); C: 3D table on Zipf(0.8) S.a, Nrs plan; "
                         "E: experiment-4 deferred unnesting (Ndu)")
     p.add_argument("--theta", type=float, default=0.8, help="config C Zipf parameter")
+    p.add_argument("--nested-build", default="agg", choices=["agg", "sort", "radix"],
+                   help="3D build: bucket-range partition + LDS aggregation (default), LSD key sort "
+                        "(HJ3D_OPT_NESTED_SORT), radix bucket CSR + per-bucket grouping (HJ3D_OPT_NESTED_RADIX)")
     p.add_argument("--log2R", type=int, default=23, help="config E: |R| = 2^log2R")
     return p.parse_args()
 
@@ -463,6 +466,10 @@ def main_single_config(args):
     torch.cuda.set_device(0)
     ctx = hj3d.Context(0)
     ctx.timing(True)
+    if args.nested_build == "radix":
+        ctx.nested_radix(True)
+    elif args.nested_build == "sort":
+        ctx.nested_sort(True)
 
     if args.workload == "C":
         nR, nS = args.nR, args.nS

@@ -141,7 +141,11 @@ enum {
   /* HJ3D_OPT_NESTED_RADIX (0/1, default 0): build nested tables from the radix-partitioned bucket
    * CSR with per-bucket key grouping instead of the key sort (faster at low bucket fill, slower
    * under heavy skew). */
-  HJ3D_OPT_NESTED_RADIX = 3
+  HJ3D_OPT_NESTED_RADIX = 3,
+  /* HJ3D_OPT_NESTED_SORT (0/1, default 0): build nested tables by the LSD key sort (nested.hip)
+   * instead of the bucket-range partition + per-partition LDS aggregation (nested_agg.hip, the
+   * default for large inputs). */
+  HJ3D_OPT_NESTED_SORT = 4
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

@@ -156,6 +156,35 @@ def test_nested_many_keys_per_bucket(ctx, nb, path):
         ctx.nested_radix(False)
 
 
+@pytest.mark.parametrize("zipf", [False, True], ids=["uniform", "zipf"])
+@pytest.mark.parametrize("nb", [7000, 20000, 100000, 250000])
+def test_nested_agg_build_vs_oracle(ctx, nb, zipf):
+    """The partition + LDS aggregation nested build (nested_agg.hip) at ~14, 5, 1 and 0.4 distinct
+    keys per bucket (the first splits every partition into several rounds), uniform and Zipf(1.0)
+    duplicates (hot keys aggregated per wave): counters, output checksums and statistics equal
+    the oracle's, and equal the LSD key-sort build's."""
+    import hj3d
+    rng = np.random.default_rng(nb + zipf)
+    nR, nS = 100_000, 400_000
+    Rk = rng.permutation(nR).astype(np.uint32)
+    Sa = (np.minimum(rng.zipf(1.3, nS) - 1, nR - 1) if zipf else rng.integers(0, nR, nS)).astype(np.uint32)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    ctx.radix_min(0)
+    try:
+        for plan, e in (("Nsr", O.nested_plan(R, 0, S, 1, nb, True)), ("Nrs", O.nested_plan(S, 1, R, 0, nb, True))):
+            for sort in (False, True):
+                ctx.nested_sort(sort)
+                got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb)
+                assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
+                    (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), (plan, sort)
+                assert got["out"] == e.out, (plan, sort)
+                assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, (plan, sort)
+    finally:
+        ctx.radix_min(1 << 20)
+        ctx.nested_sort(False)
+
+
 @pytest.mark.parametrize("path", ["default", "partitioned"])
 @pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
 def test_exp4_plans_bit_exact(ctx, name, g, path):
