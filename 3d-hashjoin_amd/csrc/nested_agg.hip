@@ -27,20 +27,32 @@ namespace {
 
 constexpr int kAggBlock = 1024;
 constexpr uint32_t kAggW = 6144;     // buckets per partition (one LDS table round at fill <= ~1.3)
-constexpr uint32_t kAggCap = 10240;  // LDS hash table slots
+// LDS hash table slots, prime: with double hashing every probe step visits all slots (double
+// hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6)
+constexpr uint32_t kAggCap = 10223;
+constexpr uint32_t kAggSlotsPer = (kAggCap + 1023) / 1024;  // slots per thread in the per-slot loops
 // new keys are admitted while fewer than this many are in the table: at most kAggBlock inserts
 // race past the test, so the table never fills and every probe sequence ends
 constexpr uint32_t kAggLimit = kAggCap - kAggBlock - 64;
+constexpr uint32_t kAggRounds = 1;  // initial rounds per partition (2, 3: slower under Zipf, pairs re-read)
 constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
-constexpr int kAggU = 4;             // pairs per thread in flight per step
+constexpr int kAggU = 8;             // pairs per thread and step (the next step's in flight)
 constexpr int kWavesA = kAggBlock / kWave;
 
 __device__ __forceinline__ uint32_t slot_of(uint32_t h) { return __umulhi(h * 0x9E3779B1u, kAggCap); }
+// per-key probe step in [1, kAggCap) (double hashing: no primary clusters, so the longest probe
+// sequence among a wave's 64 lanes, which the whole wave waits for, stays short)
+__device__ __forceinline__ uint32_t step_of(uint32_t h) { return 1u + __umulhi(h * 0x85EBCA6Bu, kAggCap - 1); }
+__device__ __forceinline__ uint32_t next_slot(uint32_t s, uint32_t st) {
+  s += st;
+  return s >= kAggCap ? s - kAggCap : s;
+}
 
 // Slot of key h, inserting it if absent (returns kInvalid when the table is at its limit: the
 // caller flags the round as overflowing).
 __device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t* nkeys) {
   uint32_t s = slot_of(h);
+  const uint32_t st = step_of(h);
   for (;;) {
     const uint32_t k = tkey[s];
     if (k == h) return s;
@@ -53,13 +65,23 @@ __device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint3
       }
       if (old == h) return s;
     }
-    s = s + 1 == kAggCap ? 0u : s + 1;
+    s = next_slot(s, st);
+  }
+}
+
+// kAggU pairs per thread of the partition's pairs from i0 (coalesced: pair i0 + u * block + tid)
+__device__ __forceinline__ void load_batch(const uint2* __restrict__ pairs, uint32_t i0, uint32_t e1, uint2 (&v)[kAggU]) {
+#pragma unroll
+  for (int u = 0; u < kAggU; ++u) {
+    const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+    v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
   }
 }
 
 __device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h) {
   uint32_t s = slot_of(h);
-  while (tkey[s] != h) s = s + 1 == kAggCap ? 0u : s + 1;
+  const uint32_t st = step_of(h);
+  while (tkey[s] != h) s = next_slot(s, st);
   return s;
 }
 
@@ -106,20 +128,20 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
                                                     uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
                                                     uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
                                                     unsigned long long* __restrict__ maxlen,
-                                                    uint32_t* __restrict__ fail) {
+                                                    uint32_t* __restrict__ fail, const uint32_t* __restrict__ order) {
   __shared__ uint32_t tkey[kAggCap];
   __shared__ uint32_t tcnt[kAggCap];  // count, then the sub cursor
   __shared__ uint32_t tmin[kAggCap];  // min row, then (after the main records are written) unused
   __shared__ uint32_t bcnt[kAggW];    // keys per bucket of the round, then their main offsets
   __shared__ uint32_t wsum[kWavesA];
   __shared__ uint32_t nkeys, ovf;
-  const uint32_t p = blockIdx.x;
+  const uint32_t p = order[blockIdx.x];
   const uint32_t b0 = p * kAggW, nbs = min(kAggW, nbl - b0);
   const uint32_t e0 = ps[p], e1 = ps[p + 1];
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   uint32_t mrun = 0, srun = 0, mxlen = 0;  // keys and rows of the finished rounds
-  uint32_t c0 = 0, span = nbs;
+  uint32_t c0 = 0, span = (nbs + kAggRounds - 1) / kAggRounds;
   while (c0 < nbs) {
     const uint32_t c1 = min(nbs, c0 + span);
     // a hash that no key of this round has: its bucket lies outside [b0 + c0, b0 + c1)
@@ -136,38 +158,45 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     }
     __syncthreads();
     // ---- pass A: count and min row per key ----
+    uint2 v[kAggU], nv[kAggU];
+    load_batch(pairs, e0, e1, v);
     for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
-      uint2 v[kAggU];
-#pragma unroll
-      for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
-        v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
-      }
+      if (i0 + kAggBlock * kAggU < e1) load_batch(pairs, i0 + kAggBlock * kAggU, e1, nv);  // next batch in flight
+      // home slots of all items read together (one LDS latency for the batch); only items whose
+      // key is not in its home slot walk the probe sequence
+      bool act[kAggU];
+      uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
         const uint32_t lb = fm.mod(v[u].x) - lo - b0;
-        bool act = i < e1 && lb >= c0 && lb < c1;
-        const uint64_t am = __ballot(act);
-        if (am) {  // the wave's first active key: aggregated (a Zipf hot key fills most lanes)
+        act[u] = i < e1 && lb >= c0 && lb < c1;
+        k0[u] = tkey[act[u] ? slot_of(v[u].x) : 0u];
+      }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint64_t am = __ballot(act[u]);
+        if (am) {  // the wave's first active key, if several lanes hold it (a Zipf hot key)
           const int leader = __ffsll((unsigned long long)am) - 1;
-          const uint32_t hl = uint32_t(__shfl(int(v[u].x), leader, kWave));
-          const bool mine = act && v[u].x == hl;
+          const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
+          const bool mine = act[u] && v[u].x == hl;
           const uint64_t same = __ballot(mine);
-          const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
-          if (lane == leader) {
-            const uint32_t s = tab_insert(tkey, hl, empty, &nkeys);
-            if (s == kInvalid) {
-              ovf = 1;
-            } else {
-              atomicAdd(&tcnt[s], uint32_t(__popcll(same)));
-              atomicMin(&tmin[s], rmin);
+          if (__popcll(same) > 1) {
+            const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
+            if (lane == leader) {
+              const uint32_t s = tab_insert(tkey, hl, empty, &nkeys);
+              if (s == kInvalid) {
+                ovf = 1;
+              } else {
+                atomicAdd(&tcnt[s], uint32_t(__popcll(same)));
+                atomicMin(&tmin[s], rmin);
+              }
             }
+            act[u] = act[u] && !mine;
           }
-          act = act && !mine;
         }
-        if (act) {
-          const uint32_t s = tab_insert(tkey, v[u].x, empty, &nkeys);
+        if (act[u]) {
+          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x) : tab_insert(tkey, v[u].x, empty, &nkeys);
           if (s == kInvalid) {
             ovf = 1;
           } else {
@@ -176,6 +205,8 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
           }
         }
       }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
     }
     __syncthreads();
     if (ovf) {  // too many distinct keys for one round: retry the first half of the range
@@ -189,23 +220,26 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     }
     // ---- main slots: rank of every key inside its bucket (registers), bucket offsets ----
     // (empty slots: tkey = empty, tcnt = 0, tmin = kInvalid)
-    uint32_t rank[kAggCap / kAggBlock];
+    uint32_t rank[kAggSlotsPer];
 #pragma unroll
-    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) {
+    for (int j = 0; j < int(kAggSlotsPer); ++j) {
       const uint32_t s = j * kAggBlock + threadIdx.x;
-      rank[j] = tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
+      rank[j] = s < kAggCap && tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
     }
     __syncthreads();
     const uint32_t nk = block_scan_lds(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
     // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
-    uint32_t cnt[kAggCap / kAggBlock];
+    uint32_t cnt[kAggSlotsPer];
 #pragma unroll
-    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) cnt[j] = tcnt[j * kAggBlock + threadIdx.x];
+    for (int j = 0; j < int(kAggSlotsPer); ++j) {
+      const uint32_t s = j * kAggBlock + threadIdx.x;
+      cnt[j] = s < kAggCap ? tcnt[s] : 0u;
+    }
     __syncthreads();
     const uint32_t nrows = block_scan_lds(tcnt, kAggCap, wsum);
     // main records (partition-local slots, global sub offsets) and the round's directory words
 #pragma unroll
-    for (int j = 0; j < int(kAggCap / kAggBlock); ++j) {
+    for (int j = 0; j < int(kAggSlotsPer); ++j) {
       const uint32_t s = j * kAggBlock + threadIdx.x;
       if (cnt[j]) {
         const uint32_t h = tkey[s];
@@ -219,32 +253,41 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     for (uint32_t k = threadIdx.x; k < c1 - c0; k += kAggBlock) off[b0 + c0 + k] = mrun + bcnt[k];
     __syncthreads();
     // ---- pass B: rows into their keys' sub ranges ----
+    load_batch(pairs, e0, e1, v);
     for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
-      uint2 v[kAggU];
-#pragma unroll
-      for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
-        v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
-      }
+      if (i0 + kAggBlock * kAggU < e1) load_batch(pairs, i0 + kAggBlock * kAggU, e1, nv);  // next batch in flight
+      bool act[kAggU];
+      uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
         const uint32_t lb = fm.mod(v[u].x) - lo - b0;
-        bool act = i < e1 && lb >= c0 && lb < c1;
-        const uint64_t am = __ballot(act);
+        act[u] = i < e1 && lb >= c0 && lb < c1;
+        k0[u] = tkey[act[u] ? slot_of(v[u].x) : 0u];
+      }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) {
+        const uint64_t am = __ballot(act[u]);
         if (am) {
           const int leader = __ffsll((unsigned long long)am) - 1;
-          const uint32_t hl = uint32_t(__shfl(int(v[u].x), leader, kWave));
-          const bool mine = act && v[u].x == hl;
+          const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
+          const bool mine = act[u] && v[u].x == hl;
           const uint64_t same = __ballot(mine);
-          uint32_t base = 0;
-          if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl)], uint32_t(__popcll(same)));
-          base = uint32_t(__shfl(int(base), leader, kWave));
-          if (mine) sub[base + uint32_t(__popcll(same & lt))] = v[u].y;
-          act = act && !mine;
+          if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive sub slots
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl)], uint32_t(__popcll(same)));
+            base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+            if (mine) sub[base + uint32_t(__popcll(same & lt))] = v[u].y;
+            act[u] = act[u] && !mine;
+          }
         }
-        if (act) sub[atomicAdd(&tcnt[tab_find(tkey, v[u].x)], 1u)] = v[u].y;
+        if (act[u]) {
+          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x) : tab_find(tkey, v[u].x);
+          sub[atomicAdd(&tcnt[s], 1u)] = v[u].y;
+        }
       }
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
     }
     mrun += nk;
     srun += nrows;
@@ -254,6 +297,34 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
   if (threadIdx.x == 0) dcount[p] = mrun;
   const uint64_t wm = wave_max(uint64_t(mxlen));
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+}
+
+// order[i] = the partition with the i-th most pairs (bitonic sort of size << 11 | p in LDS, one
+// workgroup, P <= 2048): k_nagg takes its partitions largest first, so a Zipf hot key's
+// partition starts in the first wave of workgroups instead of extending the tail.
+__global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict__ ps, uint32_t P,
+                                                     uint32_t* __restrict__ order) {
+  __shared__ uint64_t a[2048];
+  for (uint32_t i = threadIdx.x; i < 2048; i += 1024)
+    a[i] = i < P ? (uint64_t(ps[i + 1] - ps[i]) << 11) | i : 0ull;  // padding sorts last
+  __syncthreads();
+  for (uint32_t k = 2; k <= 2048; k <<= 1) {
+    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+      for (uint32_t i = threadIdx.x; i < 2048; i += 1024) {
+        const uint32_t l = i ^ j;
+        if (l > i) {
+          const bool desc = (i & k) == 0;  // descending overall
+          const uint64_t x = a[i], y = a[l];
+          if (desc ? x < y : x > y) {
+            a[i] = y;
+            a[l] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (uint32_t i = threadIdx.x; i < P; i += 1024) order[i] = uint32_t(a[i] & 2047u);
 }
 
 // off[b] += first main of b's partition; main records moved to their final slots.
@@ -295,11 +366,12 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   // scratch: pairs (n uint2) | main records before compaction (n uint4) | starts, key counts
   if ((e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrPStart].ensure((2 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPStart].ensure((3 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   uint32_t* dcount = ps + P + 2;  // P + 1 (scanned in place into the main bases)
+  uint32_t* order = dcount + P + 1;
   uint32_t np = 0;
   if ((e = radix_partition_pairs(ctx, t, r, kAggW, pairs, ps, &np, s)) != hipSuccess) return e;
   if (np != P) return hipErrorNotSupported;
@@ -307,9 +379,10 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   uint32_t* off = t->off.as<uint32_t>();
   if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
   uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
+  hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
   hipLaunchKernelGGL(k_nagg, dim3(P), dim3(kAggBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
                      uint32_t(t->desc.num_buckets), off, mtmp, t->sub.as<uint32_t>(), dcount,
-                     reinterpret_cast<unsigned long long*>(counts + 2), fail);
+                     reinterpret_cast<unsigned long long*>(counts + 2), fail, order);
   uint32_t hfail = 0;
   if ((e = hipMemcpyAsync(&hfail, fail, sizeof(hfail), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
   if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
