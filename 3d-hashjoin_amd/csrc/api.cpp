@@ -390,6 +390,20 @@ hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t
   return from_hip(ctx, bitmap_or_popcount(ctx, bitmaps, rows, words, count, ctx->stream), "hj3d_bitmap_or_popcount");
 }
 
+hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
+                        void* count) {
+  if (!ctx) return HJ3D_EINVAL;
+  if (!rel_ok(rel) || !count || (rel->n && !out) || npred > HJ3D_SEL_MAX || (npred && !preds))
+    return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid argument");
+  if (rel->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_select: more than 2^32-1 tuples");
+  for (uint32_t k = 0; k < npred; ++k) {
+    const hj3d_sel_pred& p = preds[k];
+    if ((p.word_off & 3) || p.word_off + 4 > rel->stride || p.op > HJ3D_SEL_RANGE)
+      return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid predicate");
+  }
+  return from_hip(ctx, select_pairs(ctx, *rel, preds, npred, out, count, ctx->stream), "hj3d_select");
+}
+
 hj3d_status hj3d_gen_keys(hj3d_ctx* ctx, void* tuples, uint64_t n, uint32_t stride, uint32_t key_off,
                           uint64_t row_base, uint64_t n_keys, uint64_t seed) {
   if (!ctx || (n && !tuples) || stride == 0 || (stride & 3) || (key_off & 3) || key_off + 4 > stride)

@@ -154,6 +154,8 @@ hipError_t table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out, hipS
 // part.hip
 hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t nparts, void* out_pairs,
                      void* counts, hipStream_t s);
+hipError_t select_pairs(hj3d_ctx* ctx, const hj3d_rel& rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
+                        void* count, hipStream_t s);
 hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s);
 hipError_t bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t rows, uint64_t words, void* count,
                               hipStream_t s);

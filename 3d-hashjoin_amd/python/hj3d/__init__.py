@@ -26,6 +26,9 @@ HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT = 1, 2, 3, 4
+SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
+SEL_MAX = 4
+SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
 
 MASK64 = (1 << 64) - 1
 
@@ -55,6 +58,11 @@ class _Probe2Res(C.Structure):
     _fields_ = [(f, C.c_uint64) for f in ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp",
                                           "c_unnest_1", "c_unnest_2", "c_top", "sum_a", "sum_b", "sum_c", "sum_h",
                                           "xor_h")]
+
+
+class _SelPred(C.Structure):
+    _fields_ = [("word_off", C.c_uint32), ("op", C.c_uint32), ("is_signed", C.c_uint32), ("reserved", C.c_uint32),
+                ("lo", C.c_int64), ("hi", C.c_int64)]
 
 
 class _Stats(C.Structure):
@@ -107,6 +115,7 @@ def lib():
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
         "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
+        "hj3d_select": (st, [p, R, C.POINTER(_SelPred), u32, p, p]),
         "hj3d_gen_keys": (st, [p, p, u64, u32, u32, u64, u64, u64]),
         "hj3d_gen_fk": (st, [p, p, u64, u32, u32, u64, u32, u64]),
         "hj3d_gen_zipf": (st, [p, p, u64, u32, u32, u64, u32, C.c_double, u64]),
@@ -274,6 +283,36 @@ class Context:
         r = _Probe2Res()
         self._check(lib().hj3d_probe2_result(self.h, C.byref(r)), "hj3d_probe2_result")
         return {f: getattr(r, f) for f, _ in _Probe2Res._fields_}
+
+    # ---- selection pushdown (AlgSelection / AlgDynSelection, algebra.hh:278-358) ----
+    def select(self, rel: Rel, preds, out_pairs=None, count=None, fetch: bool = True):
+        """Tuples of `rel` whose conjunction of predicates holds, as a stable (key, row) pair
+        relation. preds: [(word, op, lo[, hi][, signed])], op in SEL_OPS ("<", "<=", ">", ">=",
+        "==", "!=", "range": lo <= v < hi); compared as int32 (the reference's attrval_t) unless
+        signed=False. Returns (pairs tensor (n, 2) int32, Rel over it keyed on word 0 with row
+        word 1, count); with fetch=False the count stays on the device (count tensor) and the
+        Rel covers the capacity (rel.n) until the caller trims it."""
+        torch = _torch()
+        if len(preds) > SEL_MAX:
+            raise ValueError(f"at most {SEL_MAX} predicates")
+        arr = (_SelPred * max(1, len(preds)))()
+        for k, pr in enumerate(preds):
+            word, op, lo = pr[0], pr[1], pr[2]
+            hi = pr[3] if len(pr) > 3 and pr[3] is not None else 0
+            signed = pr[4] if len(pr) > 4 else True
+            arr[k] = _SelPred(4 * word, SEL_OPS.get(op, op), int(bool(signed)), 0, int(lo), int(hi))
+        dev = f"cuda:{self.device}"
+        if out_pairs is None:
+            out_pairs = torch.empty((max(rel.n, 1), 2), dtype=torch.int32, device=dev)
+        if count is None:
+            count = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._check(lib().hj3d_select(self.h, C.byref(rel.c), arr, len(preds), out_pairs.data_ptr(),
+                                      count.data_ptr()), "hj3d_select")
+        if not fetch:
+            return out_pairs, Rel(out_pairs, 0, 1, n=rel.n), count
+        self.sync()
+        n = int(count.item())
+        return out_pairs, Rel(out_pairs, 0, 1, n=n), n
 
     # ---- exchange / synthetic data ----
     def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts):

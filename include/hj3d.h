@@ -19,6 +19,7 @@
  *                                                                     ht_nested.hh:450-482
  *   hj3d_table_clear           HtChaining1/HtNested1::clear           ht_chaining.hh:250-258,
  *                                                                     ht_nested.hh:438-447
+ *   hj3d_select                AlgSelection / AlgDynSelection::step   algebra.hh:278-358
  *
  * Semantics kept bit-exact with the reference: hash = murmur3 fmix32 (util/hasht.hh:52-61),
  * bucket = hash % num_buckets, and every counter the reference reports (match counts,
@@ -223,6 +224,26 @@ hj3d_status hj3d_key_bitmap(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t domain,
  * back to back at bitmaps_dev. */
 hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps_dev, uint32_t rows, uint64_t words,
                                     void* count_dev);
+
+/* ---- selection pushdown: AlgSelection / AlgDynSelection (algebra.hh:278-358) on the device ----
+ * The predicate is a conjunction of `npred` (<= HJ3D_SEL_MAX) comparisons of one u32 tuple word
+ * (byte offset word_off, compared as int32 when is_signed, else as uint32) against lo (and hi for
+ * HJ3D_SEL_RANGE: lo <= v < hi). The passing tuples of `rel` are written, in scan order, to
+ * out_pairs_dev as {u32 key, u32 row} (row = the tuple's row id in rel, capacity rel->n pairs);
+ * count_dev (device u64) receives their number. The pairs are a relation {out, n, stride 8,
+ * key_off 0, row_off 4} that hj3d_build / hj3d_probe take as the selection's consumer would:
+ * same order, same row identities. Asynchronous. */
+#define HJ3D_SEL_MAX 4
+enum { HJ3D_SEL_LT = 0, HJ3D_SEL_LE, HJ3D_SEL_GT, HJ3D_SEL_GE, HJ3D_SEL_EQ, HJ3D_SEL_NE, HJ3D_SEL_RANGE };
+typedef struct {
+  uint32_t word_off;  /* byte offset of the compared u32 word, multiple of 4, < stride */
+  uint32_t op;        /* HJ3D_SEL_*                                                    */
+  uint32_t is_signed; /* compare as int32 (the reference's attrval_t is int)           */
+  uint32_t reserved;
+  int64_t lo, hi;
+} hj3d_sel_pred;
+hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
+                        void* out_pairs_dev, void* count_dev);
 
 /* ---- synthetic key/FK relations generated on the device (bench / full-size checks) ----
  * R.k = a seeded bijective permutation of [0, n_keys) (keys for global rows

@@ -202,3 +202,28 @@ def exp4_plan(R, S, T, nb, nested, agg=True, min_ms=0.0, min_reps=1) -> dict:
     d = {f: getattr(res, f) for f, _ in _Exp4Res._fields_ if f != "out"}
     d["out"] = _agg(res.out)
     return d
+
+
+_SEL_CMP = {
+    "<": lambda v, lo, hi: v < lo, "<=": lambda v, lo, hi: v <= lo, ">": lambda v, lo, hi: v > lo,
+    ">=": lambda v, lo, hi: v >= lo, "==": lambda v, lo, hi: v == lo, "!=": lambda v, lo, hi: v != lo,
+    "range": lambda v, lo, hi: (v >= lo) & (v < hi),
+}
+
+
+def select(rel: np.ndarray, key: int, preds) -> np.ndarray:
+    """AlgSelection::step / AlgDynSelection::step (algebra.hh:295-300, 335-340): a tuple goes to
+    the consumer iff the predicate holds, in scan order. The predicate is the conjunction of
+    preds = [(word, op, lo[, hi][, signed])] over u32 tuple words (compared as int32, the
+    reference's attrval_t, unless signed=False). Returns the forwarded tuples as (key, row) pairs,
+    row = index in `rel` (the tuple's identity: the reference forwards the same tuple pointer)."""
+    rel = np.ascontiguousarray(rel, dtype=np.uint32)
+    ok = np.ones(rel.shape[0], dtype=bool)
+    for pr in preds:
+        word, op, lo = pr[0], pr[1], pr[2]
+        hi = pr[3] if len(pr) > 3 and pr[3] is not None else 0
+        signed = pr[4] if len(pr) > 4 else True
+        v = rel[:, word].view(np.int32).astype(np.int64) if signed else rel[:, word].astype(np.int64)
+        ok &= _SEL_CMP[op](v, lo, hi)
+    rows = np.nonzero(ok)[0].astype(np.uint32)
+    return np.stack([rel[rows, key], rows], axis=1).astype(np.uint32) if rows.size else np.zeros((0, 2), np.uint32)
