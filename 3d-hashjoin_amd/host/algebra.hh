@@ -26,6 +26,7 @@
 #include <concepts>
 #include <cstdint>
 #include <functional>
+#include <iomanip>
 #include <iostream>
 #include <sstream>
 #include <string>
@@ -233,6 +234,13 @@ class AlgScan : public AlgBase {
   input_rel_t* _relation;
 };
 
+// Selection pushdown applies when the predicate has a device form (hj3d::device_predicate) and the
+// consumer is a device probe operator that takes a selected relation.
+template <typename Tpred, typename Tconsumer, typename Tinput, typename Tglobstat>
+inline constexpr bool hj3d_pushdown_v =
+    requires { hj3d::device_predicate<Tpred>::npred; } &&
+    requires(Tconsumer c, Tinput* b, Tglobstat* g) { c.consume_selected(b, size_t(0), nullptr, 0u, g); };
+
 // Selection operator (reference algebra.hh:278-315): host predicate, tuple at a time
 template <alg_consumer_c Tconsumer, alg_predicate_c Tpredicate>
 class AlgSelection : public AlgBase {
@@ -246,7 +254,17 @@ class AlgSelection : public AlgBase {
   inline AlgSelection(Tconsumer* aConsumer) : AlgBase("AlgSelection"), _consumer(aConsumer) {}
   inline void init(globstat_t* g) {
     reset();
+    _pushed = false;
     _consumer->init(g);
+  }
+  // Pushdown (hj3d::device_predicate<Tpredicate> specialised and a device probe consumer): the
+  // whole relation goes to the consumer with the predicate, hj3d_select filters it on the device.
+  inline void consume_relation(input_t* base, size_t n, globstat_t* g)
+    requires(hj3d_pushdown_v<Tpredicate, Tconsumer, input_t, globstat_t>)
+  {
+    using P = hj3d::device_predicate<Tpredicate>;
+    _pushed = true;
+    _consumer->consume_selected(base, n, P::preds, P::npred, g);
   }
   inline void step(input_t* aInput, globstat_t* g) {
     if (predicate_t::eval(aInput)) {
@@ -256,12 +274,15 @@ class AlgSelection : public AlgBase {
   }
   inline void fin(globstat_t* g) {
     _consumer->fin(g);
+    if constexpr (hj3d_pushdown_v<Tpredicate, Tconsumer, input_t, globstat_t>)
+      if (_pushed) _count += _consumer->selected_count();
     stopTimer();
   }
   inline const consumer_t* consumer() const { return _consumer; }
 
  private:
   consumer_t* _consumer;
+  bool _pushed = false;
 };
 
 // Dynamic selection operator (reference algebra.hh:318-358)
@@ -279,7 +300,15 @@ class AlgDynSelection : public AlgBase {
   inline AlgDynSelection(consumer_t* aConsumer) : AlgDynSelection(aConsumer, predicate_t()) {}
   inline void init(globstat_t* g) {
     reset();
+    _pushed = false;
     _consumer->init(g);
+  }
+  inline void consume_relation(input_t* base, size_t n, globstat_t* g)
+    requires(hj3d_pushdown_v<Tpredicate, Tconsumer, input_t, globstat_t>)
+  {
+    using P = hj3d::device_predicate<Tpredicate>;
+    _pushed = true;
+    _consumer->consume_selected(base, n, P::preds, P::npred, g);
   }
   inline void step(input_t* aInput, globstat_t* g) {
     if (_pred(aInput)) {
@@ -289,6 +318,8 @@ class AlgDynSelection : public AlgBase {
   }
   inline void fin(globstat_t* g) {
     _consumer->fin(g);
+    if constexpr (hj3d_pushdown_v<Tpredicate, Tconsumer, input_t, globstat_t>)
+      if (_pushed) _count += _consumer->selected_count();
     stopTimer();
   }
   inline const consumer_t* consumer() const { return _consumer; }
@@ -296,6 +327,7 @@ class AlgDynSelection : public AlgBase {
  private:
   consumer_t* _consumer;
   predicate_t _pred;
+  bool _pushed = false;
 };
 
 // ---- build operators ----
@@ -469,6 +501,16 @@ class AlgNestJoinProbe : public AlgBase {
     _in.base = base;
     _in.n = n;
   }
+  // the scanned relation behind a pushed-down selection (AlgSelection with hj3d::device_predicate)
+  inline void consume_selected(input_t* base, size_t n, const hj3d_sel_pred* preds, uint32_t npred,
+                               [[maybe_unused]] globstat_t* g) {
+    _in.base = base;
+    _in.n = n;
+    _in.preds = preds;
+    _in.npred = npred;
+    _in.selecting = true;
+  }
+  inline uint64_t selected_count() const { return _dev.rel.n; }
   inline void fin(globstat_t* g) {
     if (!_absorbed) execute();
     _consumer->fin(g);
@@ -641,6 +683,16 @@ class AlgHashJoinProbe : public AlgBase {
     _in.base = base;
     _in.n = n;
   }
+  // the scanned relation behind a pushed-down selection (AlgSelection with hj3d::device_predicate)
+  inline void consume_selected(input_t* base, size_t n, const hj3d_sel_pred* preds, uint32_t npred,
+                               [[maybe_unused]] globstat_t* g) {
+    _in.base = base;
+    _in.n = n;
+    _in.preds = preds;
+    _in.npred = npred;
+    _in.selecting = true;
+  }
+  inline uint64_t selected_count() const { return _dev.rel.n; }
   inline void fin(globstat_t* g) {
     if (!_absorbed) execute(g);
     _consumer->fin(g);
@@ -696,7 +748,7 @@ class AlgHashJoinProbe : public AlgBase {
   void emit_and_push(hj3d_table* t, Tdt& dt, globstat_t* g) {
     using namespace hj3d::host;
     Engine& e = Engine::get();
-    const uint64_t n = _in.size();
+    const uint64_t n = _dev.rel.n;  // probe tuples (the passing ones under a device selection)
     uint64_t cap = n;
     if (!IsBuildKeyUnique) cap = run_probe(t, _dev.rel, kFlags).n_out;
     DevBuffer buf;

@@ -26,6 +26,20 @@
 
 #include "hj3d.h"
 
+namespace hj3d {
+// Opt-in selection pushdown. Specialise for a selection predicate (AlgSelection's Tpredicate or
+// AlgDynSelection's functor type) with the same condition as hj3d_sel_pred terms, e.g. for
+// `L.b < 40` on tuple {int a, b}:
+//   template <> struct hj3d::device_predicate<SelectionL> {
+//     static constexpr uint32_t npred = 1;
+//     static constexpr hj3d_sel_pred preds[1] = {{4, HJ3D_SEL_LT, 1, 0, 40, 0}};
+//   };
+// Then a scanned relation flowing AlgScan -> AlgSelection -> a join probe operator is filtered by
+// hj3d_select on the device; without it the selection runs on the host, tuple at a time.
+template <typename Tpredicate>
+struct device_predicate;
+}  // namespace hj3d
+
 namespace hj3d::host {
 
 struct Error : std::runtime_error {
@@ -218,17 +232,25 @@ inline void check_joinpred(const Tprobe* p, uint32_t pk, const Tbuild* b, uint32
 
 // The input of one GPU operator: either a contiguous batch (the scanned relation) or the tuple
 // pointers pushed through step().
+// A batch may carry a device selection (AlgSelection pushed down, hj3d::device_predicate):
+// then only its passing tuples are the operator's input, still addressed by their row in the batch.
 template <typename T>
 struct Input {
   T* base = nullptr;
   uint64_t n = 0;
   std::vector<T*> ptrs;
+  const hj3d_sel_pred* preds = nullptr;
+  uint32_t npred = 0;
+  bool selecting = false;
   uint64_t size() const { return base ? n : ptrs.size(); }
   T* at(uint64_t row) const { return base ? base + row : ptrs[row]; }
   void clear() {
     base = nullptr;
     n = 0;
     ptrs.clear();
+    preds = nullptr;
+    npred = 0;
+    selecting = false;
   }
 };
 
@@ -254,8 +276,12 @@ struct DevInput {
       rel.base = RelationCache::get().upload(in.base, in.n, sizeof(T));
       rel.stride = sizeof(T);
       rel.key_off = 4 * *key_word;
+      if (in.selecting) select(in);
       return;
     }
+    if (in.selecting)
+      throw Error(std::string("hj3d: ") + op + ": a device selection needs the join key to be one u32 word of "
+                  "the tuple");
     std::vector<uint32_t> k(rel.n);
     for (uint64_t i = 0; i < rel.n; ++i) {
       const uint64_t h = uint64_t(Thashfun::eval(in.at(i)));
@@ -270,6 +296,19 @@ struct DevInput {
     rel.stride = 4;
     rel.key_off = 0;
   }
+
+  // AlgSelection on the device (hj3d_select): rel becomes the passing tuples' (key, row) pairs,
+  // rows still index the batch.
+  void select(const Input<T>& in) {
+    Engine& e = Engine::get();
+    void* d = sel.ensure(rel.n * 8 + 16);
+    uint64_t* cnt = reinterpret_cast<uint64_t*>(static_cast<char*>(d) + rel.n * 8 + 8);
+    e.check(hj3d_select(e.ctx(), &rel, in.preds, in.npred, d, cnt), "hj3d_select");
+    uint64_t n_sel = 0;
+    e.check(hj3d_download(e.ctx(), &n_sel, cnt, 8), "hj3d_download (selection count)");
+    rel = hj3d_rel{d, n_sel, 8, 0, 4, 0, 0};
+  }
+  DevBuffer sel;
 };
 
 // The device table behind HtChaining1 / HtNested1. Inserted tuples are kept as segments (the

@@ -168,3 +168,38 @@ def test_gpu_selection_then_join_seeded(ctx):
     for k in ("sum_a", "sum_b", "sum_h", "xor_h"):
         assert getattr(res, k) == exp.out[k], k
     tab.close()
+
+
+BIN = os.path.join(os.path.dirname(HERE), "3d-hashjoin_amd", "bin", "dropin_selection")
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(BIN), reason="drop-in selection program not built (make -C 3d-hashjoin_amd)")
+def test_gpu_dropin_selection_pushdown_matches_reference_example():
+    """tests/cpp/dropin_selection.cc: the example's plans through the drop-in operators, selection
+    on the host and pushed down to hj3d_select; every operator count equals the reference's and
+    the printed chaining output equals the reference's output, in the reference's order."""
+    import re
+    import subprocess
+    r = subprocess.run([BIN], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    got = {}
+    for ln in lines:
+        m = re.match(r"(\w+) (\w+) (.*)", ln)
+        if m and "=" in m.group(3):
+            got[(m.group(1), m.group(2))] = dict(kv.split("=") for kv in m.group(3).split())
+    exp = {"chain": EX["algebra_test3"]["counts"], "nested": EX["algebra_test1"]["counts"],
+           "unnest": EX["algebra_test2"]["counts"]}
+    modes = {"chain": ("host", "device", "device_dyn", "device_print"), "nested": ("host", "device"),
+             "unnest": ("host", "device")}
+    for plan, ms in modes.items():
+        for mode in ms:
+            g, c = got[(plan, mode)], exp[plan]
+            assert int(g["Top"]) == c["probe_Top"], (plan, mode)
+            assert int(g["Probe"]) == c["probe_Probe"], (plan, mode)
+            assert int(g["Sel"]) == c["probe_Sel"], (plan, mode)
+            assert int(g["Scan"]) == c["probe_Scan"], (plan, mode)
+            assert int(g["Build"]) == c["build_Build"], (plan, mode)
+    printed = [[int(v) for v in ln.strip("()").split(",")] for ln in lines if ln.startswith("(")]
+    assert printed == EX["algebra_test3"]["output"]
