@@ -113,6 +113,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_RADIX_MIN: ctx->radix_min = value < 0 ? 0 : uint64_t(value); return HJ3D_OK;
     case HJ3D_OPT_NESTED_RADIX: ctx->nested_radix = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_SORT: ctx->nested_sort = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_SEL_UNFUSED: ctx->sel_unfused = value != 0; return HJ3D_OK;
     default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
   }
 }
@@ -281,6 +282,26 @@ hj3d_status hj3d_table_size(hj3d_ctx* ctx, const hj3d_table* t, uint64_t* n_entr
   return HJ3D_OK;
 }
 
+// remember what an overflow check needs (hj3d_probe_result)
+static void note_probe(hj3d_ctx* ctx, const hj3d_table* t, uint64_t n, uint32_t flags, uint64_t out_cap) {
+  const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
+  ctx->res_flags = flags;
+  ctx->res_dense = (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
+  ctx->res_cap = (flags & HJ3D_PROBE_EMIT) ? out_cap : ~0ull;
+  ctx->res_nprobe = acc ? ctx->res_nprobe + n : n;
+  // dense output: each call needs one slot per probe tuple of its own buffer
+  const bool ovf_dense = ctx->res_dense && (flags & HJ3D_PROBE_EMIT) && n > out_cap;
+  ctx->res_overflow = (acc && ctx->res_overflow) || ovf_dense;
+  ctx->res_accumulated = acc;
+}
+
+static bool sel_ok(const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred) {
+  if (npred > HJ3D_SEL_MAX || (npred && !preds)) return false;
+  for (uint32_t k = 0; k < npred; ++k)
+    if ((preds[k].word_off & 3) || preds[k].word_off + 4 > rel->stride || preds[k].op > HJ3D_SEL_RANGE) return false;
+  return true;
+}
+
 hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe, uint32_t flags, void* out_dev,
                        uint64_t out_cap) {
   if (!ctx || !t) return HJ3D_EINVAL;
@@ -304,16 +325,43 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
                                        : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
     }
   }
-  // remember what an overflow check needs
-  ctx->res_flags = flags;
-  ctx->res_dense = (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
-  ctx->res_cap = (flags & HJ3D_PROBE_EMIT) ? out_cap : ~0ull;
-  ctx->res_nprobe = acc ? ctx->res_nprobe + probe->n : probe->n;
-  // dense output: each call needs one slot per probe tuple of its own buffer
-  const bool ovf_dense = ctx->res_dense && (flags & HJ3D_PROBE_EMIT) && probe->n > out_cap;
-  ctx->res_overflow = (acc && ctx->res_overflow) || ovf_dense;
-  ctx->res_accumulated = acc;
+  note_probe(ctx, t, probe->n, flags, out_cap);
   return from_hip(ctx, e, "hj3d_probe");
+}
+
+hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe, const hj3d_sel_pred* preds,
+                           uint32_t npred, uint32_t flags, void* out_dev, uint64_t out_cap) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  if (npred == 0) return hj3d_probe(ctx, t, probe, flags, out_dev, out_cap);
+  if (!rel_ok(probe)) return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: invalid relation");
+  if (!sel_ok(probe, preds, npred)) return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: invalid predicate");
+  if ((flags & HJ3D_PROBE_EMIT) && !out_dev && out_cap) return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: EMIT without buffer");
+  if ((flags & HJ3D_PROBE_UNNEST) && t->desc.kind != HJ3D_NESTED)
+    return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: UNNEST needs a nested table");
+  if (t->desc.kind == HJ3D_CHAIN && !(flags & HJ3D_PROBE_ACCUMULATE) && !ctx->sel_unfused &&
+      radix_probe_applicable(ctx, t, probe->n)) {
+    // the selection fused into the probe-side partitioner
+    PhaseTimer tm(ctx, HJ3D_T_PROBE);
+    uint64_t* res = ctx->res.as<uint64_t>();
+    hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+    const SelArgs a = sel_args(preds, npred);
+    if (e == hipSuccess) e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a);
+    if (e != hipErrorNotSupported) {
+      note_probe(ctx, t, probe->n, flags, out_cap);
+      return from_hip(ctx, e, "hj3d_probe_sel");
+    }
+  }
+  // select first (stable (key, row) pairs), then probe the passing tuples
+  hipError_t e = ctx->sel.ensure(probe->n * sizeof(uint2) + 16);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe_sel");
+  uint64_t* cnt = reinterpret_cast<uint64_t*>(ctx->sel.as<char>() + probe->n * sizeof(uint2) + 8);
+  e = select_pairs(ctx, *probe, preds, npred, ctx->sel.p, cnt, ctx->stream);
+  uint64_t n_sel = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&n_sel, cnt, sizeof(n_sel), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe_sel");
+  const hj3d_rel pairs{ctx->sel.p, n_sel, 8, 0, 4, 0, 0};
+  return hj3d_probe(ctx, t, &pairs, flags, out_dev, out_cap);
 }
 
 hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out) {
@@ -393,14 +441,9 @@ hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps, uint32_t
 hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
                         void* count) {
   if (!ctx) return HJ3D_EINVAL;
-  if (!rel_ok(rel) || !count || (rel->n && !out) || npred > HJ3D_SEL_MAX || (npred && !preds))
-    return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid argument");
+  if (!rel_ok(rel) || !count || (rel->n && !out)) return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid argument");
+  if (!sel_ok(rel, preds, npred)) return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid predicate");
   if (rel->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_select: more than 2^32-1 tuples");
-  for (uint32_t k = 0; k < npred; ++k) {
-    const hj3d_sel_pred& p = preds[k];
-    if ((p.word_off & 3) || p.word_off + 4 > rel->stride || p.op > HJ3D_SEL_RANGE)
-      return fail(ctx, HJ3D_EINVAL, "hj3d_select: invalid predicate");
-  }
   return from_hip(ctx, select_pairs(ctx, *rel, preds, npred, out, count, ctx->stream), "hj3d_select");
 }
 

@@ -68,6 +68,8 @@ struct hj3d_ctx {
   uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
   bool nested_radix = false;      // HJ3D_OPT_NESTED_RADIX
   bool nested_sort = false;       // HJ3D_OPT_NESTED_SORT
+  bool sel_unfused = false;       // HJ3D_OPT_SEL_UNFUSED
+  hj3d::DevBuf sel;               // hj3d_probe_sel: passing (key, row) pairs when not fused
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;
@@ -90,6 +92,66 @@ struct hj3d_table {
 
 namespace hj3d {
 
+// Selection predicate (hj3d_sel_pred conjunction) as a kernel argument, and its evaluation on the
+// u32 tuple word(s) it reads (AlgSelection::step, algebra.hh:295-300).
+struct SelArgs {
+  uint32_t npred = 0;
+  hj3d_sel_pred p[HJ3D_SEL_MAX];
+};
+__device__ __forceinline__ bool sel_one(const hj3d_sel_pred& p, uint32_t w) {
+  const int64_t v = p.is_signed ? int64_t(int32_t(w)) : int64_t(w);
+  switch (p.op) {
+    case HJ3D_SEL_LT: return v < p.lo;
+    case HJ3D_SEL_LE: return v <= p.lo;
+    case HJ3D_SEL_GT: return v > p.lo;
+    case HJ3D_SEL_GE: return v >= p.lo;
+    case HJ3D_SEL_EQ: return v == p.lo;
+    case HJ3D_SEL_NE: return v != p.lo;
+    default: return v >= p.lo && v < p.hi;  // HJ3D_SEL_RANGE
+  }
+}
+__device__ __forceinline__ bool sel_eval(const RelView& r, const SelArgs& a, uint64_t i) {
+  const char* t = r.base + i * r.stride;
+  bool ok = true;
+  for (uint32_t k = 0; k < a.npred; ++k)
+    ok = ok && sel_one(a.p[k], *reinterpret_cast<const uint32_t*>(t + a.p[k].word_off));
+  return ok;
+}
+// One predicate as an inclusive range test on the word read as int32 / uint32 (inverted for !=):
+// the form the probe partitioner evaluates in its hot loop.
+struct SelRange {
+  uint32_t word_off = 0, is_signed = 0, invert = 0, pad = 0;
+  int64_t lo = 0, hi = -1;
+  __device__ __forceinline__ bool test(uint32_t w) const {
+    const int64_t v = is_signed ? int64_t(int32_t(w)) : int64_t(w);
+    return (v >= lo && v <= hi) != (invert != 0);
+  }
+  static bool from(const SelArgs& a, SelRange* r) {
+    if (a.npred != 1) return false;
+    const hj3d_sel_pred& p = a.p[0];
+    const int64_t mn = p.is_signed ? INT32_MIN : 0, mx = p.is_signed ? INT32_MAX : int64_t(UINT32_MAX);
+    r->word_off = p.word_off;
+    r->is_signed = p.is_signed != 0;
+    r->invert = 0;
+    switch (p.op) {
+      case HJ3D_SEL_LT: r->lo = mn; r->hi = p.lo - 1; break;
+      case HJ3D_SEL_LE: r->lo = mn; r->hi = p.lo; break;
+      case HJ3D_SEL_GT: r->lo = p.lo + 1; r->hi = mx; break;
+      case HJ3D_SEL_GE: r->lo = p.lo; r->hi = mx; break;
+      case HJ3D_SEL_EQ: r->lo = p.lo; r->hi = p.lo; break;
+      case HJ3D_SEL_NE: r->lo = p.lo; r->hi = p.lo; r->invert = 1; break;
+      default: r->lo = p.lo; r->hi = p.hi - 1; break;  // RANGE
+    }
+    return true;
+  }
+};
+inline SelArgs sel_args(const hj3d_sel_pred* preds, uint32_t npred) {
+  SelArgs a{};
+  a.npred = npred;
+  for (uint32_t k = 0; k < npred; ++k) a.p[k] = preds[k];
+  return a;
+}
+
 // ---- launchers (defined in the .hip translation units); all asynchronous on `s` ----
 // scan.hip: exclusive prefix sum of n values into out[0..n], out[n] = total. in may alias out.
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
@@ -110,8 +172,11 @@ hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
                                  uint32_t* ps, uint32_t* nparts, hipStream_t s);
 // after every chaining build: buckets of <= 32 entries sorted by row (single-pass probe order)
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
+// sel (nullable, <= 2 predicates): the selection fused into the probe-side partitioner; tuples
+// failing it are dropped there and res[0] (n_probe) = the passing tuples. hipErrorNotSupported
+// when the fused form does not apply (the caller then selects first).
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                       uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+                       uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr);
 // The probe side partitioned by bucket range for a table slice of W buckets per partition
 // (k_rp_part1 + output-slot scan; layout in radix_seg.hpp). Output slots: regions first
 // (seg[P * G] of them), then the overflow list (*novf pairs). Uses scratch kScrPairs,
@@ -126,7 +191,7 @@ struct ProbeParts {
   const unsigned long long* novf = nullptr;
 };
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
-                                 hipStream_t s);
+                                 hipStream_t s, const SelArgs* sel = nullptr, unsigned long long** npass = nullptr);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,

@@ -646,11 +646,15 @@ __device__ __forceinline__ void ovf_append(bool spill_me, uint2 e, uint2* __rest
 // lanes per segment, so one wave-instruction stores 64 / SEG complete segments; the stage itself
 // needs no alignment (runs are packed). One partition per thread: P <= BLOCK. The carries are
 // flushed at the end. A tile whose runs plus carries exceed the stage first flushes the carries.
-template <int BLOCK, int ROUNDS, int SEG, bool IMPLICIT>
+// SEL: a one-word selection (AlgSelection in front of the probe) fused in, as an inclusive range
+// test on the word (SelRange): tuples failing it are dropped like tuples of unowned buckets;
+// npass += the passing tuples.
+template <int BLOCK, int ROUNDS, int SEG, bool IMPLICIT, bool SEL = false>
 __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                      uint32_t P, uint32_t ntiles, uint32_t cap,
                                                      uint2* __restrict__ region, uint32_t* __restrict__ counts,
-                                                     uint2* __restrict__ ovf, unsigned long long* __restrict__ novf) {
+                                                     uint2* __restrict__ ovf, unsigned long long* __restrict__ novf,
+                                                     SelRange sel = SelRange{}, unsigned long long* __restrict__ npass = nullptr) {
   constexpr int TILE = BLOCK * ROUNDS;
   constexpr int TBITS = __builtin_ctz(TILE);
   constexpr uint32_t kSeg = SEG;
@@ -672,10 +676,16 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
 #pragma unroll
   for (int j = 0; j < int(kSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
   uint32_t h[ROUNDS];
+  uint32_t pw[SEL ? ROUNDS : 1];  // the predicate word of the tile in flight
+  uint32_t npassed = 0;
+  auto load_pw = [&](int j, uint64_t i) {
+    if constexpr (SEL) pw[j] = i < r.n ? *reinterpret_cast<const uint32_t*>(r.base + i * r.stride + sel.word_off) : 0u;
+  };
 #pragma unroll
   for (int j = 0; j < ROUNDS; ++j) {
     const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
+    load_pw(j, i);
   }
   auto flush_carry = [&]() {  // thread me writes its carry at its cursor (a partial segment)
 #pragma unroll
@@ -698,7 +708,12 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       const uint64_t i = base + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = murmur32(h[j]);
       const uint32_t bl = fm.mod(h[j]) - lo;
-      if (i < r.n && bl < nbl) {
+      bool pass = true;
+      if constexpr (SEL) {
+        pass = sel.test(pw[j]);
+        npassed += (i < r.n && pass);
+      }
+      if (i < r.n && bl < nbl && pass) {
         const uint32_t part = fw.div(bl);
         rk[j] = (part << TBITS) | atomicAdd(&loc[part], 1u);
       } else {
@@ -763,6 +778,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
     for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = i < r.n ? r.key(i) : 0u;
+      load_pw(j, i);
     }
     __syncthreads();
     // the whole segments: stage index k of run p -> region offset k + pinfo[p].x (each run's
@@ -796,6 +812,12 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
   }
   flush_carry();
   if (me < P) counts[gbase + me] = min(my_cur, cap);
+  if constexpr (SEL) {
+    uint32_t c = npassed;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+    if (lane == 0 && c) atomicAdd(npass, (unsigned long long)c);
+  }
 }
 
 // cnt_pm[p * G + g] = counts[g * P + p]: partition-major order for the output-slot scan.
@@ -1047,7 +1069,7 @@ void launch_seg_any(const SegLaunch& L, bool unique, bool ck, uint2* out, uint64
 }  // namespace
 
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
-                                 hipStream_t s) {
+                                 hipStream_t s, const SelArgs* sel, unsigned long long** npass) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;
   if (W < 64) W = 64;
@@ -1059,6 +1081,8 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   if (P > kMaxParts) return hipErrorNotSupported;
   // up to one partition per thread: the whole-segment partitioner and its 8192-tuple tiles
   const bool seg_writes = P <= uint32_t(kPBlock);
+  SelRange sr{};
+  if (sel && (!seg_writes || !SelRange::from(*sel, &sr))) return hipErrorNotSupported;  // fused: part1r, one word
   const uint32_t tile = seg_writes ? uint32_t(kPBlock * kPRoundsR) : uint32_t(kPTile);
   pl.ntiles = uint32_t((r.n + tile - 1) / tile);
   const uint32_t G = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
@@ -1076,13 +1100,21 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   uint32_t* seg = counts + nreg;  // nreg + 1 (transposed counts, scanned in place)
   unsigned long long* novf = ctx->scratch[kScrSortV].as<unsigned long long>();
   uint2* ovf = reinterpret_cast<uint2*>(ctx->scratch[kScrSortV].as<char>() + 64);
-  if ((e = hipMemsetAsync(novf, 0, sizeof(unsigned long long), s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(novf, 0, 2 * sizeof(unsigned long long), s)) != hipSuccess) return e;  // novf, npass
+  if (npass) *npass = novf + 1;
   const RelView v = view_of(r);
   {
     PhaseTimer tm(ctx, HJ3D_T_SCATTER);
     const uint32_t lo = uint32_t(t->desc.bucket_lo);
     const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
-    if (seg_writes) {
+    if (sel) {
+      if (imp)
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, kPSeg, true, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo,
+                           nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf, sr, novf + 1);
+      else
+        hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, kPSeg, false, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm,
+                           lo, nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf, sr, novf + 1);
+    } else if (seg_writes) {
       if (imp)
         hipLaunchKernelGGL((k_rp_part1r<kPBlock, kPRoundsR, kPSeg, true>), dim3(G), dim3(kPBlock), 0, s, v, t->fm, lo, nbl,
                            pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
@@ -1117,13 +1149,14 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
 }
 
 hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                       uint64_t out_cap, uint64_t* res, hipStream_t s) {
+                       uint64_t out_cap, uint64_t* res, hipStream_t s, const SelArgs* sel) {
   hipError_t e;
   // slice width: 80% of the LDS slice budget at the table's mean bucket fill
   const double fill = t->n_build ? double(t->n_build) / double(t->nb_local) : 0.0;
   ProbeParts pp;
-  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s)) !=
-      hipSuccess)
+  unsigned long long* npass = nullptr;
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s, sel,
+                                 sel ? &npass : nullptr)) != hipSuccess)
     return e;
   SegLaunch L;
   L.t = t;
@@ -1149,7 +1182,10 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
     return e;
   // n_probe of earlier accumulated probes (the reduction below sets res[0] = that + r.n)
   uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
-  if ((e = hipMemcpyAsync(base0, res, sizeof(uint64_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+  // (with a fused selection: n_probe = the passing tuples, counted by the partitioner)
+  if ((e = hipMemcpyAsync(base0, sel ? static_cast<void*>(npass) : static_cast<void*>(res), sizeof(uint64_t),
+                          hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return e;
   const bool unique = flags & HJ3D_PROBE_UNIQUE;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
@@ -1170,7 +1206,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
-  return reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n, base0);
+  return reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, sel ? 0ull : r.n, base0);
 }
 
 }  // namespace hj3d

@@ -20,32 +20,6 @@ namespace {
 constexpr int kSelItems = 16;                     // tuples per thread per tile
 constexpr uint32_t kSelTile = kBlock * kSelItems;  // 4096
 
-struct SelArgs {
-  uint32_t npred;
-  hj3d_sel_pred p[HJ3D_SEL_MAX];
-};
-
-__device__ __forceinline__ bool sel_one(const hj3d_sel_pred& p, uint32_t w) {
-  const int64_t v = p.is_signed ? int64_t(int32_t(w)) : int64_t(w);
-  switch (p.op) {
-    case HJ3D_SEL_LT: return v < p.lo;
-    case HJ3D_SEL_LE: return v <= p.lo;
-    case HJ3D_SEL_GT: return v > p.lo;
-    case HJ3D_SEL_GE: return v >= p.lo;
-    case HJ3D_SEL_EQ: return v == p.lo;
-    case HJ3D_SEL_NE: return v != p.lo;
-    default: return v >= p.lo && v < p.hi;  // HJ3D_SEL_RANGE
-  }
-}
-
-__device__ __forceinline__ bool sel_eval(const RelView& r, const SelArgs& a, uint64_t i) {
-  const char* t = r.base + i * r.stride;
-  bool ok = true;
-  for (uint32_t k = 0; k < a.npred; ++k)
-    ok = ok && sel_one(a.p[k], *reinterpret_cast<const uint32_t*>(t + a.p[k].word_off));
-  return ok;
-}
-
 // Passing tuples per tile: one bitmask per thread (item j = tile + j*kBlock + thread).
 __device__ __forceinline__ uint32_t sel_tile_mask(const RelView& r, const SelArgs& a, uint64_t tile0) {
   uint32_t m = 0;
@@ -115,9 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_sel_write(RelView r, SelArgs a, cons
 hipError_t select_pairs(hj3d_ctx* ctx, const hj3d_rel& rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
                         void* count, hipStream_t s) {
   if (rel.n == 0) return hipMemsetAsync(count, 0, sizeof(uint64_t), s);
-  SelArgs a{};
-  a.npred = npred;
-  for (uint32_t k = 0; k < npred; ++k) a.p[k] = preds[k];
+  const SelArgs a = sel_args(preds, npred);
   const RelView r = view_of(rel);
   const uint64_t ntiles = (rel.n + kSelTile - 1) / kSelTile;
   hipError_t e = ctx->scratch[kScrD].ensure((ntiles + 1) * sizeof(uint32_t));

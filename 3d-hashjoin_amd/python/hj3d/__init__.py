@@ -25,7 +25,7 @@ HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
-OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT = 1, 2, 3, 4
+OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED = 1, 2, 3, 4, 5
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -116,6 +116,7 @@ def lib():
         "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
         "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
         "hj3d_select": (st, [p, R, C.POINTER(_SelPred), u32, p, p]),
+        "hj3d_probe_sel": (st, [p, p, R, C.POINTER(_SelPred), u32, u32, p, u64]),
         "hj3d_gen_keys": (st, [p, p, u64, u32, u32, u64, u64, u64]),
         "hj3d_gen_fk": (st, [p, p, u64, u32, u32, u64, u32, u64]),
         "hj3d_gen_zipf": (st, [p, p, u64, u32, u32, u64, u32, C.c_double, u64]),
@@ -295,12 +296,7 @@ class Context:
         torch = _torch()
         if len(preds) > SEL_MAX:
             raise ValueError(f"at most {SEL_MAX} predicates")
-        arr = (_SelPred * max(1, len(preds)))()
-        for k, pr in enumerate(preds):
-            word, op, lo = pr[0], pr[1], pr[2]
-            hi = pr[3] if len(pr) > 3 and pr[3] is not None else 0
-            signed = pr[4] if len(pr) > 4 else True
-            arr[k] = _SelPred(4 * word, SEL_OPS.get(op, op), int(bool(signed)), 0, int(lo), int(hi))
+        arr = _sel_preds(preds)
         dev = f"cuda:{self.device}"
         if out_pairs is None:
             out_pairs = torch.empty((max(rel.n, 1), 2), dtype=torch.int32, device=dev)
@@ -313,6 +309,25 @@ class Context:
         self.sync()
         n = int(count.item())
         return out_pairs, Rel(out_pairs, 0, 1, n=n), n
+
+    def probe_sel(self, table: "Table", rel: Rel, preds, unique: bool = False, unnest: bool = False, out=None,
+                  fetch: bool = True, checksum: bool = True) -> Optional[ProbeResult]:
+        """scan(rel) -> selection(preds) -> probe (hj3d_probe_sel): the selection fused into the
+        probe partitioner where it applies. n_probe of the result = the passing tuples."""
+        if len(preds) > SEL_MAX:
+            raise ValueError(f"at most {SEL_MAX} predicates")
+        flags = (PROBE_UNIQUE if unique else 0) | (PROBE_UNNEST if unnest else 0) | (PROBE_CHECKSUM if checksum else 0)
+        ptr, cap = None, 0
+        if out is not None:
+            flags |= PROBE_EMIT
+            ptr, cap = out.data_ptr(), out.numel() * out.element_size() // 8
+        self._check(lib().hj3d_probe_sel(self.h, table.h, C.byref(rel.c), _sel_preds(preds), len(preds), flags, ptr,
+                                         cap), "hj3d_probe_sel")
+        return self.probe_result() if fetch else None
+
+    def sel_unfused(self, on: bool = True):
+        """A/B switch: hj3d_probe_sel selects first instead of fusing into the partitioner."""
+        self.set_option(OPT_SEL_UNFUSED, int(on))
 
     # ---- exchange / synthetic data ----
     def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts):
@@ -381,6 +396,16 @@ class Context:
             return None
         self.sync()
         return _res5(r.cpu().tolist())
+
+
+def _sel_preds(preds):
+    arr = (_SelPred * max(1, len(preds)))()
+    for k, pr in enumerate(preds):
+        word, op, lo = pr[0], pr[1], pr[2]
+        hi = pr[3] if len(pr) > 3 and pr[3] is not None else 0
+        signed = pr[4] if len(pr) > 4 else True
+        arr[k] = _SelPred(4 * word, SEL_OPS.get(op, op), int(bool(signed)), 0, int(lo), int(hi))
+    return arr
 
 
 def _res5(v):

@@ -20,6 +20,7 @@
  *   hj3d_table_clear           HtChaining1/HtNested1::clear           ht_chaining.hh:250-258,
  *                                                                     ht_nested.hh:438-447
  *   hj3d_select                AlgSelection / AlgDynSelection::step   algebra.hh:278-358
+ *   hj3d_probe_sel             AlgScan -> AlgSelection -> AlgHashJoinProbe / AlgNestJoinProbe
  *
  * Semantics kept bit-exact with the reference: hash = murmur3 fmix32 (util/hasht.hh:52-61),
  * bucket = hash % num_buckets, and every counter the reference reports (match counts,
@@ -146,7 +147,10 @@ enum {
   /* HJ3D_OPT_NESTED_SORT (0/1, default 0): build nested tables by the LSD key sort (nested.hip)
    * instead of the bucket-range partition + per-partition LDS aggregation (nested_agg.hip, the
    * default for large inputs). */
-  HJ3D_OPT_NESTED_SORT = 4
+  HJ3D_OPT_NESTED_SORT = 4,
+  /* HJ3D_OPT_SEL_UNFUSED (0/1, default 0): hj3d_probe_sel always selects first (hj3d_select) and
+   * probes the passing pairs, instead of fusing the selection into the probe partitioner. */
+  HJ3D_OPT_SEL_UNFUSED = 5
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
@@ -244,6 +248,15 @@ typedef struct {
 } hj3d_sel_pred;
 hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                         void* out_pairs_dev, void* count_dev);
+/* Probe strand behind a selection: scan(probe) -> AlgSelection -> probe, as hj3d_probe of the
+ * passing tuples (rows = their rows in `probe`). On the chaining table's partitioned path with
+ * <= 2 predicates the selection is fused into the probe-side partitioner (the failing tuples are
+ * dropped where the tuples are read; no extra pass); otherwise hj3d_select runs first
+ * (synchronous count read). Result: n_probe = passing tuples (the selection's count()), the
+ * other fields as hj3d_probe. Dense output (chaining + HJ3D_PROBE_UNIQUE) fills n_probe slots
+ * and needs out_cap >= probe->n. */
+hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe, const hj3d_sel_pred* preds,
+                           uint32_t npred, uint32_t flags, void* out_dev, uint64_t out_cap);
 
 /* ---- synthetic key/FK relations generated on the device (bench / full-size checks) ----
  * R.k = a seeded bijective permutation of [0, n_keys) (keys for global rows

@@ -1,6 +1,7 @@
 """Selection pushdown at config-B size on one GPU: hj3d_select over S (1e8 x {k, a, b}) with
 predicate S.b < x at several selectivities, and the selected probe strand (scan -> selection ->
-probe -> count, Csr table on R = 1e7 keys) against the unselected probe. Prints one JSON line.
+probe -> count, Csr table on R = 1e7 keys) select-first and fused (hj3d_probe_sel: the predicate
+evaluated in the probe partitioner) against the unselected probe. Prints one JSON line.
 Algorithmic bytes of the selection: 12 B/tuple read + 8 B per passing tuple written.
 usage: python scripts/time_select.py [--reps N]"""
 import json
@@ -52,10 +53,14 @@ for x in (10, 50, 100):
     _, sel, n_sel = ctx.select(srel, preds, pairs, cnt)
     pm = timed(lambda: ctx.probe(tab, sel, unique=True, out=out, fetch=False, checksum=False))
     r = ctx.probe(tab, sel, unique=True, out=out)
+    fused_ms = timed(lambda: ctx.probe_sel(tab, srel, preds, unique=True, out=out, fetch=False, checksum=False))
+    rf = ctx.probe_sel(tab, srel, preds, unique=True, out=out)
+    assert (rf.n_probe, rf.n_out, rf.n_cmps) == (n_sel, r.n_out, r.n_cmps)
     alg = 12 * nS + 8 * n_sel
     res["runs"].append({"pred": f"S.b < {x}", "selected": n_sel, "select_ms": ms,
                         "select_GBs": alg / ms / 1e6, "select_frac_of_8TBs": alg / ms / 1e6 / 8000.0,
                         "probe_selected_ms": pm, "strand_ms": ms + pm,
-                        "strand_probe_tuples_per_s": nS / ((ms + pm) * 1e-3), "matches": r.n_out})
+                        "strand_probe_tuples_per_s": nS / ((ms + pm) * 1e-3), "matches": r.n_out,
+                        "fused_strand_ms": fused_ms, "fused_scan_tuples_per_s": nS / (fused_ms * 1e-3)})
     assert r.n_out == n_sel, "key/FK join: every selected S tuple has one partner"
 print(json.dumps(res))

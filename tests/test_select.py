@@ -203,3 +203,77 @@ def test_gpu_dropin_selection_pushdown_matches_reference_example():
             assert int(g["Build"]) == c["build_Build"], (plan, mode)
     printed = [[int(v) for v in ln.strip("()").split(",")] for ln in lines if ln.startswith("(")]
     assert printed == EX["algebra_test3"]["output"]
+
+
+FUSED_CASES = [
+    ("lt_signed", [(2, "<", 37)]),
+    ("le_unsigned", [(2, "<=", 0, None, False)]),
+    ("gt", [(2, ">", 90)]),
+    ("ge", [(2, ">=", 50)]),
+    ("eq", [(2, "==", 7)]),
+    ("ne", [(2, "!=", 7)]),
+    ("range", [(2, "range", 20, 30)]),
+    ("empty_range", [(2, "range", 30, 30)]),
+    ("on_key_word", [(1, "<", 1000)]),
+    ("two_preds_unfused", [(2, ">=", 10), (2, "<", 60)]),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("unique", [True, False], ids=["unique", "nonunique"])
+@pytest.mark.parametrize("name,preds", FUSED_CASES, ids=[c[0] for c in FUSED_CASES])
+def test_gpu_probe_sel_bit_exact(ctx, name, preds, unique):
+    """hj3d_probe_sel (selection fused into the probe partitioner for one predicate, select-first
+    otherwise) vs the oracle's probe of oracle.select's output: counters and output checksums."""
+    import hj3d
+    import torch
+    nR, nS = 1 << 14, 1 << 18
+    Rk, Sa, _ = O.gen_exp1(nR, nS, False, 1.0, 0)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    S[:, 2] = np.random.default_rng(5).integers(-5, 100, size=nS).astype(np.int32).view(np.uint32)
+    sel_h = O.select(S, 1, preds)
+    exp = O.chain_plan(R, 0, sel_h, 0, nR, unique, prow=1)
+    ctx.radix_min(1 << 12)  # the partitioned (fusing) path at this size
+    tab = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nR)
+    tab.build(hj3d.Rel(dev(R), 0))
+    out = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    for unfused in (False, True):
+        ctx.sel_unfused(unfused)
+        res = ctx.probe_sel(tab, hj3d.Rel(dev(S), 1), preds, unique=unique, out=out)
+        assert res.n_probe == len(sel_h), unfused
+        assert (res.n_out, res.n_cmps) == (exp.c_top, exp.c_cmp), unfused
+        for k in ("sum_a", "sum_b", "sum_h", "xor_h"):
+            assert getattr(res, k) == exp.out[k], (unfused, k)
+        pairs = out[: res.n_probe if unique else res.n_out].cpu().numpy().view(np.uint32)
+        if unique:
+            pairs = pairs[pairs[:, 1] != 0xFFFFFFFF]
+        got = pairs[:, [0, 1]]
+        assert len(got) == exp.c_top
+        assert sorted(map(tuple, got.tolist())) == sorted(
+            (int(a), int(b)) for a, b in zip(sel_h[:, 1], np.argsort(Rk)[sel_h[:, 0]]))
+    ctx.sel_unfused(False)
+    ctx.radix_min(1 << 20)
+    tab.close()
+
+
+@pytest.mark.gpu
+def test_gpu_probe_sel_nested_unnest(ctx):
+    """A selected probe into a nested table (select-first path) with unnest vs the oracle."""
+    import hj3d
+    Rk, Sa, _ = O.gen_exp1(1 << 12, 1 << 16, True, 0.8, 0)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    R[:, 2] = np.arange(len(R), dtype=np.uint32) % 10
+    S = O.tuples3(np.arange(1 << 16, dtype=np.uint32), Sa)
+    dv = O.num_distinct(Sa)
+    preds = [(2, "<", 3)]
+    sel_h = O.select(R, 0, preds)
+    exp = O.nested_plan(S, 1, sel_h, 0, dv, True, prow=1)
+    tab = hj3d.Table(ctx, hj3d.HJ3D_NESTED, dv)
+    tab.build(hj3d.Rel(dev(S), 1))
+    res = ctx.probe_sel(tab, hj3d.Rel(dev(R), 0), preds, unnest=True)
+    assert res.n_probe == len(sel_h)
+    assert (res.n_matched, res.n_out, res.n_cmps) == (exp.c_probe, exp.c_top, exp.c_cmp)
+    for k in ("sum_a", "sum_b", "sum_h", "xor_h"):
+        assert getattr(res, k) == exp.out[k], k
+    tab.close()
