@@ -442,6 +442,15 @@ inline hj3d_probe_res run_probe(hj3d_table* t, const hj3d_rel& r, uint32_t flags
   return res;
 }
 
+inline hj3d_probe_res run_probe_sel(hj3d_table* t, const hj3d_rel& r, const hj3d_sel_pred* preds, uint32_t npred,
+                                    uint32_t flags) {
+  Engine& e = Engine::get();
+  e.check(hj3d_probe_sel(e.ctx(), t, &r, preds, npred, flags, nullptr, 0), "hj3d_probe_sel");
+  hj3d_probe_res res{};
+  e.check(hj3d_probe_result(e.ctx(), &res), "hj3d_probe_sel");
+  return res;
+}
+
 inline hj3d_probe2_res run_probe2(hj3d_table* ts, hj3d_table* tt, const hj3d_rel& r) {
   Engine& e = Engine::get();
   e.check(hj3d_probe2(e.ctx(), ts, tt, &r, 0, nullptr, 0), "hj3d_probe2");
@@ -510,7 +519,7 @@ class AlgNestJoinProbe : public AlgBase {
     _in.npred = npred;
     _in.selecting = true;
   }
-  inline uint64_t selected_count() const { return _dev.rel.n; }
+  inline uint64_t selected_count() const { return _dev.n_selected; }
   inline void fin(globstat_t* g) {
     if (!_absorbed) execute();
     _consumer->fin(g);
@@ -527,6 +536,7 @@ class AlgNestJoinProbe : public AlgBase {
     auto& dt = _buildOperator->hashtable().device();
     hj3d_table* t = dt.table();
     _dev.make(_in, "AlgNestJoinProbe");
+    _dev.ensure_selected();
     if (_dev.key_word && dt.key_word() && _in.size() && dt.rows())
       check_joinpred<joinpred_t>(_in.at(0), *_dev.key_word, dt.row_ptr(0), *dt.key_word(), "AlgNestJoinProbe");
 
@@ -692,7 +702,7 @@ class AlgHashJoinProbe : public AlgBase {
     _in.npred = npred;
     _in.selecting = true;
   }
-  inline uint64_t selected_count() const { return _dev.rel.n; }
+  inline uint64_t selected_count() const { return _dev.n_selected; }
   inline void fin(globstat_t* g) {
     if (!_absorbed) execute(g);
     _consumer->fin(g);
@@ -715,12 +725,20 @@ class AlgHashJoinProbe : public AlgBase {
     if constexpr (hj3d_is_top<consumer_t>::value) {
       // Csr / CsrUU / Crs: probe -> Top (main_experiment1.cc:623-967)
       if (!_consumer->prints()) {
-        const hj3d_probe_res r = run_probe(t, _dev.rel, kFlags);
+        // a pushed-down selection runs fused into the probe partitioner (hj3d_probe_sel)
+        const hj3d_probe_res r = _dev.pending_sel ? run_probe_sel(t, _dev.rel, _dev.preds, _dev.npred, kFlags)
+                                                  : run_probe(t, _dev.rel, kFlags);
+        if (_dev.pending_sel) {
+          _dev.pending_sel = false;
+          _dev.n_selected = r.n_probe;
+        }
         absorb(r.n_out, r.n_cmps);
         OpAccess::add(*_consumer, r.n_out);
         return;
       }
-    } else if constexpr (hj3d_is_hash_probe<consumer_t>::value) {
+    }
+    _dev.ensure_selected();  // the other pipelines take the selected pairs
+    if constexpr (hj3d_is_hash_probe<consumer_t>::value) {
       // experiment 4 Chj: probe(S) -> probe(T) -> Top (main_experiment4.cc:929-1043)
       using p2_t = consumer_t;
       using top_t = typename p2_t::consumer_t;

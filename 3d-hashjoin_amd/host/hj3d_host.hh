@@ -270,13 +270,18 @@ struct DevInput {
     rel = hj3d_rel{};
     rel.row_off = HJ3D_ROW_IMPLICIT;
     rel.n = in.size();
+    pending_sel = false;
+    n_selected = rel.n;
     key_word.reset();
     if (in.base && in.n) key_word = key_word_from_samples(in.base, in.n, [](const T* t) { return Thashfun::eval(t); });
     if (key_word) {
       rel.base = RelationCache::get().upload(in.base, in.n, sizeof(T));
       rel.stride = sizeof(T);
       rel.key_off = 4 * *key_word;
-      if (in.selecting) select(in);
+      pending_sel = in.selecting;  // applied by the probe (fused) or by ensure_selected()
+      preds = in.preds;
+      npred = in.npred;
+      n_selected = in.selecting ? 0 : rel.n;
       return;
     }
     if (in.selecting)
@@ -297,18 +302,25 @@ struct DevInput {
     rel.key_off = 0;
   }
 
-  // AlgSelection on the device (hj3d_select): rel becomes the passing tuples' (key, row) pairs,
-  // rows still index the batch.
-  void select(const Input<T>& in) {
+  // AlgSelection on the device (hj3d_select), for the paths that do not fuse it: rel becomes the
+  // passing tuples' (key, row) pairs, rows still index the batch.
+  void ensure_selected() {
+    if (!pending_sel) return;
     Engine& e = Engine::get();
     void* d = sel.ensure(rel.n * 8 + 16);
     uint64_t* cnt = reinterpret_cast<uint64_t*>(static_cast<char*>(d) + rel.n * 8 + 8);
-    e.check(hj3d_select(e.ctx(), &rel, in.preds, in.npred, d, cnt), "hj3d_select");
+    e.check(hj3d_select(e.ctx(), &rel, preds, npred, d, cnt), "hj3d_select");
     uint64_t n_sel = 0;
     e.check(hj3d_download(e.ctx(), &n_sel, cnt, 8), "hj3d_download (selection count)");
     rel = hj3d_rel{d, n_sel, 8, 0, 4, 0, 0};
+    pending_sel = false;
+    n_selected = n_sel;
   }
   DevBuffer sel;
+  bool pending_sel = false;  // rel is the whole batch; the selection below is still to apply
+  const hj3d_sel_pred* preds = nullptr;
+  uint32_t npred = 0;
+  uint64_t n_selected = 0;   // the selection's count() once applied
 };
 
 // The device table behind HtChaining1 / HtNested1. Inserted tuples are kept as segments (the
