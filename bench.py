@@ -116,6 +116,37 @@ def cpu_baseline_reference(nR, nS, reps):
     }
 
 
+def cpu_baseline_reference_nrs(nR, nS, theta, reps):
+    """Config C's CPU baseline: the reference's Nrs plan (3D table on Zipf S.a, probe R, unnest,
+    counting Top; main_experiment1.cc:1001-1185) compiled from the reference sources
+    (oracle/_ref/ref_golden.out time_nrs) on a bounded sample (|R|/10, |S|/10), one pinned core.
+    Unit as the config C line: unnested output tuples per second of the probe strand."""
+    if not os.path.exists(REF_BIN):
+        return None
+    core = sorted(os.sched_getaffinity(0))[-1]
+    p = subprocess.run([REF_BIN, "time_nrs", str(nR), str(nS), str(theta), str(reps)], capture_output=True,
+                       text=True, timeout=600, preexec_fn=lambda: os.sched_setaffinity(0, {core}))
+    if p.returncode != 0:
+        log(f"reference CPU baseline (Nrs) failed (rc={p.returncode}): {p.stderr[-500:]}")
+        return None
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    assert r["c_unnest"] == nS, r  # every S tuple's key is in R
+    return {
+        "value": r["c_unnest"] / (r["probe_ns"] * 1e-9),
+        "unit": "output tuples/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": (f"the reference's Nrs plan (AlgNestJoinBuild on S.a, NB = #dv(S.a) = {r['nb']}; AlgNestJoinProbe "
+                   f"-> AlgUnnestHt -> counting AlgTop) compiled from the reference sources "
+                   f"(oracle/_ref/ref_golden.out time_nrs): |R| = {nR}, |S| = {nS} with S.a ~ Zipf({theta}) "
+                   f"(reference generator, mt19937 seed 5489), {reps} reps, clear_ht between reps, 1 pinned core"),
+        "build_ms": r["build_ns"] * 1e-6,
+        "probe_ms": r["probe_ns"] * 1e-6,
+        "host_cpu": _host_cpu(),
+        "nproc": os.cpu_count(),
+    }
+
+
 def cpu_baseline(R_host, S_host, nb, reps):
     """The oracle's single-thread port of the reference Csr plan on a bounded sample, pinned
     to one core (reported baseline, not the target). Used when oracle/_ref is absent."""
@@ -589,6 +620,9 @@ def main_single_config(args):
                      "build_achieved": build_bytes / (build_ms * 1e-3) / 1e9},
         "counters": counters, "verified_bit_exact": verified, "cpu_baseline": None,
     }
+    if args.workload == "C" and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_reference_nrs(max(nR // 10, 1), max(nS // 10, 1), args.theta,
+                                                          args.cpu_reps)
     _emit(line, args)
     if not verified:
         raise SystemExit("verification failed")

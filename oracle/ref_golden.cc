@@ -22,6 +22,7 @@
 //   ref_golden exp1 <nR> <nS> <skew 0|1> <theta> <t> <b> [dump]
 //   ref_golden exp4 <log2R> <alpha> <multA> <beta> <multB> [dump]
 //   ref_golden time_csr <nR> <nS> <reps>      (CPU baseline timing of the reference Csr plan)
+//   ref_golden time_nrs <nR> <nS> <theta> <reps>  (the same for the Nrs plan, Zipf FKs: config C)
 // Prints one JSON object on stdout. With "dump", the generated key columns are
 // also emitted (small sizes only; used for generator known-answer fixtures).
 
@@ -316,6 +317,57 @@ int timeCsr(size_t nR, size_t nS, int reps) {
               opProbe.numCmps(), top.count());
   return 0;
 }
+
+// CPU baseline of config C (bench.py --workload C, kind "reference"): the reference's Nrs plan
+// (main_experiment1.cc:1001-1185: AlgScan(S) -> AlgNestJoinBuild on S.a with NB = #dv(S.a),
+// AlgScan(R) -> AlgNestJoinProbe -> AlgUnnestHt -> counting AlgTop) on |R| = nR unique keys and
+// |S| = nS FKs ~ Zipf(theta) over [0, nR), generated as in main_experiment1.cc:415-457.
+int timeNrs(size_t nR, size_t nS, double theta, int reps) {
+  std::mt19937 rng;
+  std::vector<uint32_t> keysR(nR);
+  for (size_t i = 0; i < nR; ++i) keysR[i] = static_cast<uint32_t>(i);
+  std::shuffle(keysR.begin(), keysR.end(), rng);
+  std::vector<uint32_t> fk;
+  GenRandIntVec griv;
+  GenRandIntVec::param_t p(GenRandIntVec::dist_t::kZipf, static_cast<uint32_t>(nR), 0, theta, 0, -1);
+  griv.generate(fk, static_cast<uint>(nS), p, rng);
+  RelationRS<Tup> R, S;
+  R._tuples.resize(nR);
+  for (size_t i = 0; i < nR; ++i) R._tuples[i] = Tup{keysR[i], 0, 0};
+  S._tuples.resize(nS);
+  for (size_t i = 0; i < nS; ++i) S._tuples[i] = Tup{static_cast<uint32_t>(i), fk[i], 0};
+  const size_t nb = std::max<size_t>(std::unordered_set<uint32_t>(fk.begin(), fk.end()).size(), 1);
+  using build_t = AlgNestJoinBuild<HashA, EqA, GS>;
+  using ht_t = build_t::hashtable_t;
+  using top_t = AlgTop<Pair, GS>;
+  using unnest_t = AlgUnnestHt<top_t, Unnest<ht_t>, ht_t>;
+  using probe_t = AlgNestJoinProbe<unnest_t, build_t, HashK, PredKA, CatNested<ht_t>>;
+  GS gs;
+  build_t opBuild(nb, 10, 10);
+  AlgScan<build_t> scanB(&opBuild, &S);
+  top_t top(gNull, false);
+  unnest_t opUnnest(&top);
+  probe_t opProbe(&opUnnest, &opBuild);
+  AlgScan<probe_t> scanP(&opProbe, &R);
+  using clk = std::chrono::steady_clock;
+  std::chrono::nanoseconds tb{0}, tp{0};
+  for (int r = 0; r < reps; ++r) {
+    if (r) opBuild.clear_ht();
+    const auto t0 = clk::now();
+    scanB.run(&gs);
+    const auto t1 = clk::now();
+    scanP.run(&gs);
+    const auto t2 = clk::now();
+    tb += t1 - t0;
+    tp += t2 - t1;
+  }
+  std::printf("{\"plan\":\"Nrs\",\"nR\":%zu,\"nS\":%zu,\"theta\":%g,\"nb\":%zu,\"reps\":%d,\"build_ns\":%.1f,"
+              "\"probe_ns\":%.1f,\"c_probe\":%" PRIu64 ",\"c_cmp\":%" PRIu64 ",\"c_unnest\":%" PRIu64
+              ",\"c_top\":%" PRIu64 "}\n",
+              nR, nS, theta, nb, reps, double(tb.count()) / reps, double(tp.count()) / reps, opProbe.count(),
+              opProbe.numCmps(), opUnnest.count(), top.count());
+  return 0;
+}
 }  // namespace e1
 
 // =============================== experiment 4 ===================================
@@ -508,6 +560,8 @@ int main(int argc, char** argv) {
   }
   if (argc >= 5 && std::strcmp(argv[1], "time_csr") == 0)
     return e1::timeCsr(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]));
+  if (argc >= 6 && std::strcmp(argv[1], "time_nrs") == 0)
+    return e1::timeNrs(std::stoull(argv[2]), std::stoull(argv[3]), std::atof(argv[4]), std::atoi(argv[5]));
   std::fprintf(stderr, "usage: ref_golden exp1 nR nS skew theta t b [dump] | exp4 log2R a A b B [dump]\n");
   return 2;
 }

@@ -122,3 +122,23 @@ def test_reference_cpu_baseline_timer_counts():
                        4096, True)
     assert (r["c_probe"], r["c_cmp"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_top)
     assert r["reps"] == 2 and r["probe_ns"] > 0
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")),
+                    reason="reference harness not built")
+def test_reference_cpu_baseline_nrs_timer_counts():
+    """bench.py --workload C's cpu_baseline runs the reference Nrs plan (ref_golden.out time_nrs);
+    its counters must be those of the oracle's Nrs plan on the same Zipf generator sequence."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")
+    out = subprocess.run([exe, "time_nrs", "4096", "20000", "0.8", "2"], capture_output=True, text=True, check=True)
+    r = json.loads(out.stdout)
+    Rk, Sa, _ = O.gen_exp1(4096, 20000, True, 0.8, 0)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(20000, dtype=np.uint32), Sa)
+    dv = O.num_distinct(Sa)
+    exp = O.nested_plan(S, 1, R, 0, dv, True)
+    assert r["nb"] == dv
+    assert (r["c_probe"], r["c_cmp"], r["c_unnest"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_unnest, exp.c_top)
+    assert r["reps"] == 2 and r["probe_ns"] > 0
