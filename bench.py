@@ -147,6 +147,36 @@ def cpu_baseline_reference_nrs(nR, nS, theta, reps):
     }
 
 
+def cpu_baseline_reference_ndu(log2R, reps):
+    """Config E's CPU baseline: the reference's Ndu plan (main_experiment4.cc:831-941: two 3D
+    builds, R through both probes, deferred unnesting, counting Top) compiled from the reference
+    sources (oracle/_ref/ref_golden.out time_ndu) on the same workload as the GPU line (log2R,
+    alpha=3 A=4 beta=2 B=2, the reference generator), one pinned core."""
+    if not os.path.exists(REF_BIN):
+        return None
+    core = sorted(os.sched_getaffinity(0))[-1]
+    p = subprocess.run([REF_BIN, "time_ndu", str(log2R), "3", "4", "2", "2", str(reps)], capture_output=True,
+                       text=True, timeout=600, preexec_fn=lambda: os.sched_setaffinity(0, {core}))
+    if p.returncode != 0:
+        log(f"reference CPU baseline (Ndu) failed (rc={p.returncode}): {p.stderr[-500:]}")
+        return None
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    return {
+        "value": r["cardR"] / (r["probe_ns"] * 1e-9),
+        "unit": "probe tuples/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": (f"the reference's Ndu plan (two AlgNestJoinBuild, AlgScan(R) -> AlgNestJoinProbe(S) -> "
+                   f"AlgNestJoinProbe(T) -> AlgUnnestHt x2 -> counting AlgTop) compiled from the reference sources "
+                   f"(oracle/_ref/ref_golden.out time_ndu): the full config E workload, log2R={log2R} alpha=3 A=4 "
+                   f"beta=2 B=2 (c_top = {r['c_top']}), {reps} reps, clear_ht between reps, 1 pinned core"),
+        "build_ms": r["build_ns"] * 1e-6,
+        "probe_ms": r["probe_ns"] * 1e-6,
+        "host_cpu": _host_cpu(),
+        "nproc": os.cpu_count(),
+    }
+
+
 def cpu_baseline(R_host, S_host, nb, reps):
     """The oracle's single-thread port of the reference Csr plan on a bounded sample, pinned
     to one core (reported baseline, not the target). Used when oracle/_ref is absent."""
@@ -623,6 +653,8 @@ def main_single_config(args):
     if args.workload == "C" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_reference_nrs(max(nR // 10, 1), max(nS // 10, 1), args.theta,
                                                           args.cpu_reps)
+    elif args.workload == "E" and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline_reference_ndu(args.log2R, args.cpu_reps)
     _emit(line, args)
     if not verified:
         raise SystemExit("verification failed")

@@ -23,6 +23,7 @@
 //   ref_golden exp4 <log2R> <alpha> <multA> <beta> <multB> [dump]
 //   ref_golden time_csr <nR> <nS> <reps>      (CPU baseline timing of the reference Csr plan)
 //   ref_golden time_nrs <nR> <nS> <theta> <reps>  (the same for the Nrs plan, Zipf FKs: config C)
+//   ref_golden time_ndu <log2R> <a> <A> <b> <B> <reps>  (the experiment-4 Ndu plan: config E)
 // Prints one JSON object on stdout. With "dump", the generated key columns are
 // also emitted (small sizes only; used for generator known-answer fixtures).
 
@@ -543,6 +544,77 @@ int run(uint32_t log2R, uint32_t alpha, uint32_t mA, uint32_t beta, uint32_t mB,
   std::printf("}}\n");
   return 0;
 }
+
+// CPU baseline of config E (bench.py --workload E, kind "reference"): the reference's Ndu plan
+// (main_experiment4.cc:831-941: two AlgNestJoinBuild on S.a, T.a; AlgScan(R) -> probe S -> probe
+// T -> unnest T -> unnest S -> counting AlgTop) on the generation sequence of
+// main_experiment4.cc:517-575 (as run() above). Builds and the probe strand timed separately.
+int timeNdu(uint32_t log2R, uint32_t alpha, uint32_t mA, uint32_t beta, uint32_t mB, int reps) {
+  const size_t cardR = size_t(1) << log2R;
+  const size_t numFkCommon = cardR / (size_t(1) << alpha);
+  const size_t numFkExcl = cardR / (size_t(1) << beta);
+  const size_t cardFkCommon = numFkCommon * mA, cardFkExcl = numFkExcl * mB;
+  const size_t cardFk = cardFkCommon + cardFkExcl;
+  std::mt19937 rng;
+  std::vector<uint32_t> keys(std::max(cardR, cardFk));
+  std::iota(keys.begin(), keys.end(), 0u);
+  std::vector<uint32_t> fkC(cardFkCommon), fkS(cardFkExcl), fkT(cardFkExcl);
+  uint32_t v = 0;
+  size_t idx = 0;
+  for (; v < numFkCommon; ++v) for (uint32_t i = 0; i < mA; ++i) fkC[idx++] = v;
+  idx = 0;
+  for (; v < numFkCommon + numFkExcl; ++v) for (uint32_t i = 0; i < mB; ++i) fkS[idx++] = v;
+  idx = 0;
+  for (; v < numFkCommon + 2 * numFkExcl; ++v) for (uint32_t i = 0; i < mB; ++i) fkT[idx++] = v;
+  RelationRS<Tup> R, S, T;
+  R._tuples.resize(cardR);
+  for (size_t i = 0; i < cardR; ++i) R._tuples[i] = Tup{keys[i], 0};
+  std::shuffle(fkS.begin(), fkS.end(), rng);
+  std::shuffle(fkT.begin(), fkT.end(), rng);
+  std::shuffle(fkC.begin(), fkC.end(), rng);
+  S._tuples.resize(cardFk);
+  for (size_t i = 0; i < cardFk; ++i) S._tuples[i] = Tup{keys[i], i < cardFkCommon ? fkC[i] : fkS[i - cardFkCommon]};
+  std::shuffle(fkC.begin(), fkC.end(), rng);
+  T._tuples.resize(cardFk);
+  for (size_t i = 0; i < cardFk; ++i) T._tuples[i] = Tup{keys[i], i < cardFkCommon ? fkC[i] : fkT[i - cardFkCommon]};
+  const size_t nb = numFkCommon + numFkExcl;
+  GS gs;
+  using top_t = AlgTop<Triple, GS>;
+  using un2_t = AlgUnnestHt<top_t, UnS, nht_t>;
+  using un1_t = AlgUnnestHt<un2_t, UnT, nht_t>;
+  using pRT_t = AlgNestJoinProbe<un1_t, nbuild_t, HashNRS, PredNRS, CatNRST>;
+  using pRS_t = AlgNestJoinProbe<pRT_t, nbuild_t, HashR, PredR, CatNRS>;
+  nbuild_t bS(nb, 10, 10), bT(nb, 10, 10);
+  AlgScan<nbuild_t> scS(&bS, &S), scT(&bT, &T);
+  top_t top(gNull, false);
+  un2_t un2(&top);
+  un1_t un1(&un2);
+  pRT_t pRT(&un1, &bT);
+  pRS_t pRS(&pRT, &bS);
+  AlgScan<pRS_t> scR(&pRS, &R);
+  using clk = std::chrono::steady_clock;
+  std::chrono::nanoseconds tb{0}, tp{0};
+  for (int r = 0; r < reps; ++r) {
+    if (r) {
+      bS.clear_ht();
+      bT.clear_ht();
+    }
+    const auto t0 = clk::now();
+    scS.run(&gs);
+    scT.run(&gs);
+    const auto t1 = clk::now();
+    scR.run(&gs);
+    const auto t2 = clk::now();
+    tb += t1 - t0;
+    tp += t2 - t1;
+  }
+  std::printf("{\"plan\":\"Ndu\",\"cardR\":%zu,\"cardS\":%zu,\"nb\":%zu,\"reps\":%d,\"build_ns\":%.1f,"
+              "\"probe_ns\":%.1f,\"c_probe_rs\":%" PRIu64 ",\"c_probe_rt\":%" PRIu64 ",\"c_unnest_1\":%" PRIu64
+              ",\"c_unnest_2\":%" PRIu64 ",\"c_top\":%" PRIu64 "}\n",
+              cardR, cardFk, nb, reps, double(tb.count()) / reps, double(tp.count()) / reps, pRS.count(),
+              pRT.count(), un1.count(), un2.count(), top.count());
+  return 0;
+}
 }  // namespace e4
 
 }  // namespace
@@ -560,6 +632,9 @@ int main(int argc, char** argv) {
   }
   if (argc >= 5 && std::strcmp(argv[1], "time_csr") == 0)
     return e1::timeCsr(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]));
+  if (argc >= 8 && std::strcmp(argv[1], "time_ndu") == 0)
+    return e4::timeNdu(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
+                       std::atoi(argv[6]), std::atoi(argv[7]));
   if (argc >= 6 && std::strcmp(argv[1], "time_nrs") == 0)
     return e1::timeNrs(std::stoull(argv[2]), std::stoull(argv[3]), std::atof(argv[4]), std::atoi(argv[5]));
   std::fprintf(stderr, "usage: ref_golden exp1 nR nS skew theta t b [dump] | exp4 log2R a A b B [dump]\n");

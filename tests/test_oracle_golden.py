@@ -142,3 +142,25 @@ def test_reference_cpu_baseline_nrs_timer_counts():
     assert r["nb"] == dv
     assert (r["c_probe"], r["c_cmp"], r["c_unnest"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_unnest, exp.c_top)
     assert r["reps"] == 2 and r["probe_ns"] > 0
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")),
+                    reason="reference harness not built")
+def test_reference_cpu_baseline_ndu_timer_counts():
+    """bench.py --workload E's cpu_baseline runs the reference Ndu plan (ref_golden.out time_ndu);
+    its counters must be those of the oracle's Ndu plan on the same generator sequence."""
+    import json
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")
+    out = subprocess.run([exe, "time_ndu", "12", "3", "4", "2", "2", "2"], capture_output=True, text=True, check=True)
+    r = json.loads(out.stdout)
+    Sa, Ta = O.gen_exp4(12, 3, 4, 2, 2)
+    cardR, n = 1 << 12, len(Sa)
+    nb = (cardR >> 3) + (cardR >> 2)  # numFkCommon + numFkExclusive (main_experiment4.cc:855)
+    R = O.tuples2(np.arange(cardR, dtype=np.uint32), np.zeros(cardR, np.uint32))
+    S = O.tuples2(np.arange(n, dtype=np.uint32), Sa)
+    T = O.tuples2(np.arange(n, dtype=np.uint32), Ta)
+    exp = O.exp4_plan(R, S, T, nb, True)
+    assert r["nb"] == nb
+    assert (r["c_probe_rs"], r["c_probe_rt"], r["c_unnest_1"], r["c_unnest_2"], r["c_top"]) == (
+        exp["c_probe_rs"], exp["c_probe_rt"], exp["c_unnest_1"], exp["c_unnest_2"], exp["c_top"])
