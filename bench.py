@@ -315,6 +315,7 @@ def main():
         else:
             ctx.partition(bRel, nb, world, sendB, cntB)
             rB = hdist.exchange(sendB, cntB, recvB)
+            state["build_n"] = rB.shape[0]
             table.build(hj3d.Rel(rB, key_word=0, row_word=1))
             ev[1].record()
             # the probe side in C chunks: partition chunk c, start its all-to-all, then probe
@@ -383,6 +384,15 @@ def main():
         probe_ms = hdist.allreduce_max(probe_ms, dev)
         wall_ms = hdist.allreduce_max(wall_ms, dev)
         kern_avg = {k: (hdist.allreduce_max(v, dev) if v is not None else None) for k, v in kern_avg.items()}
+        # per-GPU imbalance of the bucket-range partition (a Zipf hot key's bucket
+        # lands on one GPU): received tuples and phase times, min / max over ranks
+        local = {"build_tuples": float(state.get("build_n", nB)), "probe_tuples": float(probe_n_local),
+                 "probe_ms": float(sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps)}
+        per_gpu = {}
+        for k, v in local.items():
+            mx, mn = hdist.allreduce_max(v, dev), -hdist.allreduce_max(-v, dev)
+            sm = hdist.allreduce_sum_u64([int(round(v * 1000))], dev)[0] / 1000.0
+            per_gpu[k] = {"min": mn, "max": mx, "max_over_mean": mx / (sm / world) if sm else None}
     else:
         exp_sum, exp_xor = exp_local[:4], exp_local[4]
         got_sum, got_xor = got_local, res.xor_h
@@ -482,6 +492,8 @@ def main():
         "counters": {"c_top": got_sum[0], "c_htProbeCmp": cmps},
         "verified_bit_exact": verified,
     }
+    if world > 1:
+        line["per_gpu"] = per_gpu
     if world == 1 and not args.no_cpu_baseline and plan == "Csr":
         m = min(args.cpu_sample, nS)
         line["cpu_baseline"] = cpu_baseline_reference(nR, m, args.cpu_reps)
