@@ -26,7 +26,13 @@ constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
 constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
 constexpr int kPRoundsR = 8;                     // k_rp_part1r: 8192-tuple tiles
-constexpr int kPSeg = 16;                        // k_rp_part1r: 128-B region segments
+#ifndef HJ3D_PSEG
+#define HJ3D_PSEG 16
+#endif
+#ifndef HJ3D_PROBE_WFRAC
+#define HJ3D_PROBE_WFRAC 0.8
+#endif
+constexpr int kPSeg = HJ3D_PSEG;                 // k_rp_part1r: 128-B region segments
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
@@ -1155,7 +1161,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   const double fill = t->n_build ? double(t->n_build) / double(t->nb_local) : 0.0;
   ProbeParts pp;
   unsigned long long* npass = nullptr;
-  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s, sel,
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(HJ3D_PROBE_WFRAC * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s, sel,
                                  sel ? &npass : nullptr)) != hipSuccess)
     return e;
   SegLaunch L;
