@@ -338,14 +338,17 @@ hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* p
   if ((flags & HJ3D_PROBE_EMIT) && !out_dev && out_cap) return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: EMIT without buffer");
   if ((flags & HJ3D_PROBE_UNNEST) && t->desc.kind != HJ3D_NESTED)
     return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: UNNEST needs a nested table");
-  if (t->desc.kind == HJ3D_CHAIN && !(flags & HJ3D_PROBE_ACCUMULATE) && !ctx->sel_unfused &&
-      radix_probe_applicable(ctx, t, probe->n)) {
+  const bool chain_radix = t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n);
+  const bool nested_radix = t->desc.kind == HJ3D_NESTED && radix_nested_applicable(ctx, t, probe->n);
+  if (!(flags & HJ3D_PROBE_ACCUMULATE) && !ctx->sel_unfused && (chain_radix || nested_radix)) {
     // the selection fused into the probe-side partitioner
     PhaseTimer tm(ctx, HJ3D_T_PROBE);
     uint64_t* res = ctx->res.as<uint64_t>();
     hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
     const SelArgs a = sel_args(preds, npred);
-    if (e == hipSuccess) e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a);
+    if (e == hipSuccess)
+      e = chain_radix ? radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a)
+                      : radix_nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a);
     if (e != hipErrorNotSupported) {
       note_probe(ctx, t, probe->n, flags, out_cap);
       return from_hip(ctx, e, "hj3d_probe_sel");

@@ -210,7 +210,7 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
 // partitioned nested probe (every mode of nested_probe); needs t->n_mains
 bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
 hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                              uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
+                              uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr);
 // exp4.hip
 hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel& r, uint32_t flags,
                   void* out, uint64_t out_cap, uint64_t* res_dev, hipStream_t s);

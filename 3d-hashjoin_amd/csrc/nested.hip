@@ -706,15 +706,16 @@ bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t 
 }
 
 hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                              uint64_t out_cap, uint64_t* res, hipStream_t s) {
+                              uint64_t out_cap, uint64_t* res, hipStream_t s, const SelArgs* sel) {
   hipError_t e;
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbl = t->nb_local;
   // slice width: 80% of the LDS budget at the mean number of main records per bucket (a
   // directory word + a 4-word main record per bucket at fill 1)
   const double fill = double(t->n_mains) / double(nbl);
   ProbeParts pp;
-  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill)), &pp, s)) !=
-      hipSuccess)
+  unsigned long long* npass = nullptr;  // fused selection: tuples passing it (n_probe)
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill)), &pp, s, sel,
+                                 sel ? &npass : nullptr)) != hipSuccess)
     return e;
   const uint32_t nblocks = pp.P * pp.splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
@@ -724,7 +725,9 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
       hipSuccess)
     return e;
   uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
-  if ((e = hipMemcpyAsync(base0, res, sizeof(uint64_t), hipMemcpyDeviceToDevice, s)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(base0, sel ? static_cast<void*>(npass) : static_cast<void*>(res), sizeof(uint64_t),
+                          hipMemcpyDeviceToDevice, s)) != hipSuccess)
+    return e;
   const bool unnest = flags & HJ3D_PROBE_UNNEST;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const uint32_t* off = t->off.as<const uint32_t>();
@@ -774,7 +777,8 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
-  if ((e = reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, r.n, base0)) != hipSuccess) return e;
+  if ((e = reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, sel ? 0ull : r.n, base0)) != hipSuccess)
+    return e;
   if (mode != kCountUN) return hipSuccess;
   // expansion over the slots: regions' then overflow pairs' (unused slots have count 0)
   if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;

@@ -249,8 +249,8 @@ typedef struct {
 hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                         void* out_pairs_dev, void* count_dev);
 /* Probe strand behind a selection: scan(probe) -> AlgSelection -> probe, as hj3d_probe of the
- * passing tuples (rows = their rows in `probe`). On the chaining table's partitioned path with
- * <= 2 predicates the selection is fused into the probe-side partitioner (the failing tuples are
+ * passing tuples (rows = their rows in `probe`). On the partitioned probe path (chaining or nested
+ * table) with one predicate the selection is fused into the probe-side partitioner (the failing tuples are
  * dropped where the tuples are read; no extra pass); otherwise hj3d_select runs first
  * (synchronous count read). Result: n_probe = passing tuples (the selection's count()), the
  * other fields as hj3d_probe. Dense output (chaining + HJ3D_PROBE_UNIQUE) fills n_probe slots

@@ -258,22 +258,33 @@ def test_gpu_probe_sel_bit_exact(ctx, name, preds, unique):
 
 
 @pytest.mark.gpu
-def test_gpu_probe_sel_nested_unnest(ctx):
-    """A selected probe into a nested table (select-first path) with unnest vs the oracle."""
+@pytest.mark.parametrize("unnest", [True, False], ids=["unnest", "nested_tuples"])
+def test_gpu_probe_sel_nested(ctx, unnest):
+    """A selected probe into a nested table (Nrs shape: 3D table on Zipf S.a, probe R), fused into
+    the nested probe's partitioner and select-first, vs the oracle's plan on oracle.select's output."""
     import hj3d
-    Rk, Sa, _ = O.gen_exp1(1 << 12, 1 << 16, True, 0.8, 0)
+    import torch
+    nR, nS = 1 << 14, 1 << 17
+    Rk, Sa, _ = O.gen_exp1(nR, nS, True, 0.8, 0)
     R = O.tuples3(Rk, np.zeros_like(Rk))
-    R[:, 2] = np.arange(len(R), dtype=np.uint32) % 10
-    S = O.tuples3(np.arange(1 << 16, dtype=np.uint32), Sa)
+    R[:, 2] = np.arange(nR, dtype=np.uint32) % 10
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
     dv = O.num_distinct(Sa)
     preds = [(2, "<", 3)]
     sel_h = O.select(R, 0, preds)
-    exp = O.nested_plan(S, 1, sel_h, 0, dv, True, prow=1)
+    exp = O.nested_plan(S, 1, sel_h, 0, dv, unnest, prow=1)
+    ctx.radix_min(1 << 10)  # the partitioned (fusing) nested probe at this size
     tab = hj3d.Table(ctx, hj3d.HJ3D_NESTED, dv)
     tab.build(hj3d.Rel(dev(S), 1))
-    res = ctx.probe_sel(tab, hj3d.Rel(dev(R), 0), preds, unnest=True)
-    assert res.n_probe == len(sel_h)
-    assert (res.n_matched, res.n_out, res.n_cmps) == (exp.c_probe, exp.c_top, exp.c_cmp)
-    for k in ("sum_a", "sum_b", "sum_h", "xor_h"):
-        assert getattr(res, k) == exp.out[k], k
+    out = torch.empty((nS + nR, 2), dtype=torch.int32, device="cuda")
+    for unfused in (False, True):
+        ctx.sel_unfused(unfused)
+        for o in (None, out):
+            res = ctx.probe_sel(tab, hj3d.Rel(dev(R), 0), preds, unnest=unnest, out=o)
+            assert res.n_probe == len(sel_h), (unfused, o is None)
+            assert (res.n_matched, res.n_out, res.n_cmps) == (exp.c_probe, exp.c_top, exp.c_cmp), (unfused, o is None)
+            for k in ("sum_a", "sum_b", "sum_h", "xor_h"):
+                assert getattr(res, k) == exp.out[k], (unfused, o is None, k)
+    ctx.sel_unfused(False)
+    ctx.radix_min(1 << 20)
     tab.close()
