@@ -218,7 +218,7 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
 hipError_t table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out, hipStream_t s);
 // part.hip
 hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t nparts, void* out_pairs,
-                     void* counts, hipStream_t s);
+                     void* counts, hipStream_t s, const SelArgs* sel = nullptr);
 hipError_t select_pairs(hj3d_ctx* ctx, const hj3d_rel& rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
                         void* count, hipStream_t s);
 hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s);

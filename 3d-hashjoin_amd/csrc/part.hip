@@ -19,15 +19,17 @@ __device__ __forceinline__ uint32_t owner_of(uint32_t key, FastMod fm, uint64_t 
   return uint32_t((b * parts) / nb);
 }
 
+// sel: a selection (AlgSelection below the exchange) evaluated where the tuples are read; tuples
+// failing it are not shipped (npred = 0: none).
 __global__ __launch_bounds__(kBlock) void k_part_hist(RelView r, FastMod fm, uint64_t nb, uint32_t parts,
-                                                      uint32_t ntiles, uint32_t* __restrict__ hist) {
+                                                      uint32_t ntiles, uint32_t* __restrict__ hist, SelArgs sel) {
   __shared__ uint32_t h[kMaxParts];
   h[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = uint64_t(blockIdx.x) * kTile;
   for (int j = 0; j < kRounds; ++j) {
     const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
-    if (i < r.n) atomicAdd(&h[owner_of(r.key(i), fm, nb, parts)], 1u);
+    if (i < r.n && (sel.npred == 0 || sel_eval(r, sel, i))) atomicAdd(&h[owner_of(r.key(i), fm, nb, parts)], 1u);
   }
   __syncthreads();
   if (threadIdx.x < parts) hist[uint64_t(threadIdx.x) * ntiles + blockIdx.x] = h[threadIdx.x];
@@ -35,7 +37,7 @@ __global__ __launch_bounds__(kBlock) void k_part_hist(RelView r, FastMod fm, uin
 
 __global__ __launch_bounds__(kBlock) void k_part_scatter(RelView r, FastMod fm, uint64_t nb, uint32_t parts,
                                                          uint32_t ntiles, const uint32_t* __restrict__ offs,
-                                                         uint2* __restrict__ out) {
+                                                         uint2* __restrict__ out, SelArgs sel) {
   __shared__ uint32_t run[kMaxParts];
   __shared__ uint32_t wcnt[kWaves][kMaxParts];
   __shared__ uint32_t tbase[kMaxParts];
@@ -49,7 +51,7 @@ __global__ __launch_bounds__(kBlock) void k_part_scatter(RelView r, FastMod fm, 
     for (int w = 0; w < kWaves; ++w) wcnt[w][threadIdx.x] = 0;
     __syncthreads();
     const uint64_t i = base + uint64_t(j) * kBlock + threadIdx.x;
-    const bool valid = i < r.n;
+    const bool valid = i < r.n && (sel.npred == 0 || sel_eval(r, sel, i));
     const uint32_t key = valid ? r.key(i) : 0u;
     const uint32_t row = valid ? r.row(i) : 0u;
     const uint32_t d = valid ? owner_of(key, fm, nb, parts) : 0u;
@@ -291,7 +293,7 @@ hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n
 }
 
 hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t parts, void* out_pairs, void* counts,
-                     hipStream_t s) {
+                     hipStream_t s, const SelArgs* sel) {
   if (parts == 0 || parts > kMaxParts || nb == 0 || nb >= (1ull << 32)) return hipErrorInvalidValue;
   hipError_t e;
   const uint64_t ntiles = (r.n + kTile - 1) / kTile;
@@ -300,10 +302,12 @@ hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t par
   uint32_t* hist = ctx->scratch[kScrD].as<uint32_t>();
   const FastMod fm = FastMod::make(uint32_t(nb));
   const RelView v = view_of(r);
-  hipLaunchKernelGGL(k_part_hist, dim3(unsigned(ntiles)), dim3(kBlock), 0, s, v, fm, nb, parts, uint32_t(ntiles), hist);
+  const SelArgs sa = sel ? *sel : SelArgs{};
+  hipLaunchKernelGGL(k_part_hist, dim3(unsigned(ntiles)), dim3(kBlock), 0, s, v, fm, nb, parts, uint32_t(ntiles), hist,
+                     sa);
   if ((e = exclusive_scan_u32(ctx, hist, hist, uint64_t(parts) * ntiles, s)) != hipSuccess) return e;
   hipLaunchKernelGGL(k_part_scatter, dim3(unsigned(ntiles)), dim3(kBlock), 0, s, v, fm, nb, parts, uint32_t(ntiles),
-                     hist, static_cast<uint2*>(out_pairs));
+                     hist, static_cast<uint2*>(out_pairs), sa);
   hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(kMaxParts), 0, s, hist, uint32_t(ntiles), parts,
                      static_cast<uint64_t*>(counts));
   return hipGetLastError();

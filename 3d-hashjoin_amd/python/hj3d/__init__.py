@@ -112,6 +112,7 @@ def lib():
         "hj3d_probe2": (st, [p, p, p, R, u32, p, u64]),
         "hj3d_probe2_result": (st, [p, C.POINTER(_Probe2Res)]),
         "hj3d_partition": (st, [p, R, u64, u32, p, p]),
+        "hj3d_partition_sel": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, p]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
         "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
@@ -330,7 +331,13 @@ class Context:
         self.set_option(OPT_SEL_UNFUSED, int(on))
 
     # ---- exchange / synthetic data ----
-    def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts):
+    def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts, preds=None):
+        """Bucket-range partition of rel into (key, row) pairs per destination (stable); with
+        preds, only the tuples passing the selection are partitioned (hj3d_partition_sel)."""
+        if preds:
+            self._check(lib().hj3d_partition_sel(self.h, C.byref(rel.c), _sel_preds(preds), len(preds), num_buckets,
+                                                 parts, out_pairs.data_ptr(), counts.data_ptr()), "hj3d_partition_sel")
+            return
         self._check(lib().hj3d_partition(self.h, C.byref(rel.c), num_buckets, parts, out_pairs.data_ptr(),
                                          counts.data_ptr()), "hj3d_partition")
 

@@ -211,6 +211,12 @@ hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out);
  * follows input order (stable). */
 hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t num_buckets, uint32_t nparts,
                            void* out_pairs_dev, void* counts_dev);
+/* The same with a selection below the exchange (AlgSelection, algebra.hh:278-358): only the tuples
+ * passing the predicate conjunction (hj3d_sel_pred, below) are partitioned and shipped; row ids
+ * stay those of `rel`, so the probe downstream reports the reference's rows. */
+typedef struct hj3d_sel_pred hj3d_sel_pred;
+hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
+                               uint64_t num_buckets, uint32_t nparts, void* out_pairs_dev, void* counts_dev);
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
 
@@ -239,13 +245,13 @@ hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps_dev, uint
  * same order, same row identities. Asynchronous. */
 #define HJ3D_SEL_MAX 4
 enum { HJ3D_SEL_LT = 0, HJ3D_SEL_LE, HJ3D_SEL_GT, HJ3D_SEL_GE, HJ3D_SEL_EQ, HJ3D_SEL_NE, HJ3D_SEL_RANGE };
-typedef struct {
+struct hj3d_sel_pred {
   uint32_t word_off;  /* byte offset of the compared u32 word, multiple of 4, < stride */
   uint32_t op;        /* HJ3D_SEL_*                                                    */
   uint32_t is_signed; /* compare as int32 (the reference's attrval_t is int)           */
   uint32_t reserved;
   int64_t lo, hi;
-} hj3d_sel_pred;
+};
 hj3d_status hj3d_select(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                         void* out_pairs_dev, void* count_dev);
 /* Probe strand behind a selection: scan(probe) -> AlgSelection -> probe, as hj3d_probe of the

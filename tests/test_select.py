@@ -288,3 +288,41 @@ def test_gpu_probe_sel_nested(ctx, unnest):
     ctx.sel_unfused(False)
     ctx.radix_min(1 << 20)
     tab.close()
+
+
+def _fmix32(x):
+    x = x.astype(np.uint64)
+    x ^= x >> np.uint64(16)
+    x = (x * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(13)
+    x = (x * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    x ^= x >> np.uint64(16)
+    return x
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("parts", [2, 8])
+def test_gpu_partition_with_selection(ctx, parts):
+    """hj3d_partition_sel (selection below the multi-GPU exchange): per destination, the passing
+    tuples' (key, row) pairs in scan order, destination = owner of murmur32(key) % NB (§8e)."""
+    import hj3d
+    import torch
+    n, nb = 300_001, 100_003
+    rng = np.random.default_rng(11)
+    t = np.stack([rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32),
+                  rng.integers(0, nb, n).astype(np.uint32),
+                  rng.integers(0, 100, n).astype(np.uint32)], axis=1)
+    preds = [(2, ">=", 25), (2, "<", 75)]
+    sel = O.select(t, 1, preds)
+    owner = ((_fmix32(sel[:, 0]) % np.uint64(nb)) * np.uint64(parts) // np.uint64(nb)).astype(np.int64)
+    out = torch.empty((n, 2), dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(parts, dtype=torch.int64, device="cuda")
+    ctx.partition(hj3d.Rel(dev(t), 1), nb, parts, out, cnt, preds=preds)
+    got_cnt = cnt.cpu().tolist()
+    assert got_cnt == [int((owner == d).sum()) for d in range(parts)]
+    got = out[: sum(got_cnt)].cpu().numpy().view(np.uint32)
+    off = 0
+    for d in range(parts):
+        exp = sel[owner == d]
+        assert (got[off: off + len(exp)] == exp).all(), d
+        off += len(exp)
