@@ -81,6 +81,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libhj3d.so not found at {LIB_PATH}; build it with `make -C 3d-hashjoin_amd` "
                           "or __graft_entry__.build()")
+    # torch first: its HIP runtime is then the one libhj3d.so binds to (one runtime per process;
+    # with libhj3d.so loaded first, torch and the library ended up on different runtimes and
+    # hj3d_ctx_create saw no device)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     p, u64, u32, i32, st = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int, C.c_int
     R, D = C.POINTER(_Rel), C.POINTER(_Desc)
