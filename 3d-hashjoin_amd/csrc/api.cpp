@@ -45,6 +45,31 @@ bool rel_ok(const hj3d_rel* r) {
 }
 
 constexpr int kResFields = 16;
+// result-slot words beyond the counters: n_out before the current probe call, and a sticky flag
+// set when a call's non-dense output exceeded its own buffer (accumulated strands included)
+constexpr int kResOutMark = 14, kResOvf = 15;
+
+__global__ void k_out_overflow(uint64_t* res, uint64_t cap) {
+  if (threadIdx.x == 0 && res[2] - res[kResOutMark] > cap) res[kResOvf] = 1;
+}
+
+bool dense_output(const hj3d_table* t, uint32_t flags) {
+  return (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
+}
+
+// Non-dense EMIT probes (chains without early exit, unnest) write as many pairs as they find; the
+// kernels drop pairs past out_cap. Mark n_out before the call and compare after it, on the stream.
+hipError_t out_mark(hj3d_ctx* ctx, const hj3d_table* t, uint32_t flags) {
+  if (!(flags & HJ3D_PROBE_EMIT) || dense_output(t, flags)) return hipSuccess;
+  uint64_t* res = ctx->res.as<uint64_t>();
+  return hipMemcpyAsync(res + kResOutMark, res + 2, sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->stream);
+}
+
+hipError_t out_check(hj3d_ctx* ctx, const hj3d_table* t, uint32_t flags, uint64_t out_cap) {
+  if (!(flags & HJ3D_PROBE_EMIT) || dense_output(t, flags)) return hipSuccess;
+  hipLaunchKernelGGL(k_out_overflow, dim3(1), dim3(64), 0, ctx->stream, ctx->res.as<uint64_t>(), out_cap);
+  return hipGetLastError();
+}
 
 }  // namespace
 
@@ -286,7 +311,7 @@ hj3d_status hj3d_table_size(hj3d_ctx* ctx, const hj3d_table* t, uint64_t* n_entr
 static void note_probe(hj3d_ctx* ctx, const hj3d_table* t, uint64_t n, uint32_t flags, uint64_t out_cap) {
   const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
   ctx->res_flags = flags;
-  ctx->res_dense = (t->desc.kind == HJ3D_CHAIN) ? (flags & HJ3D_PROBE_UNIQUE) != 0 : !(flags & HJ3D_PROBE_UNNEST);
+  ctx->res_dense = dense_output(t, flags);
   ctx->res_cap = (flags & HJ3D_PROBE_EMIT) ? out_cap : ~0ull;
   ctx->res_nprobe = acc ? ctx->res_nprobe + n : n;
   // dense output: each call needs one slot per probe tuple of its own buffer
@@ -313,6 +338,7 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   uint64_t* res = ctx->res.as<uint64_t>();
   const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
   hipError_t e = acc ? hipSuccess : hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+  if (e == hipSuccess) e = out_mark(ctx, t, flags);
   if (e == hipSuccess) {
     e = hipErrorNotSupported;
     if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n))
@@ -325,6 +351,7 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
                                        : nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
     }
   }
+  if (e == hipSuccess) e = out_check(ctx, t, flags, out_cap);
   note_probe(ctx, t, probe->n, flags, out_cap);
   return from_hip(ctx, e, "hj3d_probe");
 }
@@ -349,6 +376,7 @@ hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* p
     if (e == hipSuccess)
       e = chain_radix ? radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a)
                       : radix_nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, &a);
+    if (e == hipSuccess) e = out_check(ctx, t, flags, out_cap);
     if (e != hipErrorNotSupported) {
       note_probe(ctx, t, probe->n, flags, out_cap);
       return from_hip(ctx, e, "hj3d_probe_sel");
@@ -382,7 +410,7 @@ hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out) {
   out->sum_c = h[6];
   out->sum_h = h[7];
   out->xor_h = h[8];
-  const bool ovf = ctx->res_dense ? ctx->res_overflow : (!ctx->res_accumulated && out->n_out > ctx->res_cap);
+  const bool ovf = ctx->res_dense ? ctx->res_overflow : h[kResOvf] != 0;
   if ((ctx->res_flags & HJ3D_PROBE_EMIT) && ovf) return fail(ctx, HJ3D_EOVERFLOW, "hj3d_probe: output buffer too small");
   return HJ3D_OK;
 }

@@ -130,6 +130,8 @@ def lib():
         "hj3d_gen_zipf": (st, [p, p, u64, u32, u32, u64, u32, C.c_double, u64]),
         "hj3d_expected_fk_join": (st, [p, R, R, u64, i32, p]),
         "hj3d_expected_fk_join_gen": (st, [p, R, u64, u64, i32, p]),
+        "hj3d_gen_exp1_ref": (st, [u64, u64, i32, C.c_double, u32, p, p, i32]),
+        "hj3d_gen_exp4_ref": (st, [u32, u32, u32, u32, u32, p, p, C.POINTER(u64)]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -427,6 +429,35 @@ def _res5(v):
     return {"n": v[0], "sum_a": v[1], "sum_b": v[2], "sum_h": v[3], "xor_h": v[4]}
 
 
+def gen_exp1_ref(nR: int, nS: int, skew: bool = False, theta: float = 1.0, t: int = 0, threads: int = 0):
+    """The reference's experiment-1 input columns (hj3d_gen_exp1_ref: Experiment1::init,
+    main_experiment1.cc:415-457, bit-exact; host only, no GPU): returns numpy u32 (R.k, S.a)."""
+    import numpy as np
+    Rk = np.empty(nR, dtype=np.uint32)
+    Sa = np.empty(max(nS, 1), dtype=np.uint32)
+    st = lib().hj3d_gen_exp1_ref(nR, nS, int(bool(skew)), float(theta), t, Rk.ctypes.data, Sa.ctypes.data, threads)
+    if st != HJ3D_OK:
+        raise Hj3dError(st, "hj3d_gen_exp1_ref: invalid arguments")
+    return Rk, Sa[:nS]
+
+
+def gen_exp4_ref(log2R: int, alpha: int, mult_a: int, beta: int, mult_b: int):
+    """The reference's experiment-4 FK columns (hj3d_gen_exp4_ref: Experiment4::init,
+    main_experiment4.cc:517-575, bit-exact; host only): returns numpy u32 (S.a, T.a)."""
+    import numpy as np
+    card = C.c_uint64()
+    L = lib()
+    st = L.hj3d_gen_exp4_ref(log2R, alpha, mult_a, beta, mult_b, None, None, C.byref(card))
+    if st != HJ3D_OK:
+        raise Hj3dError(st, "hj3d_gen_exp4_ref: invalid arguments")
+    Sa = np.empty(max(card.value, 1), dtype=np.uint32)
+    Ta = np.empty(max(card.value, 1), dtype=np.uint32)
+    st = L.hj3d_gen_exp4_ref(log2R, alpha, mult_a, beta, mult_b, Sa.ctypes.data, Ta.ctypes.data, C.byref(card))
+    if st != HJ3D_OK:
+        raise Hj3dError(st, "hj3d_gen_exp4_ref: invalid arguments")
+    return Sa[:card.value], Ta[:card.value]
+
+
 def part_range(num_buckets: int, parts: int, part: int):
     lo, hi = C.c_uint64(), C.c_uint64()
     lib().hj3d_part_range(num_buckets, parts, part, C.byref(lo), C.byref(hi))
@@ -471,4 +502,5 @@ class Table:
             pass
 
 
-from .plans import EXP1_PLANS, exp1_plan, exp4_plan, num_buckets_exp1  # noqa: E402,F401
+from .plans import (EXP1_PLANS, exp1_plan, exp1_relations_ref, exp4_plan, exp4_relations_ref,  # noqa: E402,F401
+                    num_buckets_exp1)

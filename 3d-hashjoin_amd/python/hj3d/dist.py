@@ -46,26 +46,56 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
     return out
 
 
-def exchange_async(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torch.Tensor, group=None):
-    """exchange() with the pair all-to-all left in flight: returns (received view, work handle).
-    The counts are exchanged synchronously (the host needs the split sizes). work.wait() makes
-    the current stream wait for the pairs; with gloo (host-staged rehearsal) it is synchronous and
-    the handle is None."""
-    if _host_staged(group):
-        return exchange(send_pairs, send_counts, recv_buf, group), None
+def exchange_counts(send_counts: torch.Tensor, group=None):
+    """All-to-all of the per-destination counts of several partitioned chunks at once (one
+    collective, one host synchronisation for a whole probe strand, instead of one per chunk).
+
+    send_counts: int64 [C, P] (row c = hj3d_partition's counts of chunk c). Returns host lists
+    (send[c][p], recv[c][p]): recv[c][p] = pairs rank p sends this rank in chunk c."""
     world = dist.get_world_size(group)
-    recv_counts = torch.empty_like(send_counts)
-    dist.all_to_all_single(recv_counts, send_counts, group=group)
-    sc = send_counts.tolist()
-    rc = recv_counts.tolist()
-    assert len(sc) == world
+    C = send_counts.shape[0]
+    src = send_counts.t().contiguous()  # [P, C]: the block for destination p is contiguous
+    if _host_staged(group) and src.is_cuda:
+        src = src.cpu()
+    recv = torch.empty_like(src)
+    dist.all_to_all_single(recv, src, group=group)
+    sc = send_counts.cpu().tolist()
+    rc = recv.view(world, C).t().cpu().tolist()
+    return sc, rc
+
+
+def exchange_pairs_async(send_pairs: torch.Tensor, sc: list[int], rc: list[int], recv_buf: torch.Tensor,
+                         group=None):
+    """The pair all-to-all of one chunk whose counts were exchanged (exchange_counts), left in flight:
+    returns (received view, work handle or None for the host-staged gloo rehearsal). recv_buf must
+    hold sum(rc) pairs: every rank knows its own receive total before any pair collective starts,
+    so a short buffer is the caller's sizing error, reported before the collective (never a hang)."""
     total = int(sum(rc))
     if recv_buf.shape[0] < total:
         raise RuntimeError(f"exchange: receive buffer holds {recv_buf.shape[0]} pairs, {total} arrive")
     out = recv_buf[:total]
-    work = dist.all_to_all_single(out, send_pairs[: int(sum(sc))], output_split_sizes=rc, input_split_sizes=sc,
-                                  group=group, async_op=True)
+    src = send_pairs[: int(sum(sc))]
+    if _host_staged(group) and send_pairs.is_cuda:
+        got = torch.empty((total, 2), dtype=send_pairs.dtype)
+        dist.all_to_all_single(got, src.cpu(), output_split_sizes=rc, input_split_sizes=sc, group=group)
+        out.copy_(got)
+        return out, None
+    work = dist.all_to_all_single(out, src, output_split_sizes=rc, input_split_sizes=sc, group=group, async_op=True)
     return out, work
+
+
+def allreduce_stats(st: dict, device) -> dict:
+    """HtStatistics of a bucket-range sharded table (each rank's table holds a disjoint bucket range):
+    counts add, extremes take max / min, so the result is the single-table statistics."""
+    add = ("nb", "empty", "entries", "distinct", "cc0_sum", "cc0_cnt", "cc1_sum", "cc1_cnt")
+    out = dict(zip(add, allreduce_sum_u64([st[k] for k in add], device)))
+    for k in ("cc0_max", "cc1_max"):
+        out[k] = int(allreduce_max(float(st[k]), device))
+    for k in ("cc0_min", "cc1_min"):
+        # ranks whose shard has no non-empty bucket report cc1_min = 0 with cc1_cnt = 0: skip them
+        v = st[k] if (k == "cc0_min" or st["cc1_cnt"]) else float(1 << 52)
+        out[k] = int(-allreduce_max(-float(v), device))
+    return out
 
 
 def num_distinct(bitmap: torch.Tensor, or_popcount, group=None) -> int:

@@ -59,6 +59,39 @@ def exp1_plan(ctx: Context, plan: str, R, S, nb: int, out=None, table: Table | N
     return res
 
 
+def exp1_relations_ref(nR: int, nS: int, skew: bool = False, theta: float = 1.0, t: int = 0, device="cuda"):
+    """The reference's experiment-1 relations R {k,0,0}, S {i,a,0} (main_experiment1.cc:415-457,
+    495-515) from the bit-exact generator (hj3d_gen_exp1_ref), as (n, 3) int32 device tensors:
+    the generated columns are uploaded and scattered into the AoS tuples on the device."""
+    import torch
+    from . import gen_exp1_ref
+    Rk, Sa = gen_exp1_ref(nR, nS, skew, theta, t)
+    R = torch.zeros((nR, 3), dtype=torch.int32, device=device)
+    S = torch.zeros((nS, 3), dtype=torch.int32, device=device)
+    R[:, 0] = torch.from_numpy(Rk.view("int32")).to(device)
+    S[:, 0] = torch.arange(nS, dtype=torch.int32, device=device)
+    S[:, 1] = torch.from_numpy(Sa.view("int32")).to(device)
+    return R, S
+
+
+def exp4_relations_ref(log2R: int, alpha: int, mult_a: int, beta: int, mult_b: int, device="cuda"):
+    """The reference's experiment-4 relations R {k,0}, S {k,a}, T {k,a} (main_experiment4.cc:517-575)
+    from the bit-exact generator (hj3d_gen_exp4_ref), as (n, 2) int32 device tensors."""
+    import torch
+    from . import gen_exp4_ref
+    Sa, Ta = gen_exp4_ref(log2R, alpha, mult_a, beta, mult_b)
+    n, nR = len(Sa), 1 << log2R
+    R = torch.zeros((nR, 2), dtype=torch.int32, device=device)
+    R[:, 0] = torch.arange(nR, dtype=torch.int32, device=device)
+    S = torch.zeros((n, 2), dtype=torch.int32, device=device)
+    T = torch.zeros((n, 2), dtype=torch.int32, device=device)
+    S[:, 0] = torch.arange(n, dtype=torch.int32, device=device)
+    T[:, 0] = S[:, 0]
+    S[:, 1] = torch.from_numpy(Sa.view("int32")).to(device)
+    T[:, 1] = torch.from_numpy(Ta.view("int32")).to(device)
+    return R, S, T
+
+
 def exp4_plan(ctx: Context, plan: str, R, S, T, nb: int) -> dict:
     """Experiment-4 Ndu (nested, deferred unnesting) or Chj (chaining) on {k,a} relations."""
     kind = HJ3D_NESTED if plan == "Ndu" else HJ3D_CHAIN

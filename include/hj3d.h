@@ -277,6 +277,22 @@ hj3d_status hj3d_gen_fk(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t st
  * global row id: config C (nested table, Zipf 0.8 duplicates) at full size. */
 hj3d_status hj3d_gen_zipf(hj3d_ctx* ctx, void* tuples_dev, uint64_t n, uint32_t stride, uint32_t key_off,
                           uint64_t row_base, uint32_t fk_max, double theta, uint64_t seed);
+/* ---- the reference's own input generators (host, synchronous, bit-exact) ----
+ * hj3d_gen_exp1_ref replaces Experiment1::init (main_experiment1.cc:415-457): one std::mt19937
+ * stream (seed 5489) shuffles R.k = iota(nR) (std::shuffle), draws S.a uniform over [0, fkMax)
+ * (GenRandIntVec::generate_uni, util/GenRandIntVec.cc:72-98) or Zipf(theta) - 1
+ * (generate_zipf :167-200, util/zipf_distribution.hh:48-58), then permutes S.a (vec_permute
+ * :335-340); fkMax = nR >> t (main_experiment1.cc:190). Writes the columns Rk[nR], Sa[nS] to
+ * HOST memory; S.k is the row id. theta: the reference's experiment 1 fixes 1.0 (:444); config C
+ * uses 0.8. threads: workers for the Zipf attempts (0 = min(hardware threads, 16)); the result does
+ * not depend on it.
+ * hj3d_gen_exp4_ref replaces Experiment4::init (main_experiment4.cc:517-575): S.a, T.a of
+ * card = (2^log2R >> alpha) * mult_a + (2^log2R >> beta) * mult_b tuples each (R.k, S.k, T.k =
+ * iota). With Sa or Ta NULL only *card is written. */
+hj3d_status hj3d_gen_exp1_ref(uint64_t nR, uint64_t nS, int skew, double theta, uint32_t t, uint32_t* Rk,
+                              uint32_t* Sa, int threads);
+hj3d_status hj3d_gen_exp4_ref(uint32_t log2R, uint32_t alpha, uint32_t mult_a, uint32_t beta, uint32_t mult_b,
+                              uint32_t* Sa, uint32_t* Ta, uint64_t* card);
 /* Expected key/FK join aggregates WITHOUT a hash table (full-size verification of the
  * key/FK plans): `build` holds unique keys in [0, n_keys); every probe tuple's partner row is
  * inv[key], inv being the inverse of the build key column. Accumulates {n_out, sum_a, sum_b,

@@ -21,7 +21,8 @@
 // Usage:
 //   ref_golden exp1 <nR> <nS> <skew 0|1> <theta> <t> <b> [dump]
 //   ref_golden exp4 <log2R> <alpha> <multA> <beta> <multB> [dump]
-//   ref_golden time_csr <nR> <nS> <reps>      (CPU baseline timing of the reference Csr plan)
+//   ref_golden time_csr <nR> <nS> <min_reps> [prefix]  (CPU baseline timing of the reference Csr plan,
+//                                      repeat_mintime; probe side = the first `prefix` S tuples)
 //   ref_golden time_nrs <nR> <nS> <theta> <reps>  (the same for the Nrs plan, Zipf FKs: config C)
 //   ref_golden time_ndu <log2R> <a> <A> <b> <B> <reps>  (the experiment-4 Ndu plan: config E)
 // Prints one JSON object on stdout. With "dump", the generated key columns are
@@ -41,6 +42,7 @@
 
 #include "util/GenRandIntVec.hh"
 #include "util/hasht.hh"
+#include "util/measure_helpers.hh"
 #include "algebra.hh"
 #include "ht_chaining.hh"
 #include "ht_nested.hh"
@@ -218,7 +220,7 @@ void planNested(const char* name, RelationRS<Tup>& build, RelationRS<Tup>& probe
   std::printf("}");
 }
 
-int run(size_t nR, size_t nS, bool skew, double theta, uint32_t t, uint32_t b, bool dump) {
+int run(size_t nR, size_t nS, bool skew, double theta, uint32_t t, uint32_t b, bool dump, const std::string& only) {
   // Same generation sequence as main_experiment1.cc:415-457 (exact cardinalities instead of 2^x).
   std::mt19937 rng;
   std::vector<uint32_t> keysR(nR);
@@ -255,18 +257,17 @@ int run(size_t nR, size_t nS, bool skew, double theta, uint32_t t, uint32_t b, b
     printAll("Sa", fk);
     std::printf(",");
   }
+  // `only` (comma-separated plan names, empty = all) restricts the plans, for the largest inputs
+  const auto want = [&](const char* plan) { return only.empty() || ("," + only + ",").find(std::string(",") + plan + ",") != std::string::npos; };
+  bool first = true;
+  const auto sep = [&]() { if (!first) std::printf(","); first = false; };
   std::printf("\"plans\":{");
-  planChaining<HashK, EqK, HashA, PredAK, true>("Csr", R, S, nbR);
-  std::printf(",");
-  planChaining<HashK, EqK, HashA, PredAK, false>("CsrUU", R, S, nbR);
-  std::printf(",");
-  planChaining<HashA, EqA, HashK, PredKA, false>("Crs", S, R, nbS);
-  std::printf(",");
-  planNested<HashK, EqK, HashA, PredAK>("Nsr", R, S, nbR, true);
-  std::printf(",");
-  planNested<HashA, EqA, HashK, PredKA>("Nrs", S, R, nbS, true);
-  std::printf(",");
-  planNested<HashA, EqA, HashK, PredKA>("NrsNU", S, R, nbS, false);
+  if (want("Csr")) { sep(); planChaining<HashK, EqK, HashA, PredAK, true>("Csr", R, S, nbR); }
+  if (want("CsrUU")) { sep(); planChaining<HashK, EqK, HashA, PredAK, false>("CsrUU", R, S, nbR); }
+  if (want("Crs")) { sep(); planChaining<HashA, EqA, HashK, PredKA, false>("Crs", S, R, nbS); }
+  if (want("Nsr")) { sep(); planNested<HashK, EqK, HashA, PredAK>("Nsr", R, S, nbR, true); }
+  if (want("Nrs")) { sep(); planNested<HashA, EqA, HashK, PredKA>("Nrs", S, R, nbS, true); }
+  if (want("NrsNU")) { sep(); planNested<HashA, EqA, HashK, PredKA>("NrsNU", S, R, nbS, false); }
   std::printf("}}\n");
   return 0;
 }
@@ -276,7 +277,7 @@ int run(size_t nR, size_t nS, bool skew, double theta, uint32_t t, uint32_t b, b
 // unique -> counting AlgTop, clear_ht between repetitions) timed on a uniform key/FK input of
 // |R| = nR, |S| = nS generated as in main_experiment1.cc:415-457. Build and probe are timed
 // separately with steady_clock, averaged over `reps` repetitions.
-int timeCsr(size_t nR, size_t nS, int reps) {
+int timeCsr(size_t nR, size_t nS, int reps, size_t prefix) {
   std::mt19937 rng;
   std::vector<uint32_t> keysR(nR);
   for (size_t i = 0; i < nR; ++i) keysR[i] = static_cast<uint32_t>(i);
@@ -285,11 +286,16 @@ int timeCsr(size_t nR, size_t nS, int reps) {
   GenRandIntVec griv;
   GenRandIntVec::param_t p(GenRandIntVec::dist_t::kUni, static_cast<uint32_t>(nR), 0, 0.0, 0, -1);
   griv.generate(fk, static_cast<uint>(nS), p, rng);
+  // the probe side: the first `prefix` tuples of the generated |S| = nS relation (all of it when
+  // prefix is 0), so a bounded sample is a prefix of exactly the relation the GPU line joins
+  const size_t nP = prefix && prefix < nS ? prefix : nS;
   RelationRS<Tup> R, S;
   R._tuples.resize(nR);
   for (size_t i = 0; i < nR; ++i) R._tuples[i] = Tup{keysR[i], 0, 0};
-  S._tuples.resize(nS);
-  for (size_t i = 0; i < nS; ++i) S._tuples[i] = Tup{static_cast<uint32_t>(i), fk[i], 0};
+  S._tuples.resize(nP);
+  for (size_t i = 0; i < nP; ++i) S._tuples[i] = Tup{static_cast<uint32_t>(i), fk[i], 0};
+  fk.clear();
+  fk.shrink_to_fit();
 
   using build_t = AlgHashJoinBuild<HashK, EqK, GS>;
   using top_t = AlgTop<Pair, GS>;
@@ -302,20 +308,26 @@ int timeCsr(size_t nR, size_t nS, int reps) {
   AlgScan<probe_t> scanP(&opProbe, &S);
   using clk = std::chrono::steady_clock;
   std::chrono::nanoseconds tb{0}, tp{0};
-  for (int r = 0; r < reps; ++r) {
-    if (r) opBuild.clear_ht();
-    const auto t0 = clk::now();
-    scanB.run(&gs);
-    const auto t1 = clk::now();
-    scanP.run(&gs);
-    const auto t2 = clk::now();
-    tb += t1 - t0;
-    tp += t2 - t1;
-  }
-  std::printf("{\"plan\":\"Csr\",\"nR\":%zu,\"nS\":%zu,\"reps\":%d,\"build_ns\":%.1f,\"probe_ns\":%.1f,"
-              "\"c_probe\":%" PRIu64 ",\"c_cmp\":%" PRIu64 ",\"c_top\":%" PRIu64 "}\n",
-              nR, nS, reps, double(tb.count()) / reps, double(tp.count()) / reps, opProbe.count(),
-              opProbe.numCmps(), top.count());
+  // main_experiment1.cc:663-699: repeat_mintime (util/measure_helpers.hh:15-41) with >= 300 ms and
+  // `reps` minimum repetitions, clear_ht between repetitions (not after the last)
+  const auto [tot, n] = df::infra::repeat_mintime(
+      std::chrono::milliseconds(300),
+      [&]() {
+        const auto t0 = clk::now();
+        scanB.run(&gs);
+        const auto t1 = clk::now();
+        scanP.run(&gs);
+        const auto t2 = clk::now();
+        tb += t1 - t0;
+        tp += t2 - t1;
+      },
+      [&]() { opBuild.clear_ht(); }, false, size_t(reps > 0 ? reps : 1));
+  (void)tot;
+  const double nr = double(n);
+  std::printf("{\"plan\":\"Csr\",\"nR\":%zu,\"nS\":%zu,\"probe_prefix\":%zu,\"reps\":%zu,\"build_ns\":%.1f,"
+              "\"probe_ns\":%.1f,\"c_probe\":%" PRIu64 ",\"c_cmp\":%" PRIu64 ",\"c_top\":%" PRIu64 "}\n",
+              nR, nS, nP, n, double(tb.count()) / nr, double(tp.count()) / nr, opProbe.count(),
+              opProbe.numCmps(), top.count());  // counters of the last repetition (AlgScan::run resets them)
   return 0;
 }
 
@@ -352,20 +364,23 @@ int timeNrs(size_t nR, size_t nS, double theta, int reps) {
   AlgScan<probe_t> scanP(&opProbe, &R);
   using clk = std::chrono::steady_clock;
   std::chrono::nanoseconds tb{0}, tp{0};
-  for (int r = 0; r < reps; ++r) {
-    if (r) opBuild.clear_ht();
-    const auto t0 = clk::now();
-    scanB.run(&gs);
-    const auto t1 = clk::now();
-    scanP.run(&gs);
-    const auto t2 = clk::now();
-    tb += t1 - t0;
-    tp += t2 - t1;
-  }
-  std::printf("{\"plan\":\"Nrs\",\"nR\":%zu,\"nS\":%zu,\"theta\":%g,\"nb\":%zu,\"reps\":%d,\"build_ns\":%.1f,"
+  // repeat_mintime (util/measure_helpers.hh:15-41): >= 300 ms, >= `reps` repetitions, clear_ht between
+  const size_t n = df::infra::repeat_mintime(
+      std::chrono::milliseconds(300),
+      [&]() {
+        const auto t0 = clk::now();
+        scanB.run(&gs);
+        const auto t1 = clk::now();
+        scanP.run(&gs);
+        const auto t2 = clk::now();
+        tb += t1 - t0;
+        tp += t2 - t1;
+      },
+      [&]() { opBuild.clear_ht(); }, false, size_t(reps > 0 ? reps : 1)).second;
+  std::printf("{\"plan\":\"Nrs\",\"nR\":%zu,\"nS\":%zu,\"theta\":%g,\"nb\":%zu,\"reps\":%zu,\"build_ns\":%.1f,"
               "\"probe_ns\":%.1f,\"c_probe\":%" PRIu64 ",\"c_cmp\":%" PRIu64 ",\"c_unnest\":%" PRIu64
               ",\"c_top\":%" PRIu64 "}\n",
-              nR, nS, theta, nb, reps, double(tb.count()) / reps, double(tp.count()) / reps, opProbe.count(),
+              nR, nS, theta, nb, n, double(tb.count()) / n, double(tp.count()) / n, opProbe.count(),
               opProbe.numCmps(), opUnnest.count(), top.count());
   return 0;
 }
@@ -594,24 +609,27 @@ int timeNdu(uint32_t log2R, uint32_t alpha, uint32_t mA, uint32_t beta, uint32_t
   AlgScan<pRS_t> scR(&pRS, &R);
   using clk = std::chrono::steady_clock;
   std::chrono::nanoseconds tb{0}, tp{0};
-  for (int r = 0; r < reps; ++r) {
-    if (r) {
-      bS.clear_ht();
-      bT.clear_ht();
-    }
-    const auto t0 = clk::now();
-    scS.run(&gs);
-    scT.run(&gs);
-    const auto t1 = clk::now();
-    scR.run(&gs);
-    const auto t2 = clk::now();
-    tb += t1 - t0;
-    tp += t2 - t1;
-  }
-  std::printf("{\"plan\":\"Ndu\",\"cardR\":%zu,\"cardS\":%zu,\"nb\":%zu,\"reps\":%d,\"build_ns\":%.1f,"
+  const size_t n = df::infra::repeat_mintime(
+      std::chrono::milliseconds(300),
+      [&]() {
+        const auto t0 = clk::now();
+        scS.run(&gs);
+        scT.run(&gs);
+        const auto t1 = clk::now();
+        scR.run(&gs);
+        const auto t2 = clk::now();
+        tb += t1 - t0;
+        tp += t2 - t1;
+      },
+      [&]() {
+        bS.clear_ht();
+        bT.clear_ht();
+      },
+      false, size_t(reps > 0 ? reps : 1)).second;
+  std::printf("{\"plan\":\"Ndu\",\"cardR\":%zu,\"cardS\":%zu,\"nb\":%zu,\"reps\":%zu,\"build_ns\":%.1f,"
               "\"probe_ns\":%.1f,\"c_probe_rs\":%" PRIu64 ",\"c_probe_rt\":%" PRIu64 ",\"c_unnest_1\":%" PRIu64
               ",\"c_unnest_2\":%" PRIu64 ",\"c_top\":%" PRIu64 "}\n",
-              cardR, cardFk, nb, reps, double(tb.count()) / reps, double(tp.count()) / reps, pRS.count(),
+              cardR, cardFk, nb, n, double(tb.count()) / n, double(tp.count()) / n, pRS.count(),
               pRT.count(), un1.count(), un2.count(), top.count());
   return 0;
 }
@@ -623,7 +641,8 @@ int main(int argc, char** argv) {
   if (argc >= 8 && std::strcmp(argv[1], "exp1") == 0) {
     const bool dump = argc >= 9 && std::strcmp(argv[8], "dump") == 0;
     return e1::run(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]) != 0, std::atof(argv[5]),
-                   static_cast<uint32_t>(std::atoi(argv[6])), static_cast<uint32_t>(std::atoi(argv[7])), dump);
+                   static_cast<uint32_t>(std::atoi(argv[6])), static_cast<uint32_t>(std::atoi(argv[7])), dump,
+                   argc >= 10 ? std::string(argv[9]) : std::string());
   }
   if (argc >= 7 && std::strcmp(argv[1], "exp4") == 0) {
     const bool dump = argc >= 8 && std::strcmp(argv[7], "dump") == 0;
@@ -631,12 +650,13 @@ int main(int argc, char** argv) {
                    std::atoi(argv[6]), dump);
   }
   if (argc >= 5 && std::strcmp(argv[1], "time_csr") == 0)
-    return e1::timeCsr(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]));
+    return e1::timeCsr(std::stoull(argv[2]), std::stoull(argv[3]), std::atoi(argv[4]),
+                       argc >= 6 ? std::stoull(argv[5]) : 0);
   if (argc >= 8 && std::strcmp(argv[1], "time_ndu") == 0)
     return e4::timeNdu(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]),
                        std::atoi(argv[6]), std::atoi(argv[7]));
   if (argc >= 6 && std::strcmp(argv[1], "time_nrs") == 0)
     return e1::timeNrs(std::stoull(argv[2]), std::stoull(argv[3]), std::atof(argv[4]), std::atoi(argv[5]));
-  std::fprintf(stderr, "usage: ref_golden exp1 nR nS skew theta t b [dump] | exp4 log2R a A b B [dump]\n");
+  std::fprintf(stderr, "usage: ref_golden exp1 nR nS skew theta t b [dump|nodump [plan,plan...]] | exp4 log2R a A b B [dump]\n");
   return 2;
 }

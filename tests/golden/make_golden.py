@@ -7,7 +7,8 @@ and writes one JSON file per config. Only data (inputs' checksums / small input
 columns and the reference's counters, statistics and output checksums) is
 committed — never reference source.
 
-Usage: python tests/golden/make_golden.py   (needs /root/reference; runs ~1 min)
+Usage: python tests/golden/make_golden.py [name ...]   (needs /root/reference; ~15 min in all,
+most of it the two 1e7/1e8 headline configs; names restrict the run)
 """
 import json
 import os
@@ -32,19 +33,28 @@ EXP1 = [
     ("exp1_R1_S7_uni", [1, 7, 0, 1.0, 0, 1, "dump"]),                # single key, every probe collides
     ("exp1_R5_S3_uni_b4", [5, 3, 0, 1.0, 0, 4, "dump"]),             # NB = max(5/4, 1) = 1
     ("exp1_R1048576_S8388608_uni", [1048576, 8388608, 0, 1.0, 0, 1]),  # App. A -R 20 -S 23
+    # the headline configs at their exact sizes (BASELINE configs B and C; ~7 min each)
+    ("exp1_R10000000_S100000000_uni", [10000000, 100000000, 0, 1.0, 0, 1]),
+    ("exp1_R10000000_S100000000_zipf08", [10000000, 100000000, 1, 0.8, 0, 1]),
+    # config D (|R| = 1e8, |S| = 1e9; the Csr plan only: ~12 min, ~30 GB of host memory)
+    ("exp1_R100000000_S1000000000_uni", [100000000, 1000000000, 0, 1.0, 0, 1, "nodump", "Csr"]),
 ]
 EXP4 = [
     ("exp4_R3_a2_A2_b2_B1", [3, 2, 2, 2, 1, "dump"]),   # App. A print-relations case
     ("exp4_R10_a3_A2_b2_B3", [10, 3, 2, 2, 3, "dump"]),
     ("exp4_R16_a3_A4_b2_B2", [16, 3, 4, 2, 2]),
     ("exp4_R18_a1_A3_b3_B5", [18, 1, 3, 3, 5]),
+    ("exp4_R22_a3_A4_b2_B2", [22, 3, 4, 2, 2]),  # config E (SURVEY App. A -R 22 -a 3 -A 4 -b 2 -B 2)
 ]
 
 
 def main():
     if not os.path.exists(BIN):
         sys.exit(f"{BIN} missing: run `make -C oracle ref` first (needs /root/reference)")
+    only = set(sys.argv[1:])
     for name, args in [(n, ["exp1"] + a) for n, a in EXP1] + [(n, ["exp4"] + a) for n, a in EXP4]:
+        if only and name not in only:
+            continue
         out = subprocess.run([BIN] + [str(a) for a in args], check=True, capture_output=True, text=True).stdout
         d = json.loads(out)
         d["generator_args"] = args

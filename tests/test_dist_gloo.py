@@ -2,7 +2,8 @@
 
 Each rank holds a contiguous slice of R and S (global row ids), partitions it by bucket range
 exactly as hj3d_partition does (owner = bucket * P / NB, stable; restated here in numpy),
-exchanges (key, row) pairs with hj3d.dist.exchange (all_to_all), and joins its received pairs
+exchanges (key, row) pairs with hj3d.dist.exchange (all_to_all; the probe side in chunks through
+exchange_counts + exchange_pairs_async as bench.py does), and joins its received pairs
 with the oracle over the full bucket space (only its own buckets are populated). The per-rank
 counters, all-reduced with hj3d.dist, must equal the single-table oracle on the whole relations:
 join cardinality, c_htProbeCmp, unnest counts, output checksums and the table statistics.
@@ -92,11 +93,25 @@ def _worker(rank, port, case, q):
                 return keys[lo:hi], np.arange(lo, hi, dtype=np.uint32)
 
             recv = []
-            for keys in (bkeys, pkeys):
-                k, r = local(keys)
-                pairs, counts = partition(k, r, nb, WORLD)
-                got = hdist.exchange(torch.from_numpy(pairs.view(np.int32)), torch.from_numpy(counts))
-                recv.append(got.numpy().view(np.uint32))
+            k, r = local(bkeys)
+            pairs, counts = partition(k, r, nb, WORLD)
+            got = hdist.exchange(torch.from_numpy(pairs.view(np.int32)), torch.from_numpy(counts))
+            recv.append(got.numpy().view(np.uint32))
+            # the probe side as bench.py ships it: 3 chunks partitioned separately, all chunks'
+            # counts in one collective, then one pair all-to-all per chunk into one receive buffer
+            k, r = local(pkeys)
+            cb = [len(k) * c // 3 for c in range(4)]
+            parts = [partition(k[cb[c]:cb[c + 1]], r[cb[c]:cb[c + 1]], nb, WORLD) for c in range(3)]
+            sc, rc = hdist.exchange_counts(torch.from_numpy(np.stack([pc for _, pc in parts])))
+            assert sc == [pc.tolist() for _, pc in parts]
+            rbuf = torch.empty((sum(map(sum, rc)), 2), dtype=torch.int32)
+            off = 0
+            for c in range(3):
+                got, work = hdist.exchange_pairs_async(torch.from_numpy(parts[c][0].view(np.int32)), sc[c], rc[c],
+                                                       rbuf[off:])
+                assert work is None or work.wait()
+                off += got.shape[0]
+            recv.append(rbuf.numpy().view(np.uint32))
             # the owned bucket range agrees with hj3d_part_range
             lo, hi = hj3d.part_range(nb, WORLD, rank)
             bk = murmur32(recv[0][:, 0]).astype(np.uint64) % np.uint64(nb)
@@ -113,7 +128,10 @@ def _worker(rank, port, case, q):
             tot = hdist.allreduce_sum_u64(sums, "cpu")
             x = hdist.allreduce_xor_u64(e.out["xor_h"], "cpu")
             mx = hdist.allreduce_max(float(st["cc0_max"]), "cpu")
-            out[plan] = (tot, x, int(mx))
+            # the statistics of this rank's shard (its owned bucket range), reduced as bench.py does
+            shard = dict(st, nb=owned, empty=st["empty"] - (nb - owned), cc0_cnt=owned, cc0_min=0)
+            red = hdist.allreduce_stats(shard, "cpu")
+            out[plan] = (tot, x, int(mx), red)
         q.put((rank, out))
     finally:
         dist.destroy_process_group()
@@ -141,10 +159,13 @@ def test_bucket_range_exchange_world2(case):
     exp = {"Csr": O.chain_plan(R, 0, S, 1, nR, True), "Nsr": O.nested_plan(R, 0, S, 1, nR, True),
            "Crs": O.chain_plan(S, 1, R, 0, dv, False), "Nrs": O.nested_plan(S, 1, R, 0, dv, True)}
     for plan, e in exp.items():
-        tot, x, mx = res[0][plan]
+        tot, x, mx, red = res[0][plan]
         assert res[1][plan] == res[0][plan]  # every rank sees the same reduced values
         st = e.stats
         want = [e.c_probe, e.c_cmp, e.c_unnest, e.c_top, e.out["n"], e.out["sum_a"], e.out["sum_b"], e.out["sum_h"],
                 st["empty"], st["entries"], st["distinct"], st["cc0_sum"], st["cc1_sum"], st["cc1_cnt"]]
         assert tot == [v & ((1 << 64) - 1) for v in want], plan
         assert x == e.out["xor_h"] and mx == st["cc0_max"], plan
+        for k in ("nb", "empty", "entries", "distinct", "cc0_sum", "cc0_cnt", "cc1_sum", "cc1_cnt", "cc0_max",
+                  "cc1_max", "cc1_min"):
+            assert red[k] == st[k], (plan, k, red[k], st[k])

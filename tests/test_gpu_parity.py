@@ -13,8 +13,8 @@ from conftest import load_golden
 
 pytestmark = pytest.mark.gpu
 
-EXP1 = load_golden("exp1_*.json")
-EXP4 = load_golden("exp4_*.json")
+EXP1 = load_golden("exp1_*.json", headline=False)  # the headline sizes: test_gpu_headline.py
+EXP4 = load_golden("exp4_*.json", headline=False)
 STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
              "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
 PLANS = ("Csr", "CsrUU", "Crs", "Nsr", "Nrs", "NrsNU")

@@ -12,7 +12,7 @@ import pytest
 import oracle as O
 from conftest import load_golden
 
-EXP1 = load_golden("exp1_*.json")
+EXP1 = [x for x in load_golden("exp1_*.json") if x[1]["nS"] <= 100_000_000]  # config D: GPU box only
 EXP4 = load_golden("exp4_*.json")
 STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
              "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
@@ -121,7 +121,13 @@ def test_reference_cpu_baseline_timer_counts():
     exp = O.chain_plan(O.tuples3(Rk, np.zeros_like(Rk)), 0, O.tuples3(np.arange(20000, dtype=np.uint32), Sa), 1,
                        4096, True)
     assert (r["c_probe"], r["c_cmp"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_top)
-    assert r["reps"] == 2 and r["probe_ns"] > 0
+    assert r["reps"] >= 2 and r["probe_ns"] > 0  # repeat_mintime: >= min reps, doubled below 300 ms
+    # a probe prefix of the same relation: the counters of the first 5000 S tuples
+    r = json.loads(subprocess.run([exe, "time_csr", "4096", "20000", "8", "5000"], capture_output=True, text=True,
+                                  check=True).stdout)
+    exp = O.chain_plan(O.tuples3(Rk, np.zeros_like(Rk)), 0, O.tuples3(np.arange(5000, dtype=np.uint32), Sa[:5000]), 1,
+                       4096, True)
+    assert (r["probe_prefix"], r["c_probe"], r["c_cmp"]) == (5000, exp.c_probe, exp.c_cmp) and r["reps"] >= 8
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")),
@@ -141,7 +147,7 @@ def test_reference_cpu_baseline_nrs_timer_counts():
     exp = O.nested_plan(S, 1, R, 0, dv, True)
     assert r["nb"] == dv
     assert (r["c_probe"], r["c_cmp"], r["c_unnest"], r["c_top"]) == (exp.c_probe, exp.c_cmp, exp.c_unnest, exp.c_top)
-    assert r["reps"] == 2 and r["probe_ns"] > 0
+    assert r["reps"] >= 2 and r["probe_ns"] > 0  # repeat_mintime: >= min reps, doubled below 300 ms
 
 
 @pytest.mark.skipif(not os.path.exists(os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "ref_golden.out")),
