@@ -106,6 +106,7 @@ void hj3d_ctx_destroy(hj3d_ctx* ctx) {
   for (auto& b : ctx->scratch) b.release();
   ctx->res.release();
   ctx->misc.release();
+  ctx->ctl.release();
   for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -139,6 +140,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_NESTED_RADIX: ctx->nested_radix = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_SORT: ctx->nested_sort = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SEL_UNFUSED: ctx->sel_unfused = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_PACKED_PROBE: ctx->pk_off = value == 0; return HJ3D_OK;
     default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
   }
 }
@@ -337,6 +339,13 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   PhaseTimer tm(ctx, HJ3D_T_PROBE);
   uint64_t* res = ctx->res.as<uint64_t>();
   const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
+  if (pk_probe_applicable(ctx, t, probe->n, flags)) {  // the packed unique probe sets res itself
+    hipError_t e = pk_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    if (e != hipErrorNotSupported) {
+      note_probe(ctx, t, probe->n, flags, out_cap);
+      return from_hip(ctx, e, "hj3d_probe");
+    }
+  }
   hipError_t e = acc ? hipSuccess : hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) e = out_mark(ctx, t, flags);
   if (e == hipSuccess) {
@@ -367,6 +376,15 @@ hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* p
     return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: UNNEST needs a nested table");
   const bool chain_radix = t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n);
   const bool nested_radix = t->desc.kind == HJ3D_NESTED && radix_nested_applicable(ctx, t, probe->n);
+  if (!ctx->sel_unfused && pk_probe_applicable(ctx, t, probe->n, flags)) {
+    PhaseTimer tm(ctx, HJ3D_T_PROBE);
+    const SelArgs a = sel_args(preds, npred);
+    hipError_t e = pk_probe(ctx, t, *probe, flags, out_dev, out_cap, ctx->res.as<uint64_t>(), ctx->stream, &a);
+    if (e != hipErrorNotSupported) {
+      note_probe(ctx, t, probe->n, flags, out_cap);
+      return from_hip(ctx, e, "hj3d_probe_sel");
+    }
+  }
   if (!(flags & HJ3D_PROBE_ACCUMULATE) && !ctx->sel_unfused && (chain_radix || nested_radix)) {
     // the selection fused into the probe-side partitioner
     PhaseTimer tm(ctx, HJ3D_T_PROBE);

@@ -1,0 +1,787 @@
+// chain_pk.hip — the unique chaining probe on PACKED pairs: the config-B hot path
+// (AlgHashJoinProbe<..., IsBuildKeyUnique = true>::step, algebra.hh:625-659, over a whole scanned
+// relation). Two launches per probe strand, nothing else on the stream:
+//
+//   k_pk_part   one persistent 1024-thread workgroup per CU streams the probe relation once:
+//               hash (murmur3 fmix32), bucket b = h % NB and the slice p of b (slices of W
+//               buckets, sized so that a slice of the table fits LDS), and writes the pair
+//               {v, row} with v = (b - p*W) << qbits | h / NB to the workgroup's region of slice p.
+//               The bucket and the quotient determine h (h = (h / NB) * NB + b), so the probe needs
+//               neither a modulo nor a division per tuple. Regions are written in whole 128-B
+//               segments (runs shorter than a segment ride in registers to the next tile).
+//   k_pk_probe  one 1024-thread workgroup per slice (or share of its regions): stages the slice
+//               (directory + entries, entry hashes turned into quotients) in LDS, reserves its
+//               output range with one atomic, probes every pair against LDS in the reference's
+//               walk order with the unique early exit, writes {row, partner} densely; then the
+//               pairs that overflowed a region (skewed probe keys) are taken in chunks by whichever
+//               workgroups finish first, against the table in HBM; the last workgroup to finish
+//               folds every workgroup's counters into the result slot and resets the control words.
+// The control words (overflow count, output cursor, ticket, ...) are zero between probes: the last
+// workgroup of k_pk_probe restores them, so no fill runs on the stream.
+// Counters are those of radix.hip's probe: c_htProbeCmp from the sorted-bucket walk
+// [index 0, n-1, ..., 1] with early exit (buckets <= 32 entries), the order-free form beyond.
+#include <cmath>
+
+#include "radix_seg.hpp"
+
+namespace hj3d {
+namespace {
+
+constexpr int kPkBlock = 1024;
+// build-time tunables (A/B variants, scripts/gpu_variant_sweep.sh)
+#ifndef HJ3D_PK_ROUNDS
+#define HJ3D_PK_ROUNDS 8  // tuples per thread and tile: 8192-tuple tiles
+#endif
+#ifndef HJ3D_PK_AHEAD
+#define HJ3D_PK_AHEAD 1   // tiles of keys in flight: 1 (loaded after the stage is built) or 2
+#endif
+#ifndef HJ3D_PK_FLAT
+#define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (else only short ones)
+#endif
+#ifndef HJ3D_PK_SINK
+#define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
+#endif
+#ifndef HJ3D_PK_GUARD
+#define HJ3D_PK_GUARD 1   // partition: key loads and rank atomics guarded per tuple (else clamped, unconditional)
+#endif
+constexpr int kPkRounds = HJ3D_PK_ROUNDS;
+constexpr int kPkTile = kPkBlock * kPkRounds;
+static_assert((kPkTile & (kPkTile - 1)) == 0, "tile must be a power of two");
+constexpr int kPkTBits = __builtin_ctz(kPkTile);
+constexpr uint32_t kPkSeg = 16;                // 128-B region segments
+// tile + carried pairs (< 16 per slice, ~7.5 on average): 14336 pairs at 4096-tuple tiles
+constexpr uint32_t kPkStage = kPkTile + 10240 > 17408 ? 17408 : kPkTile + 10240;
+constexpr uint32_t kSortedMaxPk = 32;
+constexpr uint32_t kOvfFlag = 0x80000000u;
+
+// control words (u64) of one probe strand
+enum { kCtlNovf = 0, kCtlOut = 1, kCtlTicket = 2, kCtlOvfCursor = 3, kCtlNprobe = 4, kCtlWords = 8 };
+
+struct PkGeom {
+  FastDiv32 dnb, dw;  // / NB, / W
+  uint32_t nb, lo, nbl, W, P, qbits, qmask;
+  // hash of a packed pair in slice p
+  __device__ __forceinline__ uint32_t hash_of(uint32_t v, uint32_t p) const {
+    return (v & qmask) * nb + lo + p * W + (v >> qbits);
+  }
+};
+
+// Wave-aggregated append to the overflow list: pairs {h, row} (counted in ctl[kCtlNovf]).
+__device__ __forceinline__ void pk_ovf_append(bool me, uint2 e, uint2* __restrict__ ovf, uint64_t* ctl) {
+  const uint64_t m = __ballot(me);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  uint64_t b = 0;
+  if (lane == leader) b = atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlNovf), (unsigned long long)__popcll(m));
+  b = __shfl(b, leader, kWave);
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if (me) ovf[b + __popcll(m & lt)] = e;
+}
+
+// ---- k_pk_part: the probe relation -> packed pairs in per-(workgroup, slice) regions ----
+// Regions: region[(g * P + p) * cap + k], counts[g * P + p] pairs. One slice per thread (P <= 1024):
+// thread p carries slice p's < 16 leftover pairs in registers. SEL: a one-word selection fused in.
+// Memory ordering: vmcnt counts loads and stores together, in issue order, so a load can only be
+// waited for together with every older store. The keys of tile t+2 are therefore loaded (always,
+// clamped at the end: a fixed number of loads) right after tile t's stage is built, two tiles ahead:
+// waiting for tile t+1's keys then waits for tile t-1's region stores, never for tile t's.
+template <bool IMPLICIT, bool SEL>
+__global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint32_t ntiles, uint32_t cap,
+                                                      uint2* __restrict__ region, uint32_t* __restrict__ counts,
+                                                      uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
+                                                      SelRange sel) {
+  __shared__ uint2 stage[kPkStage];
+  __shared__ uint32_t loc[kPkBlock];
+  __shared__ uint32_t sbase[kPkBlock];
+  __shared__ uint2 seginfo[kPkStage / kPkSeg];  // whole segment: {region index | kOvfFlag + slice, stage start}
+  __shared__ uint32_t wsum[kPkBlock / kWave];
+  const uint32_t me = threadIdx.x, P = pk.P, n = uint32_t(r.n);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint32_t my_reg = (blockIdx.x * P + me) * cap;  // region of slice `me` (host: G * P * cap < 2^31)
+  uint2 creg[kPkSeg - 1];
+  uint32_t my_kc = 0, my_cur = 0;
+#pragma unroll
+  for (int j = 0; j < int(kPkSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
+  uint32_t ha[kPkRounds], hb[kPkRounds], pa[SEL ? kPkRounds : 1], pb[SEL ? kPkRounds : 1];
+  // a wave-uniform 64-bit tile pointer + 32-bit lane offsets (the loads take the scalar-base form)
+  auto load = [&](uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1], uint32_t tile) __attribute__((always_inline)) {
+    if constexpr (HJ3D_PK_GUARD) {
+      const uint32_t base = tile * kPkTile;
+#pragma unroll
+      for (int j = 0; j < kPkRounds; ++j) {
+        const uint32_t i = base + uint32_t(j) * kPkBlock + me;
+        const char* t = r.base + uint64_t(i) * r.stride;
+        h[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + r.key_off) : 0u;
+        if constexpr (SEL) pw[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + sel.word_off) : 0u;
+      }
+    } else {
+      const uint32_t base = min(tile * kPkTile, n - 1), lim = n - 1 - base;
+      const char* tp = r.base + uint64_t(base) * r.stride;
+#pragma unroll
+      for (int j = 0; j < kPkRounds; ++j) {
+        const uint32_t o = min(uint32_t(j) * kPkBlock + me, lim) * r.stride;  // unconditional: clamped
+        h[j] = *reinterpret_cast<const uint32_t*>(tp + o + r.key_off);
+        if constexpr (SEL) pw[j] = *reinterpret_cast<const uint32_t*>(tp + o + sel.word_off);
+      }
+    }
+  };
+  auto to_ovf = [&](uint2 e, uint32_t p, bool me_) __attribute__((always_inline)) {  // packed pair of slice p -> {h, row}
+    pk_ovf_append(me_, make_uint2(pk.hash_of(e.x, p), e.y), ovf, ctl);
+  };
+  auto flush_carry = [&]() __attribute__((always_inline)) {  // partial segment at the cursor
+#pragma unroll
+    for (int j = 0; j < int(kPkSeg) - 1; ++j) {
+      const bool v = me < P && uint32_t(j) < my_kc;
+      const uint32_t o = my_cur + j;
+      if (v && o < cap) region[my_reg + o] = creg[j];
+      to_ovf(creg[j], me, v && o >= cap);
+    }
+    my_cur += my_kc;
+    my_kc = 0;
+  };
+  // exclusive scan of one value per thread (one slice per thread)
+  auto scan = [&](uint32_t v, uint32_t* total) __attribute__((always_inline)) {
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t y = __shfl_up(x, o, kWave);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kPkBlock / kWave; ++w) {
+      const uint32_t t = wsum[w];
+      if (w < wid) pre += t;
+      tot += t;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+  };
+  uint32_t npassed = 0;
+  auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1]) __attribute__((always_inline)) {
+    loc[me] = 0;
+    const uint32_t base = tile * kPkTile;
+    uint32_t rk[kPkRounds];
+    __syncthreads();
+    // hash, bucket, slice, rank: the LDS atomics are unconditional (invalid tuples add 0 to slot 0)
+#pragma unroll
+    for (int j = 0; j < kPkRounds; ++j) {
+      const uint32_t i = base + uint32_t(j) * kPkBlock + me;
+      const uint32_t hv = murmur32(h[j]);
+      const uint32_t q = pk.dnb.div(hv);
+      const uint32_t bl = hv - q * pk.nb - pk.lo;
+      bool pass = i < n;
+      if constexpr (SEL) {
+        pass = pass && sel.test(pw[j]);
+        npassed += pass;
+      }
+      const bool ok = pass && bl < pk.nbl;
+      if constexpr (HJ3D_PK_GUARD) {
+        rk[j] = kInvalid;
+        if (ok) {
+          const uint32_t p = pk.dw.div(bl);
+          h[j] = ((bl - p * pk.W) << pk.qbits) | q;  // the packed pair's first word
+          rk[j] = (p << kPkTBits) | atomicAdd(&loc[p], 1u);
+        }
+      } else {
+        const uint32_t p = ok ? pk.dw.div(bl) : 0u;
+        h[j] = ((bl - p * pk.W) << pk.qbits) | q;
+        const uint32_t rank = atomicAdd(&loc[p], ok ? 1u : 0u);
+        rk[j] = ok ? (p << kPkTBits) | rank : kInvalid;
+      }
+    }
+    __syncthreads();
+    const uint32_t my_c = me < P ? loc[me] : 0u;
+    const auto seg_counts = [&]() __attribute__((always_inline)) {
+      const uint32_t L = my_kc + my_c;
+      return (L << 16) | (L / kPkSeg);
+    };
+    uint32_t tot;
+    uint32_t pre = scan(seg_counts(), &tot);
+    if ((tot >> 16) > kPkStage) {  // too many carried pairs: write them out; the tile alone fits
+      flush_carry();
+      pre = scan(seg_counts(), &tot);
+    }
+    const uint32_t my_loc = pre >> 16, my_fseg = pre & 0xFFFFu, nfull = tot & 0xFFFFu;
+    const uint32_t my_len = my_kc + my_c;
+    if (me < P) {
+      sbase[me] = my_loc + my_kc;
+#pragma unroll
+      for (int j = 0; j < int(kPkSeg) - 1; ++j)
+        if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
+      for (uint32_t sg = 0; sg < my_len / kPkSeg; ++sg) {
+        const uint32_t o = my_cur + sg * kPkSeg;  // segment-aligned; cap is a multiple of kPkSeg
+        seginfo[my_fseg + sg] = make_uint2(o < cap ? my_reg + o : (kOvfFlag | me), my_loc + sg * kPkSeg);
+      }
+    }
+    __syncthreads();
+    const uint32_t rb = IMPLICIT ? uint32_t(r.row_base) + base : 0u;
+#pragma unroll
+    for (int j = 0; j < kPkRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint32_t li = uint32_t(j) * kPkBlock + me;
+      const uint32_t row = IMPLICIT ? rb + li : r.row(uint64_t(base) + li);
+      stage[sbase[rk[j] >> kPkTBits] + (rk[j] & (kPkTile - 1))] = make_uint2(h[j], row);
+    }
+    load(h, pw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
+    __syncthreads();
+    // whole segments: kPkSeg consecutive lanes store one 128-B segment
+    for (uint32_t kk = me; kk < nfull * kPkSeg; kk += kPkBlock) {
+      const uint2 si = seginfo[kk / kPkSeg];
+      const uint32_t j = kk % kPkSeg;
+      const uint2 e = stage[si.y + j];
+      const bool spill = si.x & kOvfFlag;
+      if (!spill) region[si.x + j] = e;
+      to_ovf(e, si.x & ~kOvfFlag, spill);
+    }
+    // the run's tail (< one segment) becomes the slice's carry
+    if (me < P) {
+      const uint32_t F = my_len - my_len % kPkSeg;
+#pragma unroll
+      for (int j = 0; j < int(kPkSeg) - 1; ++j)
+        if (uint32_t(j) < my_len - F) creg[j] = stage[my_loc + F + j];
+      my_cur += F;
+      my_kc = my_len - F;
+    }
+    __syncthreads();
+  };
+  load(ha, pa, blockIdx.x);
+  if constexpr (HJ3D_PK_AHEAD == 2) {
+    load(hb, pb, blockIdx.x + gridDim.x);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += 2 * gridDim.x) {
+      process(tile, ha, pa);
+      if (tile + gridDim.x < ntiles) process(tile + gridDim.x, hb, pb);
+    }
+  } else {
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa);
+  }
+  flush_carry();
+  if (me < P) counts[blockIdx.x * P + me] = min(my_cur, cap);
+  // n_probe: every scanned tuple (the reference's probe count), or the selection's passing tuples
+  if constexpr (SEL) {
+    uint32_t c = npassed;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+    if (lane == 0 && c) atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlNprobe), (unsigned long long)c);
+  } else {
+    if (blockIdx.x == 0 && me == 0) atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlNprobe), (unsigned long long)n);
+  }
+}
+
+// ---- k_pk_probe ----
+constexpr uint32_t kLdsWords = kProbeLdsWords;
+constexpr int kItems = 8;  // pairs per lane and chunk (the next chunk in flight)
+constexpr int kGroup = 4;  // items whose LDS lookups are batched
+
+// Unique probe of one lane's items against the LDS slice: directory word (start << 16 | count),
+// entries {q, row} sorted by row inside buckets of <= 32. Walk position c = 0, 1, 2 (sorted index
+// 0, n-1, n-2) batched over kGroup items, the rest per item.
+template <int MODE, bool CK>
+__device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[kItems], uint32_t valid, uint64_t slot0,
+                                               const uint32_t* ldir, const uint2* lent, const PkGeom& pk,
+                                               uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
+                                               uint64_t out_cap, uint2* __restrict__ sink) {
+  uint32_t nm = 0, sc = 0, nv = 0;
+#pragma unroll
+  for (int g = 0; g < kItems; g += kGroup) {
+    uint32_t d[kGroup], match[kGroup], cmps[kGroup], q[kGroup];
+    bool live[kGroup];
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const bool ok = (valid >> (g + j)) & 1u;
+      const uint32_t x = uint32_t(v[g + j]);
+      q[j] = x & pk.qmask;
+      const uint32_t w = ldir[ok ? x >> pk.qbits : 0u];
+      d[j] = ok ? w : 0u;
+      match[j] = kInvalid;
+      cmps[j] = d[j] & 0xFFFFu;
+      live[j] = cmps[j] != 0 && cmps[j] <= kSortedMaxPk;
+    }
+#pragma unroll
+    for (uint32_t c = 0; c < 3; ++c) {
+#pragma unroll
+      for (int j = 0; j < kGroup; ++j) {
+        const uint32_t nn = d[j] & 0xFFFFu;
+        const bool ok = live[j] && c < nn;
+        const uint2 e = lent[ok ? (d[j] >> 16) + (c == 0 ? 0u : nn - c) : 0u];
+        const bool hit = ok && e.x == q[j];
+        match[j] = hit ? e.y : match[j];
+        cmps[j] = hit ? c + 1 : cmps[j];
+        live[j] = live[j] && !hit;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const uint32_t nn = d[j] & 0xFFFFu, s = d[j] >> 16;
+      if (live[j] && nn > 3) {
+        for (uint32_t c = 3; c < nn; ++c) {
+          const uint2 e = lent[s + nn - c];
+          if (e.x == q[j]) {
+            cmps[j] = c + 1;
+            match[j] = e.y;
+            break;
+          }
+        }
+      } else if (nn > kSortedMaxPk) {  // long bucket in arrival order: order-free form
+        uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, cnt = 0;
+        for (uint32_t k = s; k < s + nn; ++k) {
+          const uint2 e = lent[k];
+          minrow = min(minrow, e.y);
+          if (e.x == q[j]) {
+            ++cnt;
+            lo_m = min(lo_m, e.y);
+            hi_m = max(hi_m, e.y);
+          }
+        }
+        if (cnt != 0 && lo_m == minrow) {
+          cmps[j] = 1;
+          match[j] = lo_m;
+        } else if (cnt != 0) {
+          uint32_t gt = 0;
+          for (uint32_t k = s; k < s + nn; ++k) gt += lent[k].y > hi_m;
+          cmps[j] = 2 + gt;
+          match[j] = hi_m;
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kGroup; ++j) {
+      const bool ok = (valid >> (g + j)) & 1u;
+      const uint32_t row = uint32_t(v[g + j] >> 32);
+      const bool m = match[j] != kInvalid;
+      nv += ok;
+      nm += m;
+      sc += cmps[j];
+      if (MODE == 1) {
+        const uint64_t slot = slot0 + uint32_t((g + j) * 64);
+        if (HJ3D_PK_SINK) {  // every lane stores (absent items to the sink): a fixed number of stores per chunk
+          uint2* dst = (ok && slot < out_cap) ? out + slot : sink + (threadIdx.x & 63);
+          __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(dst));
+        } else if (ok && slot < out_cap) {
+          __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(out + slot));
+        }
+      }
+      if (CK && m) {
+        acc[4] += row;
+        acc[5] += match[j];
+        const uint64_t ph = pair_hash(row, match[j]);
+        acc[7] += ph;
+        acc[8] ^= ph;
+      }
+    }
+  }
+  acc[1] += nm;
+  acc[2] += nm;
+  acc[3] += sc;
+  (void)nv;
+}
+
+// The same unique probe of one {h, row} pair against buckets in HBM (off / ent, entries {h, row}):
+// slices that do not fit LDS (heavy skew) and the overflow pairs.
+template <int MODE, bool CK>
+__device__ __forceinline__ void pk_probe_hbm(uint32_t h, uint32_t row, uint32_t s, uint32_t nn,
+                                             const uint2* __restrict__ ent, uint64_t slot,
+                                             uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
+                                             uint64_t out_cap) {
+  uint32_t match = kInvalid, cmps = nn;
+  if (nn <= kSortedMaxPk) {
+    for (uint32_t c = 0; c < nn; ++c) {
+      const uint2 e = ent[s + (c == 0 ? 0u : nn - c)];
+      if (e.x == h) {
+        cmps = c + 1;
+        match = e.y;
+        break;
+      }
+    }
+  } else {
+    uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, cnt = 0;
+    for (uint32_t k = s; k < s + nn; ++k) {
+      const uint2 e = ent[k];
+      minrow = min(minrow, e.y);
+      if (e.x == h) {
+        ++cnt;
+        lo_m = min(lo_m, e.y);
+        hi_m = max(hi_m, e.y);
+      }
+    }
+    if (cnt != 0 && lo_m == minrow) {
+      cmps = 1;
+      match = lo_m;
+    } else if (cnt != 0) {
+      uint32_t gt = 0;
+      for (uint32_t k = s; k < s + nn; ++k) gt += ent[k].y > hi_m;
+      cmps = 2 + gt;
+      match = hi_m;
+    }
+  }
+  acc[3] += cmps;
+  if (match != kInvalid) {
+    acc[1] += 1;
+    acc[2] += 1;
+    if (CK) {
+      acc[4] += row;
+      acc[5] += match;
+      const uint64_t ph = pair_hash(row, match);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+  }
+  if (MODE == 1 && slot < out_cap)
+    __builtin_nontemporal_store((uint64_t(match) << 32) | row, reinterpret_cast<uint64_t*>(out + slot));
+}
+
+// Slice of buckets [b0, b0 + nbs) into LDS: directory words (start - e0) << 16 | count, then the
+// entries with their hash replaced by the quotient h / NB (the bucket is implied by the slot).
+// All loads of a round batch are issued before the first LDS write.
+__device__ __forceinline__ void pk_stage(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
+                                         uint32_t nbs, uint32_t e0, uint32_t ne, const FastDiv32& dnb, uint32_t* ldir,
+                                         uint2* lent) {
+  constexpr int kStage = 12;
+  const uint32_t nmax = max(nbs, ne);
+  for (uint32_t k0 = threadIdx.x; k0 < nmax; k0 += kPkBlock * kStage) {
+    uint32_t a[kStage], b[kStage];
+    uint2 x[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kPkBlock;
+      a[u] = k < nbs ? off[b0 + k] : 0u;
+      b[u] = k < nbs ? off[b0 + k + 1] : 0u;
+      x[u] = k < ne ? ent[e0 + k] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * kPkBlock;
+      if (k < nbs) ldir[k] = ((a[u] - e0) << 16) | (b[u] - a[u]);
+      if (k < ne) lent[k] = make_uint2(dnb.div(x[u].x), x[u].y);
+    }
+  }
+}
+
+template <int MODE, bool CK>
+__global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__ region,
+                                                       const uint32_t* __restrict__ counts, uint32_t G, uint32_t cap,
+                                                       uint32_t splits, bool flat, const uint32_t* __restrict__ off,
+                                                       const uint2* __restrict__ ent, PkGeom pk, FastMod fm,
+                                                       uint2* __restrict__ out, uint64_t out_cap,
+                                                       const uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
+                                                       uint64_t* __restrict__ partials, uint64_t* __restrict__ res,
+                                                       int accumulate, uint2* __restrict__ sink) {
+  __shared__ uint32_t lds[kLdsWords];
+  __shared__ uint32_t wtot[kPkBlock / kWave];
+  __shared__ uint64_t bbase;
+  __shared__ uint64_t red[kPkBlock / kWave][kProbeFields];
+  __shared__ uint32_t flag;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  constexpr int kWaves = kPkBlock / kWave;
+  const uint32_t P = pk.P;
+  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  const uint32_t b0 = p * pk.W;
+  const uint32_t nbs = min(pk.W, pk.nbl - b0);
+  const uint32_t e0 = off[b0], e1 = off[b0 + nbs], ne = e1 - e0;
+  const bool fits = (nbs + 2) + 2ull * ne <= kLdsWords;
+  uint32_t* ldir = lds;
+  uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
+  uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+
+  // this block's regions: wave w takes g = g_lo + w + 16 k (lane k holds region k's count)
+  const uint32_t g_lo = uint32_t(uint64_t(G) * sp / splits), g_hi = uint32_t(uint64_t(G) * (sp + 1) / splits);
+  const uint32_t nr = g_hi > g_lo + wid ? (g_hi - g_lo - wid + kWaves - 1) / kWaves : 0u;  // <= 64
+  uint32_t my_len = 0;
+  if (uint32_t(lane) < nr) my_len = counts[(g_lo + wid + kWaves * lane) * P + p];
+  uint32_t wtotal;
+  const uint32_t my_pre = wave_excl_scan(my_len, &wtotal);  // wave-local stream offset of region `lane`
+  if (lane == 0) wtot[wid] = wtotal;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < kWaves; ++w) t += wtot[w];
+    bbase = (MODE == 1 && t) ? atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlOut), (unsigned long long)t) : 0ull;
+  }
+  uint32_t wpre = 0;
+  for (int w = 0; w < wid; ++w) wpre += wtot[w];
+  auto pre_at = [&](uint32_t k) __attribute__((always_inline)) { return uint32_t(__builtin_amdgcn_readlane(int(my_pre), int(k))); };
+  auto len_at = [&](uint32_t k) __attribute__((always_inline)) { return uint32_t(__builtin_amdgcn_readlane(int(my_len), int(k))); };
+  auto src_of = [&](uint32_t k) __attribute__((always_inline)) { return region + (g_lo + wid + kWaves * k) * P * cap + p * cap; };
+
+  // one chunk = kItems x 64 consecutive items of the wave's stream (flat: regions concatenated;
+  // otherwise a chunk stays inside one region). Loads and stores of the steady-state loops are
+  // unconditional (clamped addresses, absent items stored to the sink): with a fixed count per chunk
+  // the wait for the next chunk's pairs leaves this chunk's stores in flight.
+  uint32_t rb = 0;  // flat: last region starting at or before the block of 64
+  auto load_flat = [&](uint64_t (&v)[kItems], uint32_t f0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      // block start and item clamped into the stream (the last prefetch re-reads the last chunk)
+      const uint32_t b = min(f0 + j * 64, wtotal - 1), f = min(f0 + j * 64 + lane, wtotal - 1);
+      if (pre_at(rb) > b) rb = 0;
+      while (rb + 1 < nr && pre_at(rb + 1) <= b) ++rb;
+      uint32_t rr = rb, pr = pre_at(rb);
+      for (uint32_t t = rb + 1; t < nr; ++t) {  // region starts inside the block
+        const uint32_t pt = pre_at(t);
+        if (pt > b + 63) break;
+        if (pt <= f) {
+          rr = t;
+          pr = pt;
+        }
+      }
+      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src_of(rr) + (f - pr)));
+    }
+  };
+  // non-flat cursor: region r, offset qq
+  uint32_t r = 0, qq = 0, len = nr ? len_at(0) : 0u;
+  while (r < nr && len == 0) {
+    ++r;
+    len = r < nr ? len_at(r) : 0u;
+  }
+  auto load_reg = [&](uint64_t (&v)[kItems], uint32_t rr, uint32_t q0, uint32_t ll) __attribute__((always_inline)) {
+    const uint2* src = rr < nr ? src_of(rr) : region;
+    const uint32_t last = ll ? ll - 1 : 0u;
+#pragma unroll
+    for (int j = 0; j < kItems; ++j)
+      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + min(q0 + j * 64 + lane, last)));
+  };
+  auto probe_hbm_chunk = [&](const uint64_t (&v)[kItems], uint32_t valid, uint64_t slot0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kItems; ++j) {
+      if (!((valid >> j) & 1u)) continue;
+      const uint32_t x = uint32_t(v[j]), bl = b0 + (x >> pk.qbits);
+      const uint32_t s = off[bl];
+      pk_probe_hbm<MODE, CK>(pk.hash_of(x, p), uint32_t(v[j] >> 32), s, off[bl + 1] - s, ent, slot0 + j * 64, acc,
+                             out, out_cap);
+    }
+  };
+  // the walk: probe(v, valid mask, wave-local stream offset of the lane's item 0)
+  auto walk = [&](auto&& probe) __attribute__((always_inline)) {
+    constexpr uint32_t kChunk = 64 * kItems;
+    uint64_t cur[kItems];
+    if (flat) {
+      if (wtotal == 0) return;
+      load_flat(cur, 0);
+      for (uint32_t f0 = 0; f0 < wtotal; f0 += kChunk) {
+        uint64_t nxt[kItems];
+        load_flat(nxt, min(f0 + kChunk, (wtotal - 1) & ~(kChunk - 1)));
+        uint32_t vm = 0;
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) vm |= uint32_t(f0 + j * 64 + lane < wtotal) << j;
+        probe(cur, vm, f0 + lane);
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
+      }
+    } else {
+      load_reg(cur, r, qq, len);
+      while (r < nr) {
+        uint32_t nr_ = r, nq = qq + kChunk, nl = len;
+        while (nr_ < nr && nq >= nl) {
+          ++nr_;
+          nq = 0;
+          nl = nr_ < nr ? len_at(nr_) : 0u;
+        }
+        uint64_t nxt[kItems];
+        load_reg(nxt, nr_, nq, nl);
+        uint32_t vm = 0;
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) vm |= uint32_t(qq + j * 64 + lane < len) << j;
+        probe(cur, vm, pre_at(r) + qq + lane);
+        r = nr_;
+        qq = nq;
+        len = nl;
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
+      }
+    }
+  };
+  if (fits) {
+    pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent);
+    __syncthreads();
+    walk([&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+      pk_probe_items<MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
+    });
+  } else {
+    __syncthreads();
+    walk([&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+      probe_hbm_chunk(v, valid, bbase + wpre + srel);
+    });
+  }
+  // overflow pairs {h, row} (runs that did not fit their region): chunks of 1024 claimed by any
+  // workgroup that is done with its own slice; output slots from the same cursor
+  const uint64_t novf = __hip_atomic_load(ctl + kCtlNovf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (novf) {
+    for (;;) {
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlOvfCursor), (unsigned long long)kPkBlock);
+        const uint64_t take = c < novf ? min(uint64_t(kPkBlock), novf - c) : 0ull;
+        bbase = c;
+        flag = uint32_t(take);
+        if (MODE == 1 && take)
+          red[0][0] = atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlOut), (unsigned long long)take);
+      }
+      __syncthreads();
+      const uint32_t take = flag;
+      if (!take) break;
+      const uint64_t c = bbase, ob = MODE == 1 ? red[0][0] : 0ull;
+      if (threadIdx.x < take) {
+        const uint2 e = ovf[c + threadIdx.x];
+        const uint32_t bl = fm.mod(e.x) - pk.lo;
+        const uint32_t s = off[bl];
+        pk_probe_hbm<MODE, CK>(e.x, e.y, s, off[bl + 1] - s, ent, ob + threadIdx.x, acc, out, out_cap);
+      }
+    }
+  }
+  // this block's counters -> partials row (write-through stores), then the ticket; the last block
+  // folds every row into the result slot (loads that bypass the CU's L1) and resets the control words
+  __syncthreads();
+#pragma unroll
+  for (int f = 1; f < kProbeFields; ++f) {
+    const uint64_t w = f == kProbeFields - 1 ? wave_xor(acc[f]) : wave_sum(acc[f]);
+    if (lane == 0) red[wid][f] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < kProbeFields) {
+    const int f = threadIdx.x;
+    uint64_t a = 0;
+    for (int w = 0; w < kWaves; ++w) a = f == kProbeFields - 1 ? (a ^ red[w][f]) : (a + red[w][f]);
+    __hip_atomic_store(partials + uint64_t(blockIdx.x) * kProbeFields + f, f == 0 ? 0ull : a, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (wid == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (threadIdx.x == 0) {
+      const uint64_t t = __hip_atomic_fetch_add(ctl + kCtlTicket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      flag = t == gridDim.x - 1;
+    }
+  }
+  __syncthreads();
+  if (!flag) return;
+  // the last block: column sums over every block's row
+  uint64_t sum[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kPkBlock) {
+#pragma unroll
+    for (int f = 1; f < kProbeFields; ++f) {
+      const uint64_t x = __hip_atomic_load(partials + uint64_t(b) * kProbeFields + f, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      sum[f] = f == kProbeFields - 1 ? (sum[f] ^ x) : (sum[f] + x);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int f = 1; f < kProbeFields; ++f) {
+    const uint64_t w = f == kProbeFields - 1 ? wave_xor(sum[f]) : wave_sum(sum[f]);
+    if (lane == 0) red[wid][f] = w;
+  }
+  __syncthreads();
+  if (threadIdx.x < kProbeFields) {
+    const int f = threadIdx.x;
+    uint64_t a = 0;
+    if (f == 0) {
+      a = __hip_atomic_load(ctl + kCtlNprobe, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      for (int w = 0; w < kWaves; ++w) a = f == kProbeFields - 1 ? (a ^ red[w][f]) : (a + red[w][f]);
+    }
+    if (accumulate) a = f == kProbeFields - 1 ? (res[f] ^ a) : (res[f] + a);
+    res[f] = a;
+  }
+  if (!accumulate && threadIdx.x >= kProbeFields && threadIdx.x < 16) res[threadIdx.x] = 0;
+  if (threadIdx.x < kCtlWords) __hip_atomic_store(ctl + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+bool pk_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe, uint32_t flags) {
+  return t->desc.kind == HJ3D_CHAIN && (flags & HJ3D_PROBE_UNIQUE) && !ctx->force_direct && !ctx->pk_off &&
+         n_probe >= ctx->radix_min && n_probe > 0 && t->nb_local >= 64 && t->desc.num_buckets >= 2 &&
+         n_probe < (1ull << 32) && t->built;
+}
+
+hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out, uint64_t out_cap,
+                    uint64_t* res, hipStream_t s, const SelArgs* sel) {
+  hipError_t e;
+  const uint32_t nbl = t->nb_local, nb = uint32_t(t->desc.num_buckets);
+  // slice width: 80% of the LDS slice budget at the table's mean bucket fill
+  const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
+  uint32_t W = uint32_t(0.8 * kLdsWords / (1.0 + 2.0 * fill));
+  if (W < 64) W = 64;
+  if (W > nbl) W = nbl;
+  const uint32_t P = (nbl + W - 1) / W;
+  if (P > uint32_t(kPkBlock)) return hipErrorNotSupported;  // one slice per partitioning thread
+  // the packed word: bucket in slice (bits of W - 1) and the quotient h / NB (bits of its max)
+  auto bits = [](uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; };
+  const uint32_t qbits = bits(0xFFFFFFFFull / nb), wbits = bits(W - 1);
+  if (qbits + wbits > 32) return hipErrorNotSupported;
+  SelRange sr{};
+  if (sel && !SelRange::from(*sel, &sr)) return hipErrorNotSupported;
+  const uint32_t ntiles = uint32_t((r.n + kPkTile - 1) / kPkTile);
+  const uint32_t G = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
+  // region capacity: expected pairs per (workgroup, slice) + 8 sigma + slack, whole segments
+  const uint64_t per_g = uint64_t((ntiles + G - 1) / G) * kPkTile;
+  const double ex = double(per_g < r.n ? per_g : r.n) / P;
+  uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
+  cap = (cap + kPkSeg - 1) / kPkSeg * kPkSeg;
+  const uint64_t nreg = uint64_t(G) * P;
+  if (nreg * cap >= (1ull << 31)) return hipErrorNotSupported;
+  if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPHist].ensure(nreg * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
+  uint32_t splits = P < want_blocks ? (want_blocks + P - 1) / P : 1u;
+  if (splits > G) splits = G;
+  const uint32_t nblocks = P * splits;
+  if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+    return e;
+  if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
+  PkGeom pk;
+  pk.dnb = FastDiv32::make(nb);
+  pk.dw = W >= 2 ? FastDiv32::make(W) : FastDiv32{};
+  pk.nb = nb;
+  pk.lo = uint32_t(t->desc.bucket_lo);
+  pk.nbl = nbl;
+  pk.W = W;
+  pk.P = P;
+  pk.qbits = qbits;
+  pk.qmask = qbits >= 32 ? 0xFFFFFFFFu : ((1u << qbits) - 1);
+  uint2* region = ctx->scratch[kScrPairs].as<uint2>();
+  uint32_t* counts = ctx->scratch[kScrPHist].as<uint32_t>();
+  uint2* ovf = ctx->scratch[kScrSortV].as<uint2>();
+  uint64_t* ctl = ctx->ctl.as<uint64_t>();
+  const RelView v = view_of(r);
+  const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
+  {
+    PhaseTimer tm(ctx, HJ3D_T_SCATTER);
+    if (sel) {
+      if (imp) hipLaunchKernelGGL((k_pk_part<true, true>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      else hipLaunchKernelGGL((k_pk_part<false, true>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+    } else {
+      if (imp) hipLaunchKernelGGL((k_pk_part<true, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      else hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+    }
+  }
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
+  const bool ck = flags & HJ3D_PROBE_CHECKSUM;
+  const int acc = (flags & HJ3D_PROBE_ACCUMULATE) ? 1 : 0;
+  const bool flat = HJ3D_PK_FLAT || double(r.n) / double(nreg) < 256.0;
+  uint2* o = static_cast<uint2*>(out);
+  uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  {
+    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+#define HJ3D_PK_LAUNCH(MODE, CK)                                                                                     \
+  hipLaunchKernelGGL((k_pk_probe<MODE, CK>), dim3(nblocks), dim3(kPkBlock), 0, s, region, counts, G, uint32_t(cap), \
+                     splits, flat, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pk, t->fm, o, out_cap, ovf, \
+                     ctl, partials, res, acc, reinterpret_cast<uint2*>(ctl + 64))
+    if (emit) {
+      if (ck) HJ3D_PK_LAUNCH(1, true);
+      else HJ3D_PK_LAUNCH(1, false);
+    } else {
+      if (ck) HJ3D_PK_LAUNCH(0, true);
+      else HJ3D_PK_LAUNCH(0, false);
+    }
+#undef HJ3D_PK_LAUNCH
+  }
+  return hipGetLastError();
+}
+
+}  // namespace hj3d

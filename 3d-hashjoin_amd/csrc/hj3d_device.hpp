@@ -56,6 +56,34 @@ struct FastMod {
   }
 };
 
+// Exact n / d for u32 n and 2 <= d < 2^32 with one 32-bit high multiply (the branch-free form of
+// division by an invariant integer, Granlund & Montgomery 1994): q = mulhi(magic, n),
+// n / d = (((n - q) >> 1) + q) >> shift. Powers of two take magic = 0.
+struct FastDiv32 {
+  uint32_t magic = 0, shift = 0;
+  static FastDiv32 make(uint32_t d) {
+    FastDiv32 f;
+    const uint32_t L = 31u - uint32_t(__builtin_clz(d));
+    if ((d & (d - 1)) == 0) {
+      f.shift = L - 1;
+      return f;
+    }
+    const uint64_t num = uint64_t(1) << (32 + L);
+    uint32_t m = uint32_t(num / d);
+    const uint32_t rem = uint32_t(num % d);
+    m += m;
+    const uint32_t twice = rem + rem;
+    if (twice >= d || twice < rem) m += 1;
+    f.magic = m + 1;
+    f.shift = L;
+    return f;
+  }
+  __host__ __device__ __forceinline__ uint32_t div(uint32_t n) const {
+    const uint32_t q = uint32_t((uint64_t(magic) * n) >> 32);
+    return (((n - q) >> 1) + q) >> shift;
+  }
+};
+
 // Device view of an hj3d_rel (AoS tuples in HBM).
 struct RelView {
   const char* base;

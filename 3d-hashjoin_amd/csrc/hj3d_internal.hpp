@@ -70,6 +70,16 @@ struct hj3d_ctx {
   bool nested_sort = false;       // HJ3D_OPT_NESTED_SORT
   bool sel_unfused = false;       // HJ3D_OPT_SEL_UNFUSED
   hj3d::DevBuf sel;               // hj3d_probe_sel: passing (key, row) pairs when not fused
+  bool pk_off = false;            // HJ3D_OPT_PACKED_PROBE = 0: the unique chaining probe on (hash, row) pairs
+  // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
+  // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
+  hj3d::DevBuf ctl;
+  hipError_t ensure_ctl() {
+    if (ctl.p) return hipSuccess;
+    hipError_t e = ctl.ensure(128 * sizeof(uint64_t));  // 8 control words; [64, 128): store sink
+    if (e == hipSuccess) e = hipMemsetAsync(ctl.p, 0, ctl.bytes, stream);
+    return e;
+  }
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;
@@ -192,6 +202,12 @@ struct ProbeParts {
 };
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
                                  hipStream_t s, const SelArgs* sel = nullptr, unsigned long long** npass = nullptr);
+// chain_pk.hip: the unique chaining probe on packed pairs (partitioner + probe, two launches; the
+// result slot is set, or added to with HJ3D_PROBE_ACCUMULATE, by the probe kernel itself: no fill
+// before it). hipErrorNotSupported when the geometry does not pack (use radix_probe).
+bool pk_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe, uint32_t flags);
+hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
+                    uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,

@@ -214,7 +214,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
 // (skewed keys) scatters to HBM instead and sorts its small buckets there.
 constexpr uint32_t kBuildSlice2 = 8192;
 constexpr uint32_t kBuildStage = 15000;
-__global__ __launch_bounds__(kJBlock) void k_rp_build2(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+[[maybe_unused]] __global__ __launch_bounds__(kJBlock) void k_rp_build2(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
                                                        uint32_t* __restrict__ off, uint2* __restrict__ ent) {
   __shared__ uint32_t cnt[kBuildSlice2];
@@ -277,6 +277,111 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build2(const uint2* __restrict__
   if (!staged) return;
   __syncthreads();
   for (uint32_t k = threadIdx.x; k < m; k += kJBlock) ent[s0 + k] = stage[k];
+}
+
+// The staged build as a persistent kernel (one 1024-thread workgroup per CU takes partitions
+// blockIdx.x, blockIdx.x + gridDim.x, ...): the next partition's pairs are loaded into registers
+// while the current one is built, so a CU never idles on a partition's first loads. Per partition
+// of <= kB3Per * 1024 pairs: count per bucket with LDS atomics (each pair keeps its arrival rank),
+// scan to bucket starts (-> the directory slice), stage every pair at start + arrival rank, then
+// every staged pair takes its final slot = bucket start + the rank of its row among the bucket's
+// rows (buckets of 2..kSortedMax entries come out sorted by row, with no sort pass; longer ones
+// stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) fall back to
+// k_rp_build2's scatter through HBM for that partition.
+constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12288 pairs
+__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                       FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
+                                                       uint32_t* __restrict__ off, uint2* __restrict__ ent) {
+  __shared__ uint32_t cnt[kBuildSlice2 + 1];
+  __shared__ uint2 stage[kBuildStage];
+  __shared__ uint32_t wsum[kJBlock / kWave];
+  constexpr uint32_t kCap = kB3Per * kJBlock;
+  static_assert(kCap <= kBuildStage, "a register-held partition must fit the stage");
+  uint2 ea[kB3Per], eb[kB3Per];
+  auto load = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
+    if (p >= P) return;
+    const uint32_t s0 = ps[p], s1 = ps[p + 1];
+    if (s1 - s0 > kCap) return;
+#pragma unroll
+    for (int u = 0; u < kB3Per; ++u) {
+      const uint32_t i = s0 + u * kJBlock + threadIdx.x;
+      e[u] = i < s1 ? pairs[i] : make_uint2(0, 0);
+    }
+  };
+  auto build = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
+    const uint32_t b0 = p * W;
+    const uint32_t nbs = min(W, nbl - b0);
+    const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
+    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
+    __syncthreads();
+    if (m > kCap) {  // skewed partition: scatter through HBM, sort the small buckets there
+      for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) atomicAdd(&cnt[fm.mod(pairs[i].x) - lo - b0], 1u);
+      __syncthreads();
+      lds_excl_scan(cnt, nbs, wsum);
+      for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+      if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
+      __syncthreads();
+      for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) {
+        const uint2 x = pairs[i];
+        ent[s0 + atomicAdd(&cnt[fm.mod(x.x) - lo - b0], 1u)] = x;
+      }
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) {
+        const uint32_t bs = k ? cnt[k - 1] : 0u, n = cnt[k] - bs;
+        if (n < 2 || n > kSortedMax) continue;
+        uint2* E = ent + s0 + bs;
+        for (uint32_t q = 1; q < n; ++q) {
+          const uint2 x = E[q];
+          uint32_t j = q;
+          while (j > 0 && E[j - 1].y > x.y) {
+            E[j] = E[j - 1];
+            --j;
+          }
+          E[j] = x;
+        }
+      }
+      __syncthreads();
+      return;
+    }
+    uint32_t rk[kB3Per];  // bucket << 16 | arrival rank (W <= 2^16, ranks < 2^16)
+#pragma unroll
+    for (int u = 0; u < kB3Per; ++u) {
+      const bool v = u * kJBlock + threadIdx.x < m;
+      const uint32_t b = v ? fm.mod(e[u].x) - lo - b0 : 0u;
+      rk[u] = v ? (b << 16) | atomicAdd(&cnt[b], 1u) : kInvalid;
+    }
+    __syncthreads();
+    lds_excl_scan(cnt, nbs, wsum);
+    if (threadIdx.x == 0) cnt[nbs] = m;
+    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+    if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kB3Per; ++u)
+      if (rk[u] != kInvalid) stage[cnt[rk[u] >> 16] + (rk[u] & 0xFFFFu)] = e[u];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < m; q += kJBlock) {
+      const uint2 x = stage[q];
+      const uint32_t b = fm.mod(x.x) - lo - b0;
+      const uint32_t bs = cnt[b], n = cnt[b + 1] - bs;
+      uint32_t pos = q;
+      if (n >= 2 && n <= kSortedMax) {
+        uint32_t r = 0;
+        for (uint32_t k = bs; k < bs + n; ++k) r += stage[k].y < x.y;
+        pos = bs + r;
+      }
+      ent[s0 + pos] = x;
+    }
+    __syncthreads();
+  };
+  load(ea, blockIdx.x);
+  for (uint32_t p = blockIdx.x; p < P; p += 2 * gridDim.x) {
+    load(eb, p + gridDim.x);
+    build(ea, p);
+    if (p + gridDim.x >= P) break;
+    load(ea, p + 2 * gridDim.x);
+    build(eb, p + gridDim.x);
+  }
 }
 
 enum Mode { kAgg = 0, kDense = 1, kCount = 2, kWrite = 3 };
@@ -1015,8 +1120,14 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   if (nbl && staged) {
+#ifdef HJ3D_BUILD2
     hipLaunchKernelGGL(k_rp_build2, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo),
                        nbl, pl.W, t->off.as<uint32_t>(), t->ent.as<uint2>());
+#else
+    const uint32_t g = pl.P < uint32_t(ctx->num_cus) ? pl.P : uint32_t(ctx->num_cus);
+    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
+                       pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
+#endif
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
     hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,

@@ -81,6 +81,9 @@ def parse():
                    help="workload B/D plan: Csr chaining build R / probe S (the headline); Nsr 3D table on R.k, "
                         "probe S + unnest; Nrs 3D table on S.a (NB = #dv(S.a) from the distributed pre-pass), "
                         "probe R + unnest")
+    p.add_argument("--probe-path", default="packed", choices=["packed", "pairs"],
+                   help="unique chaining probe: packed pairs, two launches (default), or the (hash, row) pair "
+                        "partitioned probe (A/B)")
     p.add_argument("--theta", type=float, default=0.8, help="config C Zipf parameter")
     p.add_argument("--nested-build", default="agg", choices=["agg", "sort", "radix"],
                    help="3D build: bucket-range partition + LDS aggregation (default), LSD key sort "
@@ -304,6 +307,8 @@ def main():
     emit = not args.no_emit
     ctx = hj3d.Context(local)
     ctx.timing(True)
+    packed = args.probe_path == "packed" and plan == "Csr"
+    ctx.packed_probe(packed)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
     fx_plan = (fx or {}).get("plans", {}).get(plan)
 
@@ -436,8 +441,9 @@ def main():
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     # per-kernel averages over the timed steps (HIP events on the engine's stream)
     kern_avg = {}
-    kprobe = "k_rp_probe_seg" if unique else "k_rn_probe_seg"
-    for name, ph in ((kprobe, hj3d.T_PROBE_KERNEL), ("k_rp_part1", hj3d.T_SCATTER)):
+    kprobe = "k_pk_probe" if packed else ("k_rp_probe_seg" if unique else "k_rn_probe_seg")
+    kpart = "k_pk_part" if packed else "k_rp_part1"
+    for name, ph in ((kprobe, hj3d.T_PROBE_KERNEL), (kpart, hj3d.T_SCATTER)):
         ms, cnt = ctx.timer(ph)
         kern_avg[name] = ms / cnt if cnt else None
     # verification step (outside the timed region): the same step once more with the
@@ -533,8 +539,8 @@ def main():
 
     # ---- roofline of the dominant kernel ----
     # Algorithmic bytes per launch, n = probe tuples of this rank per launch:
-    #   k_rp_part1      n * (12 + 8)                read the S tuple (AoS {k,a,b}), write the (hash,row) pair
-    #   k_rp_probe_seg  n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
+    #   k_pk_part (k_rp_part1)      n * (12 + 8)   read the S tuple (AoS {k,a,b}), write the packed pair
+    #   k_pk_probe (k_rp_probe_seg) n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
     #                                                    the table slices (entries + directory) once
     #   k_rn_probe_seg  (3D plans, unnest materialised): n * (8 + 16) read the pair, write the slot's
     #                   output count (8), sub offset and probe row (4 + 4); + the slices (directory +
@@ -544,11 +550,11 @@ def main():
     n = probe_n_local / launches
     tuple_bytes = 12 if world == 1 else 8
     if unique:
-        alg = {"k_rp_part1": n * (tuple_bytes + 8),
+        alg = {kpart: n * (tuple_bytes + 8),
                kprobe: n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4}
     else:
         n_keys = dv if plan == "Nrs" else nR_tot
-        alg = {"k_rp_part1": n * (tuple_bytes + 8),
+        alg = {kpart: n * (tuple_bytes + 8),
                kprobe: n * (8 + (16 if emit else 0)) + (n_keys // world) * 16 + (nb // world) * 4}
     kernels = {}
     for k, ms in kern_avg.items():

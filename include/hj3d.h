@@ -150,7 +150,11 @@ enum {
   HJ3D_OPT_NESTED_SORT = 4,
   /* HJ3D_OPT_SEL_UNFUSED (0/1, default 0): hj3d_probe_sel always selects first (hj3d_select) and
    * probes the passing pairs, instead of fusing the selection into the probe partitioner. */
-  HJ3D_OPT_SEL_UNFUSED = 5
+  HJ3D_OPT_SEL_UNFUSED = 5,
+  /* HJ3D_OPT_PACKED_PROBE (0/1, default 1): the unique chaining probe partitions the probe side into
+   * packed {bucket-in-slice | hash / NB, row} pairs and finishes in two launches; 0 keeps the
+   * {hash, row} partitioned probe (A/B measurements). */
+  HJ3D_OPT_PACKED_PROBE = 6
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

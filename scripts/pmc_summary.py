@@ -22,7 +22,7 @@ import os
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe", "k_rp_scatter", "k_rp_hist", "k_rp_build2", "k_rp_build",
+KERNELS = ("k_pk_probe", "k_pk_part", "k_pk_build", "k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe", "k_rp_scatter", "k_rp_hist", "k_rp_build2", "k_rp_build",
            "k_sort_small_buckets", "k_scan_tiles")
 
 

@@ -342,3 +342,27 @@ def test_num_distinct_bitmap_matches_reference(ctx, name, g):
     bm2 = torch.zeros((1, (k + 31) // 32), dtype=torch.int32, device="cuda")
     ctx.key_bitmap(relS, k, bm2[0], out)
     assert int(out.item()) == int((S[:, 1] >= k).sum())
+
+
+@pytest.mark.parametrize("theta", [0.6, 1.0])
+def test_chaining_build_skewed_partition(ctx, theta):
+    """A chaining table at fill ~1 over Zipf keys: the staged persistent build (k_rp_build3) holds a
+    partition of up to 12288 pairs in registers; the hot keys' partition exceeds that and takes the
+    HBM scatter fallback inside the same kernel. Statistics, comparison counts and the output of
+    the unique and non-unique probes equal the oracle's (rows sorted inside buckets of <= 32)."""
+    rng = np.random.default_rng(int(theta * 10))
+    nB, nP = 2_000_000, 2_000_000
+    Bk = (np.minimum(rng.zipf(1.0 + theta, nB), 5_000_000) - 1).astype(np.uint32)
+    Pk = rng.integers(0, 4_000_000, nP).astype(np.uint32)
+    B = O.tuples3(Bk, np.zeros(nB, np.uint32))
+    P = O.tuples3(np.arange(nP, dtype=np.uint32), Pk)
+    import hj3d
+    for unique in (True, False):
+        e = O.chain_plan(B, 0, P, 1, nB, unique)
+        t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nB)
+        t.build(hj3d.Rel(dev(B), 0))
+        r = ctx.probe(t, hj3d.Rel(dev(P), 1), unique=unique)
+        assert (r.n_out, r.n_cmps) == (e.c_probe, e.c_cmp), unique
+        assert {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_c": 0, "sum_h": r.sum_h, "xor_h": r.xor_h} == e.out
+        st = t.stats()
+        assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
