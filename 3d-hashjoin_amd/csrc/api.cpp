@@ -293,6 +293,28 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   return from_hip(ctx, e, "hj3d_build");
 }
 
+hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
+                              uint64_t* n_payload, uint64_t* n_sub) {
+  if (!ctx || !t || !n_payload || !n_sub) return HJ3D_EINVAL;
+  const uint64_t nbl = t->nb_local;
+  uint32_t last = 0;  // off[nb_local] = the payload count
+  hipError_t e = hipMemcpyAsync(&last, t->off.as<uint32_t>() + nbl, sizeof(last), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_table_export");
+  const bool nested = t->desc.kind == HJ3D_NESTED;
+  *n_payload = t->built ? last : 0;
+  *n_sub = nested && t->built ? t->n_build : 0;
+  if (!off && !payload && !sub) return HJ3D_OK;
+  if (!off || (*n_payload && !payload) || (*n_sub && !sub)) return fail(ctx, HJ3D_EINVAL, "hj3d_table_export: null array");
+  e = hipMemcpyAsync(off, t->off.p, (nbl + 1) * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess && *n_payload)
+    e = hipMemcpyAsync(payload, nested ? t->main.p : t->ent.p, *n_payload * (nested ? 16 : 8), hipMemcpyDeviceToHost,
+                       ctx->stream);
+  if (e == hipSuccess && *n_sub) e = hipMemcpyAsync(sub, t->sub.p, *n_sub * 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  return from_hip(ctx, e, "hj3d_table_export");
+}
+
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out) {
   if (!ctx || !t || !out) return HJ3D_EINVAL;
   std::memset(out, 0, sizeof(*out));

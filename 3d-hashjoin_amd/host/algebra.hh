@@ -15,7 +15,9 @@
 //     and only their counters come back (algebra.hh:435-459, 510-541, 625-659 semantics,
 //     comparison counts included). A chaining probe into any other consumer materialises its
 //     output pairs on the device and pushes concat(probe, build) tuples in the reference's
-//     order. Nested probes into other consumers are refused (hj3d::host::Error).
+//     order. A nested probe into any other consumer runs the reference's tuple-at-a-time probe
+//     over a host node view of the device table (correct, slow; ht_nested.hh findMainNodeByOther)
+//     and AlgUnnestHt expands the nested tuples it receives on the host.
 // No operator has a host-side join: without a GPU the engine cannot be created and the first
 // build/probe throws.
 #pragma once
@@ -521,7 +523,7 @@ class AlgNestJoinProbe : public AlgBase {
   }
   inline uint64_t selected_count() const { return _dev.n_selected; }
   inline void fin(globstat_t* g) {
-    if (!_absorbed) execute();
+    if (!_absorbed) execute(g);
     _consumer->fin(g);
     stopTimer();
   }
@@ -531,7 +533,7 @@ class AlgNestJoinProbe : public AlgBase {
  private:
   using ht_t = typename build_t::hashtable_t;
 
-  void execute() {
+  void execute(globstat_t* g) {
     using namespace hj3d::host;
     auto& dt = _buildOperator->hashtable().device();
     hj3d_table* t = dt.table();
@@ -589,8 +591,33 @@ class AlgNestJoinProbe : public AlgBase {
         }
       }
     }
-    throw Error("hj3d: AlgNestJoinProbe: this consumer pipeline has no device implementation (supported: "
-                "probe->Top, probe->unnest->Top, probe->probe->unnest->unnest->Top, with Top not printing)");
+    host_probe(g);
+  }
+
+  // Any other consumer pipeline (a printing Top, a custom consumer, an unnest into something
+  // else): the reference's tuple-at-a-time probe (algebra.hh:435-459) over the host node view of
+  // the device table (HtNested1::findMainNodeByOther), pushing nested tuples in probe order.
+  // Correct but slow; the fused strands above are the fast path.
+  void host_probe(globstat_t* g) {
+    const auto& ht = _buildOperator->hashtable();
+    auto push = [&](input_t* t) {
+      const auto [mn, cmps] = ht.template findMainNodeByOther<input_t, hashfun_t, joinpred_t>(t);
+      _numCmps += cmps;
+      if (mn == nullptr) return;
+      output_t o = concatfun_t::eval(t, mn);
+      inc();
+      _consumer->step(&o, g);
+    };
+    if (_dev.n_selected != _in.size() || _dev.rel.row_off != HJ3D_ROW_IMPLICIT) {
+      // a device selection was applied: its passing rows, in scan order
+      std::vector<uint32_t> pr(2 * _dev.rel.n);
+      hj3d::host::Engine& e = hj3d::host::Engine::get();
+      if (_dev.rel.n) e.check(hj3d_download(e.ctx(), pr.data(), _dev.rel.base, _dev.rel.n * 8), "hj3d_download (selection)");
+      for (uint64_t i = 0; i < _dev.rel.n; ++i) push(_in.at(pr[2 * i + 1]));
+    } else {
+      for (uint64_t i = 0; i < _in.size(); ++i) push(_in.at(i));
+    }
+    _absorbed = true;
   }
 
   // the second probe's hash of concat(r, <a main node of this table>) equals this probe's hash of r
@@ -623,8 +650,10 @@ class AlgNestJoinProbe : public AlgBase {
 
 /*
  * 3D hash join unnest (reference algebra.hh:476-552). count() = unnested output tuples.
- * Runs fused inside the preceding AlgNestJoinProbe; a nested tuple pushed by other code
- * cannot be expanded on the host (there are no host-side main nodes) and throws.
+ * Runs fused inside the preceding AlgNestJoinProbe on the device; nested tuples pushed to step()
+ * (the host probe path of AlgNestJoinProbe, or other code holding main nodes of HtNested1's host
+ * node view) are expanded on the host as the reference does: the main node's tuple, then its
+ * sub-chain.
  */
 template <alg_consumer_c Tconsumer, alg_unnestfun_c Tunnestfun, typename Thtnested>
 class AlgUnnestHt : public AlgBase {
@@ -643,9 +672,17 @@ class AlgUnnestHt : public AlgBase {
     reset();
     _consumer->init(g);
   }
-  inline void step([[maybe_unused]] input_t* aNestedTuple, [[maybe_unused]] globstat_t* g) {
-    throw hj3d::host::Error("hj3d: AlgUnnestHt::step: nested tuples are expanded on the device by the "
-                            "preceding AlgNestJoinProbe");
+  inline void step(input_t* aNestedTuple, globstat_t* g) {
+    const auto* mn = unnestfun_t::getMainNode(aNestedTuple);
+    unnestfun_t::eval_left(&_outputTuple, aNestedTuple);
+    unnestfun_t::eval_right(&_outputTuple, aNestedTuple, mn->data());
+    _consumer->step(&_outputTuple, g);
+    inc();
+    for (auto* sn = mn->child(); sn != nullptr; sn = sn->next()) {
+      unnestfun_t::eval_right(&_outputTuple, aNestedTuple, sn->data());
+      _consumer->step(&_outputTuple, g);
+      inc();
+    }
   }
   inline void fin(globstat_t* g) {
     _consumer->fin(g);
@@ -655,6 +692,7 @@ class AlgUnnestHt : public AlgBase {
 
  private:
   consumer_t* _consumer;
+  output_t _outputTuple{};
 };
 
 /*

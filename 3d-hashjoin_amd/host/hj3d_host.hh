@@ -10,17 +10,20 @@
 //   * key_word_of<Thashfun>(): locates the u32 join attribute inside an opaque tuple type by
 //     fingerprinting the hash functor (murmur3 fmix32 is a bijection, util/hasht.hh:52-61), and
 //     check_joinpred<>() verifies that a join predicate is key equality on the located words.
-//   * RelationCache: device copies of the host relations, re-uploaded when a sample of their
-//     bytes changes.
+//   * RelationCache: device copies of the host relations, re-uploaded when their contents change
+//     (a full 64-bit fingerprint of every byte, computed in parallel; HJ3D_TRUST_RELATIONS=1
+//     checks a 257-tuple sample instead, for drivers that never modify a relation in place).
 #pragma once
 
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <map>
 #include <optional>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <type_traits>
 #include <vector>
 
@@ -121,8 +124,11 @@ class DevBuffer {
 };
 
 // Device copies of host relations keyed by their address. A relation is re-uploaded when its
-// size, stride or a 257-tuple byte sample changes (drivers do not modify relations between
-// scans; call invalidate() after modifying one in place).
+// size, stride or contents change: the fingerprint covers every byte (8-byte words folded by
+// several threads for large relations), so a relation regenerated or modified in place at the
+// same address is never joined from a stale device copy. HJ3D_TRUST_RELATIONS=1 fingerprints a
+// 257-tuple sample instead (faster, unsafe under in-place modification); invalidate() forces the
+// next upload either way.
 class RelationCache {
  public:
   static RelationCache& get() {
@@ -131,8 +137,8 @@ class RelationCache {
   }
   const void* upload(const void* host, uint64_t n, uint32_t stride) {
     Entry& e = _m[host];
-    const uint64_t sig = sample(host, n, stride);
-    if (e.buf && e.n == n && e.stride == stride && e.sig == sig) return e.buf->get();
+    const uint64_t sig = trust_sample() ? sample(host, n, stride) : fingerprint(host, n * stride);
+    if (e.buf && e.n == n && e.stride == stride && e.sig == sig && e.valid) return e.buf->get();
     if (!e.buf) e.buf = new DevBuffer();
     Engine& g = Engine::get();
     void* d = e.buf->ensure(n * stride);
@@ -140,14 +146,55 @@ class RelationCache {
     e.n = n;
     e.stride = stride;
     e.sig = sig;
+    e.valid = true;
+    ++_uploads;
     return d;
   }
   void invalidate(const void* host) {
     auto it = _m.find(host);
-    if (it != _m.end()) it->second.sig ^= 1;
+    if (it != _m.end()) it->second.valid = false;
   }
+  uint64_t uploads() const { return _uploads; }  // uploads so far (tests)
   ~RelationCache() {
     for (auto& kv : _m) delete kv.second.buf;
+  }
+
+  // 64-bit fingerprint of `bytes` bytes: per 8-byte word w at index i, mix(w ^ i * K) summed (order-
+  // free, so the word ranges of the threads combine by addition).
+  static uint64_t fingerprint(const void* host, uint64_t bytes) {
+    const unsigned char* p = static_cast<const unsigned char*>(host);
+    const uint64_t words = bytes / 8;
+    auto range = [p](uint64_t a, uint64_t b) {
+      uint64_t s0 = 0, s1 = 0;
+      uint64_t i = a;
+      for (; i + 1 < b; i += 2) {
+        uint64_t w0, w1;
+        std::memcpy(&w0, p + 8 * i, 8);
+        std::memcpy(&w1, p + 8 * i + 8, 8);
+        s0 += mix(w0 ^ (i * 0x9e3779b97f4a7c15ull));
+        s1 += mix(w1 ^ ((i + 1) * 0x9e3779b97f4a7c15ull));
+      }
+      if (i < b) {
+        uint64_t w;
+        std::memcpy(&w, p + 8 * i, 8);
+        s0 += mix(w ^ (i * 0x9e3779b97f4a7c15ull));
+      }
+      return s0 + s1;
+    };
+    uint64_t h = 0;
+    const unsigned nt = words >= (uint64_t(1) << 22) ? std::min(16u, std::max(1u, std::thread::hardware_concurrency())) : 1u;
+    if (nt > 1) {
+      std::vector<uint64_t> part(nt, 0);
+      std::vector<std::thread> th;
+      for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] { part[t] = range(words * t / nt, words * (t + 1) / nt); });
+      for (auto& x : th) x.join();
+      for (uint64_t v : part) h += v;
+    } else {
+      h = range(0, words);
+    }
+    for (uint64_t b = words * 8; b < bytes; ++b) h += mix(uint64_t(p[b]) ^ (b << 8) ^ 0xa5a5a5a5ull);
+    return mix(h ^ bytes);
   }
 
  private:
@@ -155,7 +202,20 @@ class RelationCache {
     DevBuffer* buf = nullptr;
     uint64_t n = 0, sig = 0;
     uint32_t stride = 0;
+    bool valid = false;
   };
+  static uint64_t mix(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+  }
+  static bool trust_sample() {
+    static const bool t = [] {
+      const char* v = std::getenv("HJ3D_TRUST_RELATIONS");
+      return v && v[0] == '1';
+    }();
+    return t;
+  }
   static uint64_t sample(const void* host, uint64_t n, uint32_t stride) {
     uint64_t h = 0xcbf29ce484222325ull ^ n;
     const unsigned char* p = static_cast<const unsigned char*>(host);
@@ -167,6 +227,7 @@ class RelationCache {
     return h;
   }
   std::map<const void*, Entry> _m;
+  uint64_t _uploads = 0;
 };
 
 // ---- locating the join attribute behind opaque functors ----
@@ -362,6 +423,7 @@ class DeviceTable {
     _segs.clear();
     _rows.clear();
     _dirty = false;
+    ++_version;
     Engine& e = Engine::get();
     e.check(hj3d_table_clear(e.ctx(), _t), "hj3d_table_clear");
   }
@@ -373,6 +435,28 @@ class DeviceTable {
   Tdata* row_ptr(uint64_t row) const { return _rows.at(row); }
   uint64_t rows() const { return _rows.size(); }
   const std::optional<uint32_t>& key_word() const { return _dev.key_word; }
+  // Host copy of the device arrays (hj3d_table_export), fetched once per build: the per-tuple
+  // probe API (findDirEntryByOther / findMainNodeByOther) walks node views made from it.
+  struct Mirror {
+    std::vector<uint32_t> off, payload, sub;  // payload: {hash, row} or {hash, first_row, sub_off, sub_len}
+    uint64_t n_payload = 0;
+  };
+  const Mirror& mirror() {
+    hj3d_table* t = table();
+    if (_mirror_version == _version) return _mirror;
+    Engine& e = Engine::get();
+    uint64_t np = 0, ns = 0;
+    e.check(hj3d_table_export(e.ctx(), t, nullptr, nullptr, nullptr, &np, &ns), "hj3d_table_export");
+    _mirror.off.assign(_nb + 1, 0);
+    _mirror.payload.assign(np * (_kind == HJ3D_NESTED ? 4 : 2), 0);
+    _mirror.sub.assign(ns, 0);
+    _mirror.n_payload = np;
+    e.check(hj3d_table_export(e.ctx(), t, _mirror.off.data(), _mirror.payload.data(), _mirror.sub.data(), &np, &ns),
+            "hj3d_table_export");
+    _mirror_version = _version;
+    return _mirror;
+  }
+  uint64_t version() const { return _version; }  // bumped by every build / clear
   hj3d_stats stats() {
     hj3d_table* t = table();
     Engine& e = Engine::get();
@@ -398,6 +482,7 @@ class DeviceTable {
     e.check(hj3d_build(e.ctx(), _t, &_dev.rel), "hj3d_build");
     e.check(hj3d_ctx_sync(e.ctx()), "hj3d_build (sync)");
     _dirty = false;
+    ++_version;
   }
   uint32_t _kind;
   size_t _nb;
@@ -406,6 +491,8 @@ class DeviceTable {
   std::vector<Tdata*> _rows;
   DevInput<Thashfun> _dev;
   bool _dirty = false;
+  uint64_t _version = 1, _mirror_version = 0;
+  Mirror _mirror;
 };
 
 }  // namespace hj3d::host

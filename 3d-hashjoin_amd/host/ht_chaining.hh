@@ -5,13 +5,17 @@
 // compile unchanged. The table itself lives on the device (CSR buckets of {hash, row}, see
 // DESIGN.md §3): insert() records tuples, the device build runs at the first probe or
 // statistics call after an insert, and probing is done by the algebra.hh probe operators
-// through the C ABI. Node is kept as a type (24 B, as the reference prints it) for drivers
-// that name it.
+// through the C ABI. Node (24 B, as the reference prints it) is a real node: per-tuple callers
+// of findDirEntryByOther get the reference's directory slot and chain, rebuilt on the host from
+// the device table.
 #pragma once
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "concepts.hh"
 #include "hj3d_host.hh"
@@ -89,12 +93,18 @@ class HtChaining1 {
 
   stats_t makeStatistics() const { return HtStatistics::from(_dev.stats(), _size); }
 
-  // Per-tuple probing of the device table is not offered; the probe operators of algebra.hh
-  // probe whole inputs on the device.
+  // HtChaining1::findDirEntryByOther (ht_chaining.hh:236-248): the directory slot of the probe
+  // tuple's bucket as the reference lays it out, walked through the reference's node iterator.
+  // Correct but slow: the first call after a build copies the device table to the host and
+  // materialises the reference's node layout from it (directory node = the bucket's first insert,
+  // then the chain newest first), so per-tuple callers that walk the table themselves run
+  // unchanged; the algebra.hh probe operators never take this path.
   template <typename Tprobedata, alg_hashfun_c Tprobehashfun>
-  const_node_iterator findDirEntryByOther(const Tprobedata*) const {
-    throw hj3d::host::Error("hj3d: HtChaining1::findDirEntryByOther: per-tuple probes are not supported by the "
-                            "device table; use AlgHashJoinProbe");
+  const_node_iterator findDirEntryByOther(const Tprobedata* aProbeTuple) const {
+    static_assert(std::is_same_v<hashvalue_t, typename Tprobehashfun::output_t>);
+    const hashvalue_t h = Tprobehashfun::eval(aProbeTuple);
+    nodes();
+    return const_node_iterator(&_dir[size_t(h) % numBuckets()]);
   }
 
   // ---- device access for the algebra.hh operators ----
@@ -102,6 +112,35 @@ class HtChaining1 {
   hj3d::host::DeviceTable<data_t, hashfun_t>& device() const { return _dev; }
 
  private:
+  // the reference's node layout rebuilt from the host mirror of the device table
+  void nodes() const {
+    auto& dev = _dev;
+    const auto& m = dev.mirror();
+    if (_nodes_version == dev.version()) return;
+    const size_t nb = numBuckets();
+    _dir.assign(nb, Node());
+    _chain.clear();
+    _chain.reserve(m.n_payload);
+    std::vector<std::pair<uint32_t, uint32_t>> b;  // (row, hash) of one bucket
+    for (size_t k = 0; k < nb; ++k) {
+      const uint32_t s = m.off[k], e = m.off[k + 1];
+      if (s == e) continue;
+      b.clear();
+      for (uint32_t i = s; i < e; ++i) b.emplace_back(m.payload[2 * i + 1], m.payload[2 * i]);
+      std::sort(b.begin(), b.end());  // row order = insertion order
+      Node* next = nullptr;
+      for (size_t j = 1; j < b.size(); ++j) {  // chain: head-inserted, so the newest comes first
+        _chain.emplace_back(dev.row_ptr(b[j].first));
+        _chain.back().init(dev.row_ptr(b[j].first), hashvalue_t(b[j].second), next);
+        next = &_chain.back();
+      }
+      _dir[k].init(dev.row_ptr(b[0].first), hashvalue_t(b[0].second), next);
+    }
+    _nodes_version = dev.version();
+  }
+
   mutable hj3d::host::DeviceTable<data_t, hashfun_t> _dev;
   size_t _size;
+  mutable std::vector<Node> _dir, _chain;
+  mutable uint64_t _nodes_version = 0;
 };

@@ -4,13 +4,18 @@
 // Same template signature and member types as the reference (MainNode, SubNode, data_t are
 // named by the drivers' nested tuple and unnest functor types). The table lives on the device
 // (one main record per distinct key + a row list per key); probe, unnest and
-// deferred unnest run fused on the device through the algebra.hh operators.
+// deferred unnest run fused on the device through the algebra.hh operators. MainNode / SubNode
+// are real nodes: findMainNodeByOther returns the reference's main node (with its sub-chain),
+// rebuilt on the host from the device table, for per-tuple callers and host-side consumers.
 #pragma once
 
+#include <algorithm>
 #include <cstddef>
 #include <cstdint>
 #include <tuple>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "concepts.hh"
 #include "hj3d_host.hh"
@@ -118,16 +123,71 @@ class HtNested1 {
 
   stats_t makeStatistics() const { return HtStatistics::from(_dev.stats(), _size); }
 
+  // HtNested1::findMainNodeByOther (ht_nested.hh:354-382): the main node of the probe tuple's key
+  // and the main-chain comparisons, walked as the reference walks them. Correct but slow: the
+  // first call after a build copies the device table to the host and materialises the reference's
+  // node layout (main nodes in first-occurrence order, each key's further tuples as a sub-chain,
+  // newest first), whose MainNode / SubNode pointers an unnest functor can then follow.
   template <typename Tprobedata, alg_hashfun_c Tprobehashfun, alg_binary_predicate_c Tjoinpred>
-  const std::tuple<const MainNode*, const uint64_t> findMainNodeByOther(const Tprobedata*) const {
-    throw hj3d::host::Error("hj3d: HtNested1::findMainNodeByOther: per-tuple probes are not supported by the "
-                            "device table; use AlgNestJoinProbe");
+  const std::tuple<const MainNode*, const uint64_t> findMainNodeByOther(const Tprobedata* aProbeTuple) const {
+    static_assert(std::is_same_v<hashvalue_t, typename Tprobehashfun::output_t>);
+    const hashvalue_t h = Tprobehashfun::eval(aProbeTuple);
+    nodes();
+    const MainNode* n = &_dir[size_t(h) % numBuckets()];
+    uint64_t cmps = 0;
+    do {
+      if (n->isEmpty()) return {nullptr, cmps};
+      ++cmps;
+      if (n->hashvalue() == h && Tjoinpred::eval(aProbeTuple, n->data())) return {n, cmps};
+      n = n->next();
+    } while (n != nullptr);
+    return {nullptr, cmps};
   }
 
   // the device table is built lazily, hence mutable behind the const observers
   hj3d::host::DeviceTable<data_t, hashfun_t>& device() const { return _dev; }
 
  private:
+  // the reference's node layout rebuilt from the host mirror of the device table
+  void nodes() const {
+    auto& dev = _dev;
+    const auto& m = dev.mirror();
+    if (_nodes_version == dev.version()) return;
+    const size_t nb = numBuckets();
+    _dir.assign(nb, MainNode());
+    _mains.clear();
+    _mains.reserve(m.n_payload);
+    _subs.clear();
+    _subs.reserve(m.sub.size());
+    std::vector<std::pair<uint32_t, uint32_t>> mains;  // (first row, main record) of one bucket
+    std::vector<uint32_t> rows;
+    for (size_t k = 0; k < nb; ++k) {
+      const uint32_t s = m.off[k], e = m.off[k + 1];
+      if (s == e) continue;
+      mains.clear();
+      for (uint32_t i = s; i < e; ++i) mains.emplace_back(m.payload[4 * i + 1], i);
+      std::sort(mains.begin(), mains.end());  // first-occurrence order of the keys
+      MainNode* prev = nullptr;
+      for (size_t j = 0; j < mains.size(); ++j) {
+        const uint32_t* rec = &m.payload[4 * size_t(mains[j].second)];
+        MainNode* mn = j == 0 ? &_dir[k] : &_mains.emplace_back();
+        mn->init(dev.row_ptr(rec[1]), hashvalue_t(rec[0]));
+        // sub-chain: the key's other tuples, head-inserted, so the newest comes first
+        rows.assign(m.sub.begin() + rec[2], m.sub.begin() + rec[2] + rec[3]);
+        std::sort(rows.begin(), rows.end());
+        SubNode* head = nullptr;
+        for (size_t q = 1; q < rows.size(); ++q) head = &_subs.emplace_back(dev.row_ptr(rows[q]), head);
+        mn->_subchain_head = head;
+        if (prev) prev->_next = mn;
+        prev = mn;
+      }
+    }
+    _nodes_version = dev.version();
+  }
+
   mutable hj3d::host::DeviceTable<data_t, hashfun_t> _dev;
   size_t _size;
+  mutable std::vector<MainNode> _dir, _mains;
+  mutable std::vector<SubNode> _subs;
+  mutable uint64_t _nodes_version = 0;
 };

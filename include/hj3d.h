@@ -29,6 +29,12 @@
  * reference's chain order (chaining: directory entry first, then newest-first; nested:
  * main nodes in first-occurrence order) is reproduced arithmetically from row ids.
  *
+ * Join predicate: the engine joins on EQUALITY OF THE u32 JOIN ATTRIBUTE, tested as equality of
+ * its fmix32 hash. fmix32 is a bijection on u32 (every step is invertible), so equal hashes are
+ * equal keys and the reference's joinpred after the hash compare (algebra.hh:647-648) is implied
+ * (SURVEY App. B item 7). A caller whose join predicate is anything else must not use this ABI;
+ * the drop-in layer checks this on sample tuples (hj3d_host.hh check_joinpred) and refuses.
+ *
  * Conventions: all relation/pair pointers are DEVICE pointers; every call is enqueued on the
  * context's stream (asynchronous) unless documented as synchronous. Calls return hj3d_status;
  * nothing throws. One host thread per context.
@@ -188,6 +194,15 @@ hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build)
 hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t);
 /* Build: replaces the table content with the tuples of `build` (asynchronous). */
 hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
+/* Host copy of a table's device arrays (synchronous): what the drop-in layer's per-tuple probes
+ * walk (HtChaining1::findDirEntryByOther ht_chaining.hh:236-248, HtNested1::findMainNodeByOther
+ * ht_nested.hh:354-382). Call with NULL arrays first to get the sizes: *n_payload = entries
+ * (chaining) or main records (nested), *n_sub = build rows of a nested table (0 for chaining).
+ * Then off[nb_local + 1] receives the CSR offsets of the local buckets into the payload, payload
+ * the chaining entries {u32 hash, u32 row} or the nested main records {u32 hash, first_row,
+ * sub_off, sub_len}, and sub (nested) the build rows grouped per key, sub[sub_off .. + sub_len). */
+hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
+                              uint64_t* n_payload, uint64_t* n_sub);
 /* Synchronous statistics (makeStatistics). */
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out);
 /* Number of tuples / distinct keys currently stored (synchronous). */
