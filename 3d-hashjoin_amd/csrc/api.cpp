@@ -83,6 +83,11 @@ hj3d_status hj3d_ctx_create(int device, void* stream, hj3d_ctx** out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return HJ3D_EDEVICE;
   if (hipSetDevice(device) != hipSuccess) return HJ3D_EDEVICE;
+  std::string why;
+  if (!runtime_check(&why)) {
+    std::fprintf(stderr, "hj3d_ctx_create: %s\n", why.c_str());
+    return HJ3D_EDEVICE;
+  }
   hj3d_ctx* ctx = new (std::nothrow) hj3d_ctx();
   if (!ctx) return HJ3D_ENOMEM;
   ctx->device = device;
@@ -102,6 +107,7 @@ hj3d_status hj3d_ctx_create(int device, void* stream, hj3d_ctx** out) {
 void hj3d_ctx_destroy(hj3d_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  (void)hj3d_comm_destroy(ctx);
   (void)hipStreamSynchronize(ctx->stream);
   for (auto& b : ctx->scratch) b.release();
   ctx->res.release();

@@ -43,7 +43,12 @@ struct DevBuf {
   template <typename T> T* as() const { return static_cast<T*>(p); }
 };
 
+// comm.hip: false (and why) when two HIP runtimes are mapped into the process
+bool runtime_check(std::string* msg);
+
 }  // namespace hj3d
+
+struct hj3d_comm_state;  // comm.hip: RCCL communicator, exchange stream, tickets
 
 // Opaque handles of the C ABI.
 struct hj3d_ctx {
@@ -80,6 +85,7 @@ struct hj3d_ctx {
     if (e == hipSuccess) e = hipMemsetAsync(ctl.p, 0, ctl.bytes, stream);
     return e;
   }
+  hj3d_comm_state* comm = nullptr;  // hj3d_comm_init
   struct Span { hipEvent_t a, b; };
   std::vector<Span> spans[HJ3D_T_NTIMERS];
   std::vector<hipEvent_t> event_pool;

@@ -132,6 +132,17 @@ def lib():
         "hj3d_expected_fk_join_gen": (st, [p, R, u64, u64, i32, p]),
         "hj3d_gen_exp1_ref": (st, [u64, u64, i32, C.c_double, u32, p, p, i32]),
         "hj3d_gen_exp4_ref": (st, [u32, u32, u32, u32, u32, p, p, C.POINTER(u64)]),
+        "hj3d_runtime_info": (st, [C.c_char_p, u64]),
+        "hj3d_comm_unique_id": (st, [p, C.c_char_p]),
+        "hj3d_comm_init": (st, [p, C.c_char_p, i32, i32]),
+        "hj3d_comm_destroy": (st, [p]),
+        "hj3d_comm_rank": (st, [p, C.POINTER(i32), C.POINTER(i32)]),
+        "hj3d_comm_counts": (st, [p, p, u32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "hj3d_comm_exchange": (st, [p, p, C.POINTER(C.c_int64), p, C.POINTER(C.c_int64), u64, u32,
+                                    C.POINTER(u32)]),
+        "hj3d_comm_wait": (st, [p, u32]),
+        "hj3d_comm_allreduce_u64": (st, [p, p, u64, i32]),
+        "hj3d_comm_allgather": (st, [p, p, p, u64]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -466,6 +477,93 @@ def part_range(num_buckets: int, parts: int, part: int):
     lo, hi = C.c_uint64(), C.c_uint64()
     lib().hj3d_part_range(num_buckets, parts, part, C.byref(lo), C.byref(hi))
     return lo.value, hi.value
+
+
+def runtime_info() -> str:
+    """The HIP runtime (and RCCL) libhj3d.so runs on (hj3d_runtime_info)."""
+    buf = C.create_string_buffer(4096)
+    lib().hj3d_runtime_info(buf, len(buf))
+    return buf.value.decode()
+
+
+RED_SUM, RED_MAX, RED_MIN = 0, 1, 2
+COMM_ID_BYTES = 128
+
+
+class Comm:
+    """libhj3d's RCCL communicator on a Context (hj3d_comm_*): the exchange of the bucket-range
+    partitioned join and the merge of per-rank counters, the same entry points
+    the C++ hosts call. `uid` is the 128-byte id from Comm.unique_id(ctx) on rank 0, handed to the
+    other ranks by any side channel (hj3d.dist.comm_from_torch uses torch.distributed)."""
+
+    def __init__(self, ctx: Context, uid: bytes, rank: int, world: int):
+        if len(uid) != COMM_ID_BYTES:
+            raise ValueError("communicator id must be 128 bytes")
+        self.ctx = ctx
+        ctx._check(lib().hj3d_comm_init(ctx.h, uid, rank, world), "hj3d_comm_init")
+        self.rank, self.world = rank, world
+
+    @staticmethod
+    def unique_id(ctx: Context) -> bytes:
+        buf = C.create_string_buffer(COMM_ID_BYTES)
+        ctx._check(lib().hj3d_comm_unique_id(ctx.h, buf), "hj3d_comm_unique_id")
+        return buf.raw
+
+    def counts(self, counts):
+        """All-to-all of per-destination counts, int64 device tensor [C, world] (row c = the counts
+        hj3d_partition wrote for chunk c): host lists (send[c][p], recv[c][p]). Synchronous."""
+        Cn, P = counts.shape
+        if P != self.world or not counts.is_contiguous():
+            raise ValueError("counts must be a contiguous [chunks, world] int64 tensor")
+        snd = (C.c_int64 * (Cn * P))()
+        rcv = (C.c_int64 * (Cn * P))()
+        self.ctx._check(lib().hj3d_comm_counts(self.ctx.h, counts.data_ptr(), Cn, snd, rcv), "hj3d_comm_counts")
+        return ([list(snd[c * P:(c + 1) * P]) for c in range(Cn)], [list(rcv[c * P:(c + 1) * P]) for c in range(Cn)])
+
+    def exchange(self, send, sc, rc, recv_buf, asynchronous: bool = True):
+        """Grouped send / recv of one chunk of (key, row) pairs (rows of `send` grouped by
+        destination, sc[p] rows for peer p) into recv_buf (rc[p] rows from peer p, in rank order).
+        Returns (received view, ticket or None); wait(ticket) orders the context stream after it."""
+        P = self.world
+        total = int(sum(rc))
+        elem = send.element_size() * (send.shape[1] if send.dim() > 1 else 1)
+        if recv_buf.element_size() * (recv_buf.shape[1] if recv_buf.dim() > 1 else 1) != elem:
+            raise ValueError("send and receive rows differ in size")
+        sca, rca = (C.c_int64 * P)(*sc), (C.c_int64 * P)(*rc)
+        t = C.c_uint32()
+        self.ctx._check(lib().hj3d_comm_exchange(self.ctx.h, send.data_ptr() if send.numel() else None, sca,
+                                                 recv_buf.data_ptr() if recv_buf.numel() else None, rca,
+                                                 recv_buf.shape[0], elem, C.byref(t) if asynchronous else None),
+                        "hj3d_comm_exchange")
+        return recv_buf[:total], (t.value if asynchronous else None)
+
+    def wait(self, ticket: int):
+        self.ctx._check(lib().hj3d_comm_wait(self.ctx.h, ticket), "hj3d_comm_wait")
+
+    def allreduce_u64(self, values, op: int = RED_SUM):
+        """u64 counters reduced over ranks (mod 2^64 for the sum). Synchronous."""
+        torch = _torch()
+        t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in (int(x) & MASK64 for x in values)],
+                         dtype=torch.int64, device=f"cuda:{self.ctx.device}")
+        self.ctx._check(lib().hj3d_comm_allreduce_u64(self.ctx.h, t.data_ptr(), t.numel(), op),
+                        "hj3d_comm_allreduce_u64")
+        self.ctx.sync()
+        return [int(x) & MASK64 for x in t.cpu().tolist()]
+
+    def allgather_u64(self, value: int):
+        torch = _torch()
+        v = int(value) & MASK64
+        dev = f"cuda:{self.ctx.device}"
+        src = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v], dtype=torch.int64, device=dev)
+        dst = torch.empty(self.world, dtype=torch.int64, device=dev)
+        self.ctx._check(lib().hj3d_comm_allgather(self.ctx.h, src.data_ptr(), dst.data_ptr(), 8), "hj3d_comm_allgather")
+        self.ctx.sync()
+        return [int(x) & MASK64 for x in dst.cpu().tolist()]
+
+    def close(self):
+        if self.ctx is not None and getattr(self.ctx, "h", None):
+            lib().hj3d_comm_destroy(self.ctx.h)
+        self.ctx = None
 
 
 class Table:

@@ -2,15 +2,55 @@
 
 One process per GPU. Every rank partitions its local slice of a relation into (key, global
 row) pairs grouped by the owning rank (owner(bucket) = bucket * P / NB; hj3d_partition on the
-GPU), exchanges the per-destination counts, then the pairs, with all_to_all over
-torch.distributed (RCCL over xGMI with backend "nccl"; gloo in the CPU tests). Each rank then
-builds / probes only its own bucket range, so the reference's per-bucket semantics (chain
-order, comparison counts, statistics) are preserved and the counters simply add up.
+GPU), exchanges the per-destination counts, then the pairs. Each rank then builds / probes only
+its own bucket range, so the reference's per-bucket semantics (chain order, comparison counts,
+statistics) are preserved and the counters simply add up.
+
+Two transports behind the same functions:
+- GPU ranks: libhj3d's own RCCL communicator (hj3d.Comm, hj3d_comm_* in include/hj3d.h), the
+  implementation the C++ hosts call too. comm_from_torch() creates it (torch.distributed only
+  carries the 128-byte id from rank 0) and use_comm() routes the functions below through it:
+  counts all-to-all, grouped send / recv of the pairs on the engine's exchange stream (tickets
+  instead of host waits), u64 counter all-reduce / all-gather.
+- Without a communicator: torch.distributed collectives, host-staged under gloo. This is the CPU
+  test transport (tests/test_dist_gloo.py) and the several-ranks-on-one-GPU rehearsal
+  (bench.py --rehearse), which RCCL cannot run ("Duplicate GPU": one rank per device).
 """
 from __future__ import annotations
 
 import torch
 import torch.distributed as dist
+
+
+_comm = None
+
+
+def use_comm(comm) -> None:
+    """Route the exchange and the counter merges of this process through `comm` (hj3d.Comm), or
+    back to torch.distributed with None."""
+    global _comm
+    _comm = comm
+
+
+def comm_from_torch(ctx, group=None):
+    """An hj3d.Comm over the ranks of the initialised torch.distributed group: rank 0 creates the
+    RCCL id, torch.distributed broadcasts it (the only thing it carries), every rank joins."""
+    import hj3d
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    obj = [hj3d.Comm.unique_id(ctx) if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return hj3d.Comm(ctx, obj[0], rank, world)
+
+
+class _Ticket:
+    """work-handle look-alike of an asynchronous hj3d_comm_exchange: wait() orders the engine's
+    stream after the exchange (no host synchronisation)."""
+
+    def __init__(self, comm, t):
+        self.comm, self.t = comm, t
+
+    def wait(self):
+        self.comm.wait(self.t)
 
 
 def _host_staged(group=None) -> bool:
@@ -25,6 +65,13 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
 
     send_counts: int64 tensor [P] on the pairs' device (as written by hj3d_partition).
     Returns the received pairs (a view of recv_buf when it is large enough)."""
+    if _comm is not None:
+        sc, rc = _comm.counts(send_counts.reshape(1, -1).contiguous())
+        total = int(sum(rc[0]))
+        if recv_buf is None or recv_buf.shape[0] < total:
+            recv_buf = torch.empty((max(total, 1), 2), dtype=send_pairs.dtype, device=send_pairs.device)
+        out, _ = _comm.exchange(send_pairs, sc[0], rc[0], recv_buf, asynchronous=False)
+        return out
     world = dist.get_world_size(group)
     if _host_staged(group) and send_pairs.is_cuda:
         rb = recv_buf.cpu() if recv_buf is not None else None
@@ -52,6 +99,8 @@ def exchange_counts(send_counts: torch.Tensor, group=None):
 
     send_counts: int64 [C, P] (row c = hj3d_partition's counts of chunk c). Returns host lists
     (send[c][p], recv[c][p]): recv[c][p] = pairs rank p sends this rank in chunk c."""
+    if _comm is not None:
+        return _comm.counts(send_counts.contiguous())
     world = dist.get_world_size(group)
     C = send_counts.shape[0]
     src = send_counts.t().contiguous()  # [P, C]: the block for destination p is contiguous
@@ -73,6 +122,9 @@ def exchange_pairs_async(send_pairs: torch.Tensor, sc: list[int], rc: list[int],
     total = int(sum(rc))
     if recv_buf.shape[0] < total:
         raise RuntimeError(f"exchange: receive buffer holds {recv_buf.shape[0]} pairs, {total} arrive")
+    if _comm is not None:
+        out, t = _comm.exchange(send_pairs, sc, rc, recv_buf, asynchronous=True)
+        return out, _Ticket(_comm, t)
     out = recv_buf[:total]
     src = send_pairs[: int(sum(sc))]
     if _host_staged(group) and send_pairs.is_cuda:
@@ -89,6 +141,13 @@ def allreduce_stats(st: dict, device) -> dict:
     counts add, extremes take max / min, so the result is the single-table statistics."""
     add = ("nb", "empty", "entries", "distinct", "cc0_sum", "cc0_cnt", "cc1_sum", "cc1_cnt")
     out = dict(zip(add, allreduce_sum_u64([st[k] for k in add], device)))
+    if _comm is not None:
+        import hj3d
+        mx = _comm.allreduce_u64([st["cc0_max"], st["cc1_max"]], hj3d.RED_MAX)
+        cc1_min = st["cc1_min"] if st["cc1_cnt"] else (1 << 64) - 1
+        mn = _comm.allreduce_u64([st["cc0_min"], cc1_min], hj3d.RED_MIN)
+        out.update(cc0_max=mx[0], cc1_max=mx[1], cc0_min=mn[0], cc1_min=mn[1])
+        return out
     for k in ("cc0_max", "cc1_max"):
         out[k] = int(allreduce_max(float(st[k]), device))
     for k in ("cc0_min", "cc1_min"):
@@ -113,6 +172,12 @@ def num_distinct(bitmap: torch.Tensor, or_popcount, group=None) -> int:
     if words % world:
         raise ValueError(f"bitmap words ({words}) must be a multiple of the world size ({world})")
     src = bitmap.reshape(-1)
+    if _comm is not None:
+        recv = torch.empty_like(src)
+        per = [words // world] * world
+        _comm.exchange(src, per, per, recv, asynchronous=False)
+        c = int(or_popcount(recv.view(world, words // world)))
+        return _comm.allreduce_u64([c])[0]
     if _host_staged(group) and src.is_cuda:
         src = src.cpu()
     recv = torch.empty_like(src)
@@ -148,6 +213,8 @@ def num_distinct_rel(ctx, rel, domain: int, group=None) -> int:
 
 def allreduce_sum_u64(values: list[int], device) -> list[int]:
     """Sum u64 counters over ranks (mod 2^64, as the reference's u64 counters would wrap)."""
+    if _comm is not None:
+        return _comm.allreduce_u64(values)
     device = "cpu" if _host_staged() else device
     t = torch.tensor([v - (1 << 64) if v >= (1 << 63) else v for v in values], dtype=torch.int64, device=device)
     dist.all_reduce(t)
@@ -155,6 +222,11 @@ def allreduce_sum_u64(values: list[int], device) -> list[int]:
 
 
 def allreduce_xor_u64(value: int, device) -> int:
+    if _comm is not None:
+        x = 0
+        for v in _comm.allgather_u64(value):
+            x ^= v
+        return x
     device = "cpu" if _host_staged() else device
     world = dist.get_world_size()
     t = torch.tensor([value - (1 << 64) if value >= (1 << 63) else value], dtype=torch.int64, device=device)

@@ -74,6 +74,9 @@ def parse():
     p.add_argument("--chunks", type=int, default=4,
                    help="N>1: S is exchanged in this many chunks, each chunk's all-to-all overlapping the "
                         "previous chunk's probe")
+    p.add_argument("--dist-path", action="store_true",
+                   help="N=1: run the multi-GPU strand (partition, RCCL exchange through libhj3d, bucket-range "
+                        "table, chunked probe) on one GPU (the GPU test of that code path)")
     p.add_argument("--rehearse", action="store_true",
                    help="N>1 on ONE GPU: every rank on cuda:0, gloo exchange staged through host memory "
                         "(checks the multi-GPU code path; the numbers are not a scaling measurement)")
@@ -279,9 +282,10 @@ def main():
     local = 0 if args.rehearse else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    from hj3d import dist as hdist
+    sharded = world > 1 or args.dist_path  # the partition + exchange strand
     if world > 1:
         import torch.distributed as dist
-        from hj3d import dist as hdist
         if args.rehearse:
             dist.init_process_group("gloo")
         else:
@@ -307,6 +311,11 @@ def main():
     emit = not args.no_emit
     ctx = hj3d.Context(local)
     ctx.timing(True)
+    if sharded and not args.rehearse:
+        # the data path (counts, pairs, counter merges) on libhj3d's own RCCL communicator;
+        # torch.distributed only hands over its id and times (barriers, max over ranks). World
+        # size 1 (--dist-path): RCCL ships every chunk to this rank itself.
+        hdist.use_comm(hdist.comm_from_torch(ctx) if world > 1 else hj3d.Comm(ctx, hj3d.Comm.unique_id(ctx), 0, 1))
     packed = args.probe_path == "packed" and plan == "Csr"
     ctx.packed_probe(packed)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
@@ -351,7 +360,7 @@ def main():
     unique, unnest = plan == "Csr", plan != "Csr"
 
     C = max(1, args.chunks)
-    if world == 1:
+    if not sharded:
         table = hj3d.Table(ctx, kind, nb)
         table.reserve(nB)
         out = torch.empty((nS, 2), dtype=torch.int32, device=dev) if emit else None
@@ -385,7 +394,7 @@ def main():
 
     def step(ev):
         ev[0].record()
-        if world == 1:
+        if not sharded:
             table.build(bRel)
             ev[1].record()
             ctx.probe(table, pRel, unique=unique, unnest=unnest, out=out, fetch=False, checksum=state.get("ck", False))
@@ -459,7 +468,7 @@ def main():
     # repeat_mintime (util/measure_helpers.hh:15-41 as main_experiment1.cc:663-699 uses it): >= 8
     # repetitions, doubled while their total is below 300 ms, clear_ht between repetitions
     mintime = None
-    if world == 1 and not args.no_mintime:
+    if not sharded and not args.no_mintime:
         state["ck"] = False  # timed like the K steps: no verification checksums
         n_rep, tot_b, tot_p, i = 8, 0.0, 0.0, 0
         while i < n_rep:
@@ -547,9 +556,9 @@ def main():
     #                   output count (8), sub offset and probe row (4 + 4); + the slices (directory +
     #                   16-B main records) once. The expansion kernels that follow are not in this timer.
     # (N > 1: the probe side is the received pair array, 8 B per tuple.)
-    launches = 1 if world == 1 else C
+    launches = C if sharded else 1
     n = probe_n_local / launches
-    tuple_bytes = 12 if world == 1 else 8
+    tuple_bytes = 8 if sharded else 12
     if unique:
         alg = {kpart: n * (tuple_bytes + 8),
                kprobe: n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4}
@@ -564,7 +573,7 @@ def main():
                           "frac": alg[k] / (ms * 1e-3) / 1e9 / PEAK_HBM_GBS}
     dom = max(kernels, key=lambda k: kernels[k]["avg_ms"])
     traffic, pmc = None, None
-    if world == 1 and plan == "Csr" and args.pmc_json and os.path.exists(args.pmc_json):
+    if not sharded and plan == "Csr" and args.pmc_json and os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
@@ -608,8 +617,10 @@ def main():
             "workload": workload, "config": args.workload,
             "plan": plan, "R_total": nR_tot, "S_total": nS_tot, "R_per_gpu": nR_tot // world,
             "S_per_gpu": nS_tot // world, "num_buckets": nb, "num_dv_Sa": dv,
-            "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if world > 1 else "single GPU",
-            "exchange_chunks": (C if world > 1 else None),
+            "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if sharded else "single GPU",
+            "exchange_chunks": (C if sharded else None),
+            "exchange": ("libhj3d hj3d_comm_* over RCCL" if sharded and not args.rehearse else
+                         "torch.distributed gloo, host-staged (rehearsal)" if sharded else None),
             "rehearsal_one_gpu": bool(args.rehearse),
         },
         "build_ms": build_ms,

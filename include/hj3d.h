@@ -239,6 +239,49 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
 
+/* ---- the exchange itself: RCCL over xGMI, one communicator per context ----
+ * One process (or host thread) per GPU, one context per process. RCCL is resolved at run time: a
+ * librccl already mapped into the process (torch's) is used, else /opt/rocm's (hj3d_runtime_info
+ * names the files). Collective calls must be made by every rank in the same order.
+ *   hj3d_comm_unique_id  rank 0 creates the 128-byte communicator id; the host hands it to the
+ *                        other ranks by any side channel (torch.distributed broadcast, a file, MPI);
+ *   hj3d_comm_init       every rank joins (synchronous; collective);
+ *   hj3d_comm_counts     all-to-all of per-destination counts of `chunks` partitioned chunks at once:
+ *                        counts_dev = device i64 [chunks][world] (the counts hj3d_partition wrote,
+ *                        one row per chunk); send_host / recv_host = host i64 [chunks][world],
+ *                        recv[c][p] = elements rank p sends this rank in chunk c (synchronous: the
+ *                        one host synchronisation of an exchange strand; collective);
+ *   hj3d_comm_exchange   grouped send / recv of one chunk: send_dev holds send_counts[p] elements of
+ *                        elem_bytes for every peer p back to back (hj3d_partition's layout), recv_dev
+ *                        receives recv_counts[p] elements from every peer in rank order. A receive
+ *                        total above recv_cap returns HJ3D_EOVERFLOW BEFORE the collective: every
+ *                        rank knows its totals from hj3d_comm_counts, so size recv_dev from them
+ *                        (a rank that skips the call leaves its peers waiting). ticket == NULL:
+ *                        enqueued on the context stream. ticket != NULL: enqueued on the context's
+ *                        exchange stream after the work already on the context stream, so probes of
+ *                        earlier chunks overlap it; hj3d_comm_wait(ticket) orders the context stream
+ *                        after it (tickets recycle after 64 exchanges). Collective;
+ *   hj3d_comm_allreduce_u64 / hj3d_comm_allgather  merge the per-rank result slots and statistics
+ *                        (u64 counters add, extremes max / min; xor via all-gather), on the context
+ *                        stream. Collective. */
+#define HJ3D_COMM_ID_BYTES 128
+enum { HJ3D_RED_SUM = 0, HJ3D_RED_MAX = 1, HJ3D_RED_MIN = 2 };
+hj3d_status hj3d_comm_unique_id(hj3d_ctx* ctx, uint8_t* id);
+hj3d_status hj3d_comm_init(hj3d_ctx* ctx, const uint8_t* id, int rank, int world);
+hj3d_status hj3d_comm_destroy(hj3d_ctx* ctx);
+hj3d_status hj3d_comm_rank(const hj3d_ctx* ctx, int* rank, int* world);
+hj3d_status hj3d_comm_counts(hj3d_ctx* ctx, const void* counts_dev, uint32_t chunks, int64_t* send_host,
+                             int64_t* recv_host);
+hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_t* send_counts, void* recv_dev,
+                               const int64_t* recv_counts, uint64_t recv_cap, uint32_t elem_bytes,
+                               uint32_t* ticket);
+hj3d_status hj3d_comm_wait(hj3d_ctx* ctx, uint32_t ticket);
+hj3d_status hj3d_comm_allreduce_u64(hj3d_ctx* ctx, void* buf_dev, uint64_t n, int op);
+hj3d_status hj3d_comm_allgather(hj3d_ctx* ctx, const void* send_dev, void* recv_dev, uint64_t bytes);
+/* Which HIP runtime (and RCCL) this library runs on: file names and versions, as text. hj3d_ctx_create
+ * fails with HJ3D_EDEVICE (reason on stderr) when two HIP runtimes are mapped into the process. */
+hj3d_status hj3d_runtime_info(char* buf, uint64_t cap);
+
 /* ---- #dv pre-pass (the number of distinct join-attribute values sizes the build-on-S.a plans:
  * NB = #dv(S.a) / b, main_experiment1.cc:453-454 counts it with an unordered_set, 875, 1001,
  * 1214 use it). One GPU: key_bitmap + or_popcount with rows = 1. Multi-GPU (SURVEY §8e step 1,

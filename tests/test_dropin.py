@@ -139,3 +139,40 @@ def test_gpu_pertuple_probe_api_and_host_unnest():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     for name in PERTUPLE_CHECKS:
         assert f"PASS {name}" in r.stdout, r.stdout
+
+
+# ---- tests/cpp/dist_join.cc: the multi-GPU strand from C++ on the C ABI (hj3d_comm_*) ----
+DIST_JOIN = os.path.join(ROOT, "3d-hashjoin_amd", "bin", "dist_join")
+
+
+def test_dist_join_program_builds_and_fails_loudly_without_gpu():
+    r = subprocess.run(["make", "-C", os.path.join(ROOT, "3d-hashjoin_amd"), "bin/dist_join"],
+                       capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    if _cpu_only():
+        r = subprocess.run([DIST_JOIN, "1024", "8192", "Csr"], capture_output=True, text=True, timeout=60)
+        assert r.returncode != 0 and "no CPU path" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(DIST_JOIN), reason="dist_join not built")
+@pytest.mark.parametrize("plan", ["Csr", "Nsr"])
+def test_gpu_dist_join_cpp_host_equals_reference(plan):
+    """The C++ host's partition -> RCCL exchange (libhj3d) -> build / 3-chunk probe -> merge strand at
+    world size 1, on the reference's relations: every counter, checksum and statistic equals the
+    reference binary's fixture (tests/golden/exp1_R1048576_S8388608_uni.json)."""
+    import json
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "exp1_R1048576_S8388608_uni.json")))
+    r = subprocess.run([DIST_JOIN, str(g["nR"]), str(g["nS"]), plan, "3"], capture_output=True, text=True,
+                       timeout=300, env=dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0"))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("c_build=")]  # RCCL may print banners
+    assert len(line) == 1, r.stdout[-3000:]
+    got = {k: int(v) for k, v in (kv.split("=") for kv in line[0].split())}
+    ref = g["plans"][plan]
+    assert got["c_build"] == ref["c_build"] and got["c_top"] == ref["c_top"] and got["c_cmp"] == ref["c_cmp"]
+    for k in ("n", "sum_a", "sum_b", "sum_h", "xor_h"):
+        assert got[k] == ref["out"][k], k
+    for k in ("nb", "empty", "entries", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt", "cc1_min", "cc1_max", "cc1_sum",
+              "cc1_cnt"):
+        assert got[k] == ref["stats"][k], k

@@ -6,6 +6,11 @@ counters, output checksums and sharded-table statistics must equal the fixture t
 binary wrote for the same relations (tests/golden/exp1_R1048576_S8388608_uni.json): the
 verification step of bench.py compares them and the run fails otherwise.
 
+The exchange as the product runs it: libhj3d's own RCCL communicator (hj3d_comm_*) at world size 1
+(the box has one GPU): the partition -> count all-to-all -> asynchronous pair exchange (tickets) ->
+build / chunked probe strand, its merge collectives, bench.py --dist-path, and the refusal of a
+short receive buffer before the collective. tests/test_dropin.py runs the same strand from C++.
+
 Also: output overflow of an accumulated, non-dense probe strand is reported (HJ3D_EOVERFLOW)."""
 import json
 import os
@@ -73,3 +78,115 @@ def test_accumulated_unnest_overflow_is_reported(ctx):
     # a new strand starts clean
     ctx.probe(t, hj3d.Rel(S, 1), unnest=True, out=big, fetch=False)
     assert not ctx.probe_result().overflow
+
+
+# ---- libhj3d's own RCCL exchange (hj3d_comm_*), world size 1 on the box's one GPU ----
+STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
+             "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
+
+
+@pytest.fixture(scope="module")
+def comm(ctx):
+    import hj3d
+    c = hj3d.Comm(ctx, hj3d.Comm.unique_id(ctx), 0, 1)
+    yield c
+    c.close()
+
+
+def test_runtime_is_single(ctx):
+    """One HIP runtime mapped (torch's, shared by libhj3d.so): hj3d_ctx_create checks it."""
+    import hj3d
+    info = hj3d.runtime_info()
+    assert "hip mapped=1" in info, info
+
+
+@pytest.mark.parametrize("plan", ["Csr", "Nsr"])
+def test_rccl_exchange_strand_equals_reference(ctx, comm, plan):
+    """The multi-GPU strand of bench.py on libhj3d's communicator: hj3d_partition -> hj3d_comm_counts
+    (3 probe chunks in one collective) -> hj3d_comm_exchange (asynchronous, on the exchange stream,
+    tickets) -> explicit-row build / accumulated chunked probe, on the reference's relations
+    (fixture exp1_R1048576_S8388608_uni): every counter, checksum and statistic equals the
+    reference binary's. World size 1: RCCL sends each chunk to this rank itself."""
+    import json
+    import torch
+    import hj3d
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "exp1_R1048576_S8388608_uni.json")))
+    nR, nS = g["nR"], g["nS"]
+    R, S = hj3d.exp1_relations_ref(nR, nS)
+    nb = nR
+    P, C = 1, 3
+    unique, unnest = plan == "Csr", plan == "Nsr"
+    kind = hj3d.HJ3D_CHAIN if plan == "Csr" else hj3d.HJ3D_NESTED
+    dev = "cuda"
+    # build side
+    sendB = torch.empty((nR, 2), dtype=torch.int32, device=dev)
+    cntB = torch.zeros((1, P), dtype=torch.int64, device=dev)
+    ctx.partition(hj3d.Rel(R, 0), nb, P, sendB, cntB[0])
+    scB, rcB = comm.counts(cntB)
+    assert scB == [[nR]] and rcB == [[nR]]
+    recvB = torch.empty((nR, 2), dtype=torch.int32, device=dev)
+    rB, _ = comm.exchange(sendB, scB[0], rcB[0], recvB, asynchronous=False)
+    t = hj3d.Table(ctx, kind, nb, *hj3d.part_range(nb, P, 0))
+    t.build(hj3d.Rel(rB, key_word=0, row_word=1))
+    # probe side in chunks, all counts in one collective, exchanges in flight together
+    sb = [nS * c // C for c in range(C + 1)]
+    sendP = torch.empty((nS, 2), dtype=torch.int32, device=dev)
+    cntP = torch.zeros((C, P), dtype=torch.int64, device=dev)
+    for c in range(C):
+        ctx.partition(hj3d.Rel(S[sb[c]:sb[c + 1]], 1, row_base=sb[c]), nb, P, sendP[sb[c]:sb[c + 1]], cntP[c])
+    scP, rcP = comm.counts(cntP)
+    assert [r[0] for r in rcP] == [sb[c + 1] - sb[c] for c in range(C)]
+    recvP = torch.empty((nS, 2), dtype=torch.int32, device=dev)
+    pend, off = [], 0
+    for c in range(C):
+        v, tk = comm.exchange(sendP[sb[c]:sb[c + 1]], scP[c], rcP[c], recvP[off:])
+        off += v.shape[0]
+        pend.append((v, tk))
+    for c, (v, tk) in enumerate(pend):
+        comm.wait(tk)
+        ctx.probe(t, hj3d.Rel(v, key_word=0, row_word=1), unique=unique, unnest=unnest, fetch=False,
+                  accumulate=c > 0)
+    r = ctx.probe_result()
+    ref = g["plans"][plan]
+    assert r.n_cmps == ref["c_cmp"]
+    n_top = r.n_out
+    assert n_top == ref["c_top"]
+    got = {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_h": r.sum_h, "xor_h": r.xor_h}
+    assert got == {k: ref["out"][k] for k in got}
+    # the counter merge of the multi-GPU verification (identity at world size 1)
+    assert comm.allreduce_u64([r.n_cmps, 2**64 - 1]) == [r.n_cmps, 2**64 - 1]
+    assert comm.allreduce_u64([7], hj3d.RED_MAX) == [7] and comm.allgather_u64(r.xor_h) == [r.xor_h]
+    st = t.stats()
+    assert {k: st[k] for k in STAT_KEYS} == {k: ref["stats"][k] for k in STAT_KEYS}
+    t.close()
+
+
+def test_rccl_exchange_short_buffer_is_refused(ctx, comm):
+    """A receive buffer below the exchanged total is refused before the collective (HJ3D_EOVERFLOW)."""
+    import torch
+    import hj3d
+    send = torch.zeros((100, 2), dtype=torch.int32, device="cuda")
+    recv = torch.empty((99, 2), dtype=torch.int32, device="cuda")
+    with pytest.raises(hj3d.Hj3dError) as e:
+        comm.exchange(send, [100], [100], recv, asynchronous=False)
+    assert e.value.status == hj3d.HJ3D_EOVERFLOW
+    # the communicator is still usable
+    v, _ = comm.exchange(send[:99], [99], [99], recv, asynchronous=False)
+    assert v.shape[0] == 99
+
+
+@pytest.mark.parametrize("plan", ["Csr", "Nsr", "Nrs"])
+def test_bench_dist_path_on_rccl_equals_reference(plan, tmp_path):
+    """bench.py's multi-GPU strand with the exchange on libhj3d's RCCL communicator (--dist-path,
+    world size 1): the verification step compares with the reference binary's fixture."""
+    out = tmp_path / "line.json"
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--dist-path", "--workload", "D",
+           "--nR", "1048576", "--nS", "8388608", "--plan", plan, "--steps", "2", "--warmup", "1", "--chunks", "3",
+           "--json-out", str(out), "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    line = json.loads(out.read_text())
+    v = line["verification"]
+    assert line["verified_bit_exact"], v
+    assert "exp1_R1048576_S8388608_uni.json" in v["against"]
+    assert line["config"]["exchange"].startswith("libhj3d")
