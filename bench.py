@@ -577,7 +577,7 @@ def main():
         try:
             with open(args.pmc_json) as f:
                 pm = json.load(f)
-            if pm.get("nS") == nS and pm.get("nR") == nR and pm.get("emit") == emit:
+            if pm.get("workload", "B") == "B" and pm.get("nS") == nS and pm.get("nR") == nR and pm.get("emit") == emit:
                 pmc = pm.get("kernels", {})
                 traffic = (pmc.get(dom) or {}).get("traffic_bytes_per_launch")
         except (OSError, ValueError):
@@ -659,6 +659,27 @@ def main():
         torch.distributed.destroy_process_group()
     if not verified:
         raise SystemExit(f"verification failed: {verify}")
+
+
+def _load_pmc(path, workload):
+    """The PMC summary at `path` if it was taken on `workload` (scripts/pmc_summary.py)."""
+    import glob
+    cands = ([path] if path else []) + sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")),
+                                              reverse=True)
+    pm = None
+    for path in cands:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload", "B") == workload:
+            pm = d
+            break
+    if pm is None:
+        return None
+    pm["_path"] = os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))
+    return pm
 
 
 def main_single_config(args):
@@ -798,6 +819,23 @@ def main_single_config(args):
                      "build_achieved": build_bytes / (build_ms * 1e-3) / 1e9},
         "counters": counters, "verification": verify, "verified_bit_exact": verified, "cpu_baseline": None,
     }
+    # HBM traffic of the phases from a PMC summary of this workload (scripts/gpu_pmc.sh +
+    # scripts/pmc_summary.py --workload C|E): bytes per step of each phase's kernels
+    pm = _load_pmc(args.pmc_json, args.workload)
+    if pm:
+        ph_build = ("k_rp_hist", "k_rp_scatter", "k_nagg", "k_nagg_mains", "k_rs_scatter", "k_rs_hist")
+        ph_probe = ("k_rp_part1", "k_rn_probe_seg", "k_expand_light", "k_expand_heavy_flat", "k_ndu_seg", "k_ndu",
+                    "k_ndu_heavy")
+        tr = {k: d.get("traffic_bytes_per_launch") for k, d in pm["kernels"].items()
+              if d.get("traffic_bytes_per_launch")}
+        line["roofline"]["traffic"] = sum(v for k, v in tr.items() if k in ph_probe) or None
+        line["roofline"]["build_traffic"] = sum(v for k, v in tr.items() if k in ph_build) or None
+        line["roofline"]["build_alg_bytes"] = build_bytes
+        line["roofline"]["probe_alg_bytes"] = probe_bytes
+        line["roofline"]["kernel_traffic"] = {
+            k: {"traffic": v, "fetch": pm["kernels"][k].get("fetch_bytes"), "write": pm["kernels"][k].get("write_bytes")}
+            for k, v in tr.items() if k in ph_build + ph_probe}
+        line["roofline"]["pmc_source"] = pm.get("_path")
     if args.workload == "C" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_reference_nrs(max(nR // 10, 1), max(nS // 10, 1), args.theta,
                                                           args.cpu_reps)

@@ -22,8 +22,13 @@ import os
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ("k_pk_probe", "k_pk_part", "k_pk_build", "k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe", "k_rp_scatter", "k_rp_hist", "k_rp_build2", "k_rp_build",
-           "k_sort_small_buckets", "k_scan_tiles")
+# longer names first: a name is matched as a substring of the mangled kernel name
+KERNELS = ("k_pk_probe", "k_pk_part", "k_pk_build", "k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe",
+           "k_rp_scatter", "k_rp_hist", "k_rp_build3", "k_rp_build2", "k_rp_build", "k_sort_small_buckets",
+           "k_scan_tiles",
+           # nested (config C) and experiment-4 (config E) kernels
+           "k_nagg_mains", "k_nagg_order", "k_nagg_rebase", "k_nagg", "k_rn_probe_seg", "k_expand_light",
+           "k_expand_heavy_flat", "k_heavy_offsets", "k_ndu_seg", "k_ndu_heavy", "k_ndu", "k_rs_scatter", "k_rs_hist")
 
 
 def short(name):
@@ -43,6 +48,7 @@ def main():
     ap.add_argument("--nS", type=int, default=100_000_000)
     ap.add_argument("--emit", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--workload", default="B", help="bench.py --workload of the profiled run (B, C, E)")
     a = ap.parse_args()
     src = os.path.join(ROOT, "gpurun_out", f"pmc_{a.tag}")
     # (kernel, counter) -> list of (grid, value) over dispatches
@@ -80,8 +86,9 @@ def main():
             d["issue_stall_frac"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
             d["active_frac"] = d.get("SQ_ACTIVE_INST_ANY", 0) / wc
     out = {
-        "tag": a.tag, "nR": a.nR, "nS": a.nS, "emit": bool(a.emit),
-        "command": "rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline",
+        "tag": a.tag, "workload": a.workload, "nR": a.nR, "nS": a.nS, "emit": bool(a.emit),
+        "command": "rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
+                   + ("" if a.workload == "B" else f" --workload {a.workload}"),
         "corrections": "FETCH_SIZE, WRITE_SIZE in KiB; FETCH_SIZE x2 (gfx950 streaming-read undercount); "
                        "WRITE_SIZE as reported (8-B/lane stores uncalibrated)",
         "kernels": kern,
