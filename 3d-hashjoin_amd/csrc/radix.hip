@@ -54,28 +54,40 @@ inline FastDiv make_div(uint32_t d) {
   return f;
 }
 
+// Partition sizes per scatter workgroup: workgroup g of the G = gridDim.x persistent workgroups
+// counts the tiles g, g + G, ... that k_rp_scatter's workgroup g will write, so one column per
+// workgroup (hist[p * G + g]) instead of one per tile: P x G counters, whose partition-major
+// write-out is then small (a per-tile column costs a 64-B line per counter: P x ntiles lines).
 __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                      uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist) {
   __shared__ uint32_t cnt[kMaxParts];
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
   __syncthreads();
-  const uint64_t base = uint64_t(blockIdx.x) * kPTile;
   uint32_t key[kPRounds];
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
-    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
+    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
     key[j] = i < r.n ? r.key(i) : 0u;
   }
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    uint32_t bl[kPRounds];
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-    if (i < r.n) {
-      const uint32_t bl = fm.mod(murmur32(key[j])) - lo;
-      if (bl < nbl) atomicAdd(&cnt[fw.div(bl)], 1u);
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = uint64_t(tile) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
+      bl[j] = i < r.n ? fm.mod(murmur32(key[j])) - lo : nbl;
     }
+    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
+      key[j] = i < r.n ? r.key(i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kPRounds; ++j)
+      if (bl[j] < nbl) atomicAdd(&cnt[fw.div(bl[j])], 1u);
   }
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * ntiles + blockIdx.x] = cnt[p];
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * gridDim.x + blockIdx.x] = cnt[p];
 }
 
 template <int BLOCK = kJBlock>
@@ -101,11 +113,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
   }
+  // this workgroup's write cursor per partition (its column of the scanned k_rp_hist counts)
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = offs[uint64_t(p) * gridDim.x + blockIdx.x];
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
-      loc[p] = 0;
-      gb[p] = offs[uint64_t(p) * ntiles + tile];
-    }
+    for (uint32_t p = threadIdx.x; p < P; p += kPBlock) loc[p] = 0;
     const uint64_t base = uint64_t(tile) * kPTile;
     uint32_t rk[kPRounds];
     __syncthreads();
@@ -142,12 +153,15 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
       out[gb[p] + (k - loc[p])] = e;
     }
     __syncthreads();
+    for (uint32_t p = threadIdx.x; p < P; p += kPBlock)  // advance the cursors by the tile's runs
+      gb[p] += (p + 1 < P ? loc[p + 1] : m) - loc[p];
+    __syncthreads();
   }
 }
 
-__global__ void k_rp_starts(const uint32_t* __restrict__ offs, uint32_t ntiles, uint32_t P, uint32_t* __restrict__ ps) {
+__global__ void k_rp_starts(const uint32_t* __restrict__ offs, uint32_t G, uint32_t P, uint32_t* __restrict__ ps) {
   for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p <= P; p += gridDim.x * blockDim.x)
-    ps[p] = offs[uint64_t(p) * ntiles];
+    ps[p] = offs[uint64_t(p) * G];
 }
 
 // Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. BLOCK threads.
@@ -1038,25 +1052,26 @@ Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
 hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
                            uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1) {
   hipError_t e;
-  const uint64_t hn = uint64_t(pl.P) * pl.ntiles + 1;
+  // G persistent workgroups in both passes, one histogram column per workgroup
+  const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
+  const uint64_t hn = uint64_t(pl.P) * g + 1;
   if ((e = ctx->scratch[kScrPHist].ensure(hn * sizeof(uint32_t))) != hipSuccess) return e;
   uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
   const RelView v = view_of(r);
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
   if (r.n) {
     PhaseTimer tm(ctx, t_hist);
-    hipLaunchKernelGGL(k_rp_hist, dim3(pl.ntiles), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
-                       pl.ntiles, hist);
+    hipLaunchKernelGGL(k_rp_hist, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P, pl.ntiles,
+                       hist);
   }
   if ((e = exclusive_scan_u32(ctx, hist, hist, hn - 1, s)) != hipSuccess) return e;
   if (r.n) {
     PhaseTimer tm(ctx, t_scatter);
-    const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
     hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
                        pl.ntiles, hist, out);
   }
   if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
-  hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, pl.ntiles, pl.P, ps);
+  hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, g, pl.P, ps);
   return hipGetLastError();
 }
 
