@@ -84,8 +84,9 @@ __device__ __forceinline__ void pk_ovf_append(bool me, uint2 e, uint2* __restric
 // thread p carries slice p's < 16 leftover pairs in registers. SEL: a one-word selection fused in.
 // Memory ordering: vmcnt counts loads and stores together, in issue order, so a load can only be
 // waited for together with every older store. The keys of tile t+2 are therefore loaded (always,
-// clamped at the end: a fixed number of loads) right after tile t's stage is built, two tiles ahead:
-// waiting for tile t+1's keys then waits for tile t-1's region stores, never for tile t's.
+// clamped at the end: a fixed number of loads) right after tile t's stage is built; by default the
+// next tile's (HJ3D_PK_AHEAD = 1), with HJ3D_PK_AHEAD = 2 tile t+2's, so that waiting for tile t+1's
+// keys waits for tile t-1's region stores, never for tile t's (measured slower: register spills).
 template <bool IMPLICIT, bool SEL>
 __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint32_t ntiles, uint32_t cap,
                                                       uint2* __restrict__ region, uint32_t* __restrict__ counts,
