@@ -113,6 +113,7 @@ void hj3d_ctx_destroy(hj3d_ctx* ctx) {
   ctx->res.release();
   ctx->misc.release();
   ctx->ctl.release();
+  ctx->scan_status.release();
   for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -286,14 +287,25 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   } else {
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
                                                   : hipErrorNotSupported;
-    if (e == hipErrorNotSupported && !ctx->nested_sort) e = nested_build_agg(ctx, t, *build, ctx->stream);
+    bool agg = false;
+    if (e == hipErrorNotSupported && !ctx->nested_sort) {
+      e = nested_build_agg(ctx, t, *build, ctx->stream);
+      agg = e == hipSuccess;
+    }
     if (e == hipErrorNotSupported) e = nested_build(ctx, t, *build, ctx->stream);
-    // the partitioned probe sizes its LDS slices by the number of main records
-    t->n_mains = 0;
-    if (e == hipSuccess)
-      e = hipMemcpyAsync(&t->n_mains, t->counts.as<uint64_t>() + 1, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                         ctx->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    // the partitioned probe sizes its LDS slices by the number of main records: counts read once
+    // after the build (word 1 = main records; word 3 = the aggregation build's give-up flag)
+    uint64_t hc[4] = {0, 0, 0, 0};
+    auto read_counts = [&]() {
+      hipError_t x = hipMemcpyAsync(hc, t->counts.p, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream);
+      return x == hipSuccess ? hipStreamSynchronize(ctx->stream) : x;
+    };
+    if (e == hipSuccess) e = read_counts();
+    if (e == hipSuccess && agg && uint32_t(hc[3]) != 0) {  // a key range too dense for the LDS table
+      e = nested_build(ctx, t, *build, ctx->stream);
+      if (e == hipSuccess) e = read_counts();
+    }
+    t->n_mains = e == hipSuccess ? hc[1] : 0;
   }
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");

@@ -555,13 +555,16 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
                              out, out_cap);
     }
   };
-  // the walk: probe(v, valid mask, wave-local stream offset of the lane's item 0)
-  auto walk = [&](auto&& probe) __attribute__((always_inline)) {
+  // the walk: probe(v, valid mask, wave-local stream offset of the lane's item 0); stage() runs
+  // (followed by a barrier) once the first chunk's loads are issued, so their latency overlaps it
+  auto walk = [&](auto&& stage, auto&& probe) __attribute__((always_inline)) {
     constexpr uint32_t kChunk = 64 * kItems;
     uint64_t cur[kItems];
     if (flat) {
+      if (wtotal) load_flat(cur, 0);
+      stage();
+      __syncthreads();
       if (wtotal == 0) return;
-      load_flat(cur, 0);
       for (uint32_t f0 = 0; f0 < wtotal; f0 += kChunk) {
         uint64_t nxt[kItems];
         load_flat(nxt, min(f0 + kChunk, (wtotal - 1) & ~(kChunk - 1)));
@@ -574,6 +577,8 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
       }
     } else {
       load_reg(cur, r, qq, len);
+      stage();
+      __syncthreads();
       while (r < nr) {
         uint32_t nr_ = r, nq = qq + kChunk, nl = len;
         while (nr_ < nr && nq >= nl) {
@@ -596,16 +601,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     }
   };
   if (fits) {
-    pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent);
-    __syncthreads();
-    walk([&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
-      pk_probe_items<MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
-    });
+    walk([&]() __attribute__((always_inline)) { pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent); },
+         [&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+           pk_probe_items<MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
+         });
   } else {
-    __syncthreads();
-    walk([&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
-      probe_hbm_chunk(v, valid, bbase + wpre + srel);
-    });
+    walk([&]() __attribute__((always_inline)) {},
+         [&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+           probe_hbm_chunk(v, valid, bbase + wpre + srel);
+         });
   }
   // overflow pairs {h, row} (runs that did not fit their region): chunks of 1024 claimed by any
   // workgroup that is done with its own slice; output slots from the same cursor

@@ -312,7 +312,9 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
     if (same && radix_nested_applicable(ctx, ts, r.n) && radix_nested_applicable(ctx, tt, r.n)) {
       const double fill = double(ts->n_mains + tt->n_mains) / double(ts->nb_local);
       ProbeParts pp;
-      e = radix_partition_probe(ctx, ts, r, uint32_t(0.8 * kProbeLdsWords / (2.0 + 4.0 * fill)), &pp, s);
+      // no output: the regions' output slots are not needed
+      e = radix_partition_probe(ctx, ts, r, uint32_t(0.8 * kProbeLdsWords / (2.0 + 4.0 * fill)), &pp, s, nullptr,
+                                nullptr, false);
       if (e == hipSuccess) {
         const uint32_t nblocks = pp.P * pp.splits;
         hipLaunchKernelGGL(k_ndu_seg<true>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,

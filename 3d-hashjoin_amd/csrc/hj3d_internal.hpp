@@ -50,6 +50,9 @@ bool runtime_check(std::string* msg);
 
 struct hj3d_comm_state;  // comm.hip: RCCL communicator, exchange stream, tickets
 
+// ctl word (u64 index) of exclusive_scan_u32's tile ticket; words 0..4 belong to chain_pk.hip
+constexpr int kCtlScanTicket = 6;
+
 // Opaque handles of the C ABI.
 struct hj3d_ctx {
   int device = 0;
@@ -79,6 +82,8 @@ struct hj3d_ctx {
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
+  uint32_t scan_epoch = 0;  // tags the look-back status words of exclusive_scan_u32 (scan.hip)
+  hj3d::DevBuf scan_status;  // its per-tile status words (no other use)
   hipError_t ensure_ctl() {
     if (ctl.p) return hipSuccess;
     hipError_t e = ctl.ensure(128 * sizeof(uint64_t));  // 8 control words; [64, 128): store sink
@@ -206,8 +211,11 @@ struct ProbeParts {
   const uint2* ovf = nullptr;
   const unsigned long long* novf = nullptr;
 };
+// slots = false: the caller never writes output (the dense output slots of the regions, a
+// transpose + scan of the region counts, are not computed; pp->seg is then undefined)
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
-                                 hipStream_t s, const SelArgs* sel = nullptr, unsigned long long** npass = nullptr);
+                                 hipStream_t s, const SelArgs* sel = nullptr, unsigned long long** npass = nullptr,
+                                 bool slots = true);
 // chain_pk.hip: the unique chaining probe on packed pairs (partitioner + probe, two launches; the
 // result slot is set, or added to with HJ3D_PROBE_ACCUMULATE, by the probe kernel itself: no fill
 // before it). hipErrorNotSupported when the geometry does not pack (use radix_probe).

@@ -299,42 +299,59 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
 }
 
-// order[i] = the partition with the i-th most pairs (bitonic sort of size << 11 | p in LDS, one
-// workgroup, P <= 2048): k_nagg takes its partitions largest first, so a Zipf hot key's
-// partition starts in the first wave of workgroups instead of extending the tail.
+// order = the partitions by size class, heavy first (> 8x the mean pairs, then > 2x, then the
+// rest), each class in index order: k_nagg takes its partitions in this order, so a Zipf hot
+// key's partition starts in the first wave of workgroups instead of extending the tail. One
+// workgroup, P <= 2048 (a stable three-way split by block scans; a full sort by size cost 27 us).
 __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict__ ps, uint32_t P,
                                                      uint32_t* __restrict__ order) {
-  __shared__ uint64_t a[2048];
-  for (uint32_t i = threadIdx.x; i < 2048; i += 1024)
-    a[i] = i < P ? (uint64_t(ps[i + 1] - ps[i]) << 11) | i : 0ull;  // padding sorts last
-  __syncthreads();
-  for (uint32_t k = 2; k <= 2048; k <<= 1) {
-    for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-      for (uint32_t i = threadIdx.x; i < 2048; i += 1024) {
-        const uint32_t l = i ^ j;
-        if (l > i) {
-          const bool desc = (i & k) == 0;  // descending overall
-          const uint64_t x = a[i], y = a[l];
-          if (desc ? x < y : x > y) {
-            a[i] = y;
-            a[l] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  __shared__ uint32_t wsum[16];
+  __shared__ uint32_t base;
+  const uint32_t mean = P ? (ps[P] - ps[0]) / P : 0u;
+  uint32_t cls[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {  // thread t holds partitions 2t, 2t + 1
+    const uint32_t p = 2 * threadIdx.x + k;
+    const uint32_t sz = p < P ? ps[p + 1] - ps[p] : 0u;
+    cls[k] = p >= P ? 3u : sz > 8u * mean ? 0u : sz > 2u * mean ? 1u : 2u;
   }
-  for (uint32_t i = threadIdx.x; i < P; i += 1024) order[i] = uint32_t(a[i] & 2047u);
+  if (threadIdx.x == 0) base = 0;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  for (uint32_t c = 0; c < 3; ++c) {
+    const uint32_t a0 = cls[0] == c, a1 = cls[1] == c, t = a0 + a1;
+    uint32_t wt;
+    const uint32_t wpre = wave_excl_scan(t, &wt);
+    if (lane == 0) wsum[wid] = wt;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      pre += w < wid ? wsum[w] : 0u;
+      tot += wsum[w];
+    }
+    const uint32_t at = base + pre + wpre;
+    if (a0) order[at] = 2 * threadIdx.x;
+    if (a1) order[at + a0] = 2 * threadIdx.x + 1;
+    __syncthreads();
+    if (threadIdx.x == 0) base += tot;
+    __syncthreads();
+  }
 }
 
 // off[b] += first main of b's partition; main records moved to their final slots.
+// k_nagg_rebase / k_nagg_mains / k_nagg_counts run only when no partition gave up (`fail`: the
+// sort build replaces the table then; the host checks the flag once, after the whole build).
 __global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ off, uint32_t nbl,
-                                                        const uint32_t* __restrict__ mbase) {
+                                                        const uint32_t* __restrict__ mbase,
+                                                        const uint32_t* __restrict__ fail) {
+  if (*fail) return;
   for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[b / kAggW];
 }
 
 __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
-                                                       const uint32_t* __restrict__ mbase, uint4* __restrict__ mains) {
+                                                       const uint32_t* __restrict__ mbase, uint4* __restrict__ mains,
+                                                       const uint32_t* __restrict__ fail) {
+  if (*fail) return;
   const uint32_t p = blockIdx.x;
   const uint32_t n = mbase[p + 1] - mbase[p];
   for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[mbase[p] + i] = mtmp[ps[p] + i];
@@ -342,6 +359,7 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
 
 __global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t P,
                               uint32_t nbl, uint32_t* __restrict__ off, uint64_t* __restrict__ counts) {
+  if (reinterpret_cast<const uint32_t*>(counts + 3)[0]) return;  // fail flag
   counts[0] = ps[P];
   counts[1] = mbase[P];
   off[nbl] = mbase[P];
@@ -383,13 +401,11 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   hipLaunchKernelGGL(k_nagg, dim3(P), dim3(kAggBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
                      uint32_t(t->desc.num_buckets), off, mtmp, t->sub.as<uint32_t>(), dcount,
                      reinterpret_cast<unsigned long long*>(counts + 2), fail, order);
-  uint32_t hfail = 0;
-  if ((e = hipMemcpyAsync(&hfail, fail, sizeof(hfail), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
-  if (hfail) return hipErrorNotSupported;  // table untouched apart from scratch: the caller sorts
+  // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
+  // and the caller, which reads the counts once after the build, runs the sort build instead
   if ((e = exclusive_scan_u32(ctx, dcount, dcount, P, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl, dcount);
-  hipLaunchKernelGGL(k_nagg_mains, dim3(P), dim3(kBlock), 0, s, mtmp, ps, dcount, t->main.as<uint4>());
+  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl, dcount, fail);
+  hipLaunchKernelGGL(k_nagg_mains, dim3(P), dim3(kBlock), 0, s, mtmp, ps, dcount, t->main.as<uint4>(), fail);
   hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(1), 0, s, ps, dcount, P, nbl, off, counts);
   t->n_build = n;
   return hipGetLastError();

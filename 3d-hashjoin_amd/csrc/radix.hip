@@ -1201,7 +1201,7 @@ void launch_seg_any(const SegLaunch& L, bool unique, bool ck, uint2* out, uint64
 }  // namespace
 
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
-                                 hipStream_t s, const SelArgs* sel, unsigned long long** npass) {
+                                 hipStream_t s, const SelArgs* sel, unsigned long long** npass, bool slots) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;
   if (W < 64) W = 64;
@@ -1261,8 +1261,10 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
                          nbl, pl.fw, P, pl.ntiles, uint32_t(cap), region, counts, ovf, novf);
     }
   }
-  hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, G, P, seg);
-  if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
+  if (slots) {
+    hipLaunchKernelGGL(k_transpose_counts, dim3(grid_for(ctx, nreg, 256)), dim3(256), 0, s, counts, G, P, seg);
+    if ((e = exclusive_scan_u32(ctx, seg, seg, nreg, s)) != hipSuccess) return e;
+  }
   pp->W = pl.W;
   pp->P = P;
   pp->G = G;

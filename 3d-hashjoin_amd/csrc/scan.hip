@@ -1,9 +1,12 @@
-// scan.hip — exclusive prefix sums (CSR directory offsets, output offsets).
+// scan.hip — exclusive prefix sums (CSR directory offsets, partition histograms, output offsets).
 //
-// Reduce-then-scan in three launches over 4096-element tiles: (1) per-tile sums,
-// (2) one workgroup scans the tile sums, (3) per-tile scan with the tile's offset.
-// HBM traffic: 2 reads + 1 write of the array. Used for bucket offsets (NB+1 u32)
-// and per-probe output offsets (u64).
+// u32: one launch, single pass with decoupled look-back over 4096-element tiles: a workgroup
+// takes the next tile by ticket, publishes the tile's sum, adds up its predecessors' published
+// sums (or the first inclusive prefix it meets) and publishes its own inclusive prefix. Status
+// words carry a per-call epoch, so nothing is cleared between calls; the last tile resets the
+// ticket. HBM traffic: 1 read + 1 write of the array.
+// u64: reduce-then-scan in three launches: (1) per-tile sums, (2) one workgroup scans the tile
+// sums, (3) per-tile scan with the tile's offset (2 reads + 1 write).
 #include "hj3d_internal.hpp"
 
 namespace hj3d {
@@ -136,6 +139,73 @@ __global__ __launch_bounds__(kBlock) void k_scan_tiles(const T* in, T* out, uint
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = sums[gridDim.x];
 }
 
+// status word of a tile: epoch << 34 | flag << 32 | value (flag 1: the tile's sum, 2: inclusive prefix).
+// The published value travels inside the status word itself, so relaxed device-scope atomics
+// suffice (no release / acquire fences, no cache write-back instructions).
+constexpr uint64_t kLbAgg = 1ull << 32, kLbInc = 2ull << 32;
+__global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t* in, uint32_t* out, uint64_t n,
+                                                    uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
+                                                    uint32_t epoch, uint32_t ntiles) {
+  __shared__ uint32_t lds[kBlock / kWave];
+  __shared__ uint32_t tile[kScanPad];
+  __shared__ uint32_t tid_s, pre_s;
+  if (threadIdx.x == 0) tid_s = atomicAdd(ticket, 1u);
+  __syncthreads();
+  const uint32_t t = tid_s;
+  const uint64_t base = uint64_t(t) * kTile;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
+    tile[scan_slot(k)] = base + k < n ? in[base + k] : 0u;
+  }
+  __syncthreads();
+  uint32_t v[kScanItems];
+  uint32_t local = 0;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    v[j] = tile[scan_slot(threadIdx.x * kScanItems + j)];
+    local += v[j];
+  }
+  uint32_t total;
+  uint32_t pre = block_excl_scan(local, lds, &total);
+  if (threadIdx.x == 0) {
+    const uint64_t tag = uint64_t(epoch) << 34;
+    uint32_t excl = 0;
+    if (t == 0) {
+      __hip_atomic_store(status, tag | kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(status + t, tag | kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // tiles below t were taken by running workgroups (tickets), which publish without waiting
+      for (int64_t q = int64_t(t) - 1; q >= 0;) {
+        const uint64_t w = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((w >> 34) != epoch || ((w >> 32) & 3u) == 0) continue;  // not yet published
+        excl += uint32_t(w);
+        if (((w >> 32) & 3u) == 2u) break;
+        --q;
+      }
+      __hip_atomic_store(status + t, tag | kLbInc | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    pre_s = excl;
+    if (t == ntiles - 1) {
+      out[n] = excl + total;
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is taken
+    }
+  }
+  __syncthreads();
+  pre += pre_s;
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    tile[scan_slot(threadIdx.x * kScanItems + j)] = pre;
+    pre += v[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < kScanItems; ++j) {
+    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
+    if (base + k < n) out[base + k] = tile[scan_slot(k)];
+  }
+}
+
 template <typename T>
 hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t s) {
   if (n == 0) return hipMemsetAsync(out, 0, sizeof(T), s);
@@ -199,7 +269,24 @@ hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, i
 }
 
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s) {
-  return excl_scan<uint32_t>(ctx, in, out, n, s);
+  if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint32_t), s);
+  const uint64_t tiles = (n + kTile - 1) / kTile;
+  if (tiles >= (1ull << 31)) return excl_scan<uint32_t>(ctx, in, out, n, s);
+  DevBuf& st = ctx->scan_status;
+  const void* before = st.p;
+  hipError_t e = st.ensure(tiles * sizeof(uint64_t));
+  // fresh memory could hold a word that looks published for this epoch: clear it once
+  if (e == hipSuccess && st.p != before) e = hipMemsetAsync(st.p, 0, st.bytes, s);
+  if (e == hipSuccess) e = ctx->ensure_ctl();
+  if (e != hipSuccess) return e;
+  // the ticket: a control word kept zero between calls (the last tile resets it)
+  uint32_t* ticket = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + kCtlScanTicket);
+  ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << 30) - 1);
+  if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0 is the epoch of cleared memory
+  const uint32_t epoch = ctx->scan_epoch;
+  hipLaunchKernelGGL(k_scan_lb, dim3(unsigned(tiles)), dim3(kBlock), 0, s, in, out, n,
+                     st.as<uint64_t>(), ticket, epoch, uint32_t(tiles));
+  return hipGetLastError();
 }
 hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
   return excl_scan<uint64_t>(ctx, in, out, n, s);

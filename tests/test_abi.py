@@ -51,3 +51,12 @@ def test_null_and_invalid_arguments_rejected():
     assert L.hj3d_build(None, None, None) == hj3d.HJ3D_EINVAL
     assert L.hj3d_probe(None, None, None, 0, None, 0) == hj3d.HJ3D_EINVAL
     assert L.hj3d_table_create(None, None, None) == hj3d.HJ3D_EINVAL
+
+
+def test_single_hip_runtime_mapped():
+    """The loader maps torch first, so libhj3d.so binds torch's HIP runtime: exactly one libamdhip64
+    in the process (hj3d_ctx_create refuses to run with two). No GPU needed."""
+    import hj3d
+    info = hj3d.runtime_info()
+    assert "hip mapped=1" in info, info
+    assert "libamdhip64" in info, info
