@@ -29,6 +29,8 @@ import subprocess
 import threading
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
 
@@ -328,10 +330,14 @@ def main():
     Rk_full = None
     if args.inputs == "reference":
         # every rank runs the reference's sequential generator stream and keeps its slice
-        Rk_full, Sa = hj3d.gen_exp1_ref(nR_tot, nS_tot)
-        R[:, 0] = torch.from_numpy(Rk_full[r_lo:r_hi].view("int32")).to(dev)
+        if world > 1:  # generated once per node (local rank 0), memory-mapped by every rank
+            maker = int(os.environ.get("LOCAL_RANK", "0")) == 0  # (--rehearse maps every rank to device 0)
+            Rk_full, Sa = reference_columns_cached(nR_tot, nS_tot, maker, barrier)
+        else:
+            Rk_full, Sa = hj3d.gen_exp1_ref(nR_tot, nS_tot)
+        R[:, 0] = torch.from_numpy(np.ascontiguousarray(Rk_full[r_lo:r_hi]).view("int32")).to(dev)
         S[:, 0] = torch.arange(s_lo, s_hi, dtype=torch.int64, device=dev).to(torch.int32)
-        S[:, 1] = torch.from_numpy(Sa[s_lo:s_hi].view("int32")).to(dev)
+        S[:, 1] = torch.from_numpy(np.ascontiguousarray(Sa[s_lo:s_hi]).view("int32")).to(dev)
         del Sa
         data = ("the reference's generator (hj3d_gen_exp1_ref = Experiment1::init, main_experiment1.cc:415-457, "
                 "bit-exact: R.k = std::shuffle(iota), S.a ~ uniform_int over [0,|R|) then vec_permute, mt19937 seed 5489)")
@@ -659,6 +665,36 @@ def main():
         torch.distributed.destroy_process_group()
     if not verified:
         raise SystemExit(f"verification failed: {verify}")
+
+
+def reference_columns_cached(nR, nS, maker, barrier):
+    """The reference's experiment-1 columns (R.k, S.a) for N > 1 ranks: the generator is one
+    sequential mt19937 stream (minutes of one core at config D), so one process per node
+    (`maker`) runs it and writes relation files under $HJ3D_REL_CACHE (default
+    $TMPDIR/hj3d_relcache), reused by later runs; every rank then maps them and copies its slice."""
+    import tempfile
+    from hj3d import relfile
+    d = os.environ.get("HJ3D_REL_CACHE", os.path.join(tempfile.gettempdir(), "hj3d_relcache"))
+    meta = {"gen": "hj3d_gen_exp1_ref", "nR": nR, "nS": nS, "skew": 0, "theta": 1.0, "t": 0}
+    pr, ps = os.path.join(d, f"exp1_R{nR}_S{nS}_Rk.rel"), os.path.join(d, f"exp1_R{nR}_S{nS}_Sa.rel")
+
+    def valid(p):
+        try:
+            return relfile.read_header(p).get("meta") == meta
+        except (OSError, ValueError):
+            return False
+
+    if maker and not (valid(pr) and valid(ps)):
+        import hj3d
+        os.makedirs(d, exist_ok=True)
+        Rk, Sa = hj3d.gen_exp1_ref(nR, nS)
+        relfile.save(pr, Rk.reshape(-1, 1), 0, meta)
+        relfile.save(ps, Sa.reshape(-1, 1), 0, meta)
+        del Rk, Sa
+    barrier()
+    if not (valid(pr) and valid(ps)):
+        raise SystemExit(f"reference relation cache missing under {d}")
+    return relfile.load(pr, verify=False)[0][:, 0], relfile.load(ps, verify=False)[0][:, 0]
 
 
 def _load_pmc(path, workload):
