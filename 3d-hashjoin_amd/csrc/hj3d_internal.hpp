@@ -173,6 +173,41 @@ inline SelArgs sel_args(const hj3d_sel_pred* preds, uint32_t npred) {
   return a;
 }
 
+// ---- decoupled look-back (exclusive_scan_u32, k_pk_build) ----
+// Status word of item t: epoch << 34 | flag << 32 | value, flag 1 = the item's own sum, 2 = its
+// inclusive prefix; words of other epochs read as unpublished (nothing is cleared between calls).
+// The value travels inside the word, so relaxed device-scope atomics suffice.
+constexpr uint64_t kLbAgg = 1ull << 32, kLbInc = 2ull << 32;
+__device__ __forceinline__ void lb_publish(uint64_t* status, uint32_t t, uint32_t epoch, uint64_t flag, uint32_t v) {
+  __hip_atomic_store(status + t, (uint64_t(epoch) << 34) | flag | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Called by one whole wave: the sum of items [0, t) from their status words, 64 predecessors per
+// step (lane k reads item q - k; the nearest inclusive prefix ends the walk). Items below t must
+// be published by running workgroups (taken by ticket), which never wait for later items.
+__device__ __forceinline__ uint32_t lb_exclusive(const uint64_t* status, uint32_t t, uint32_t epoch) {
+  const int lane = threadIdx.x & 63;
+  uint32_t excl = 0;
+  int64_t hi = int64_t(t) - 1;
+  while (hi >= 0) {
+    const int64_t q = hi - lane;
+    const uint64_t w = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                              : ((uint64_t(epoch) << 34) | kLbInc);  // before item 0: prefix 0
+    const uint32_t f = uint32_t(w >> 32) & 3u;
+    const bool ready = (w >> 34) == epoch && f != 0;
+    const uint64_t inc = __ballot(ready && f == 2u), nready = __ballot(!ready);
+    const int fi = inc ? __ffsll((unsigned long long)inc) - 1 : 63;  // nearest inclusive (or the whole step)
+    const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+    if (nready & need) continue;  // a predecessor in range has not published yet: read again
+    uint32_t v = lane <= fi ? uint32_t(w) : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += uint32_t(__shfl_xor(int(v), o, 64));
+    excl += v;
+    if (inc) break;
+    hi -= 64;
+  }
+  return excl;
+}
+
 // ---- launchers (defined in the .hip translation units); all asynchronous on `s` ----
 // scan.hip: exclusive prefix sum of n values into out[0..n], out[n] = total. in may alias out.
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);

@@ -139,10 +139,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_tiles(const T* in, T* out, uint
   if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = sums[gridDim.x];
 }
 
-// status word of a tile: epoch << 34 | flag << 32 | value (flag 1: the tile's sum, 2: inclusive prefix).
-// The published value travels inside the status word itself, so relaxed device-scope atomics
-// suffice (no release / acquire fences, no cache write-back instructions).
-constexpr uint64_t kLbAgg = 1ull << 32, kLbInc = 2ull << 32;
 __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t* in, uint32_t* out, uint64_t n,
                                                     uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
                                                     uint32_t epoch, uint32_t ntiles) {
@@ -168,28 +164,20 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t* in, uint32_t
   }
   uint32_t total;
   uint32_t pre = block_excl_scan(local, lds, &total);
-  if (threadIdx.x == 0) {
-    const uint64_t tag = uint64_t(epoch) << 34;
-    uint32_t excl = 0;
-    if (t == 0) {
-      __hip_atomic_store(status, tag | kLbInc | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(status + t, tag | kLbAgg | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // tiles below t were taken by running workgroups (tickets), which publish without waiting
-      for (int64_t q = int64_t(t) - 1; q >= 0;) {
-        const uint64_t w = __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((w >> 34) != epoch || ((w >> 32) & 3u) == 0) continue;  // not yet published
-        excl += uint32_t(w);
-        if (((w >> 32) & 3u) == 2u) break;
-        --q;
-      }
-      __hip_atomic_store(status + t, tag | kLbInc | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const int wid = threadIdx.x >> 6;
+  if (threadIdx.x == 0) lb_publish(status, t, epoch, t == 0 ? kLbInc : kLbAgg, total);
+  if (wid == 0 && t > 0) {  // the first wave looks back over the tiles taken before this one
+    const uint32_t excl = lb_exclusive(status, t, epoch);
+    if (threadIdx.x == 0) {
+      lb_publish(status, t, epoch, kLbInc, excl + total);
+      pre_s = excl;
     }
-    pre_s = excl;
-    if (t == ntiles - 1) {
-      out[n] = excl + total;
-      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is taken
-    }
+  } else if (threadIdx.x == 0) {
+    pre_s = 0;
+  }
+  if (threadIdx.x == 0 && t == ntiles - 1) {
+    out[n] = pre_s + total;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is taken
   }
   __syncthreads();
   pre += pre_s;
