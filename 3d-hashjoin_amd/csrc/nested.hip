@@ -271,7 +271,7 @@ struct SlotSrc {
   }
 };
 
-template <bool SLOTS>
+template <bool SLOTS, bool CK>
 __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t nslots, const uint64_t* __restrict__ ooff,
                                                          const uint32_t* __restrict__ sub, uint2* __restrict__ out,
                                                          uint64_t out_cap, uint32_t* __restrict__ heavy,
@@ -324,13 +324,16 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t n
     const uint32_t br = sub[lz[lo] + q], prow = lpr[lo];
     const uint64_t o = lpos[lo] + q;
     if (o < out_cap) __builtin_nontemporal_store((uint64_t(br) << 32) | prow, reinterpret_cast<uint64_t*>(out + o));
-    acc[4] += prow;
-    acc[5] += br;
-    const uint64_t ph = pair_hash(prow, br);
-    acc[7] += ph;
-    acc[8] ^= ph;
+    if (CK) {
+      acc[4] += prow;
+      acc[5] += br;
+      const uint64_t ph = pair_hash(prow, br);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
   }
-  block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+  // the output checksums only (the counts are the probe's): no partials without HJ3D_PROBE_CHECKSUM
+  if (CK) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
 }
 
 // hoff[q] = first flattened output of heavy slot q (exclusive scan of their counts, one workgroup;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(1024) void k_heavy_offsets(const uint32_t* __restri
 // coalesced and a lane binary-searches hoff only once (a heavy slot spans >= kHeavyOut outputs).
 constexpr uint32_t kHeavySpan = 64 * 16;
 
-template <bool SLOTS>
+template <bool SLOTS, bool CK>
 __global__ __launch_bounds__(kBlock) void k_expand_heavy_flat(SlotSrc src, const uint64_t* __restrict__ ooff,
                                                               const uint32_t* __restrict__ sub,
                                                               const uint32_t* __restrict__ heavy,
@@ -417,14 +420,16 @@ __global__ __launch_bounds__(kBlock) void k_expand_heavy_flat(SlotSrc src, const
       const uint32_t br = sub[z + k];
       if (ob + k < out_cap)
         __builtin_nontemporal_store((uint64_t(br) << 32) | pr, reinterpret_cast<uint64_t*>(out + ob + k));
-      acc[4] += pr;
-      acc[5] += br;
-      const uint64_t ph = pair_hash(pr, br);
-      acc[7] += ph;
-      acc[8] ^= ph;
+      if (CK) {
+        acc[4] += pr;
+        acc[5] += br;
+        const uint64_t ph = pair_hash(pr, br);
+        acc[7] += ph;
+        acc[8] ^= ph;
+      }
     }
   }
-  block_flush<kProbeFields, 1>(acc, res);
+  if (CK) block_flush<kProbeFields, 1>(acc, res);
 }
 
 // ---- partitioned probe (radix_seg.hpp): the probe side is partitioned by bucket range and
@@ -569,24 +574,30 @@ namespace {
 
 // Light expansion (one workgroup per 256 slots, partials per workgroup) then the heavy slots
 // flattened over the chip (hoff in kScrD).
-hipError_t expand(hj3d_ctx* ctx, const SlotSrc& src, bool slots, uint64_t nslots, const uint64_t* ooff,
+// ck: fold the output checksums (HJ3D_PROBE_CHECKSUM; the light kernel's per-workgroup partials
+// are then reduced by the caller), otherwise the expansion only writes the pairs.
+hipError_t expand(hj3d_ctx* ctx, const SlotSrc& src, bool slots, bool ck, uint64_t nslots, const uint64_t* ooff,
                   const uint32_t* sub, uint2* out, uint64_t out_cap, uint32_t* heavy, uint32_t* nheavy,
                   uint64_t* partials, uint64_t* res, hipStream_t s) {
   const uint32_t nblk = uint32_t((nslots + kBlock - 1) / kBlock);
   uint64_t* hoff = ctx->scratch[kScrD].as<uint64_t>();
-  if (slots)
-    hipLaunchKernelGGL(k_expand_light<true>, dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
+  auto launch = [&](auto slots_c, auto ck_c) {
+    constexpr bool SL = decltype(slots_c)::value, CK = decltype(ck_c)::value;
+    hipLaunchKernelGGL((k_expand_light<SL, CK>), dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
                        heavy, nheavy, partials);
-  else
-    hipLaunchKernelGGL(k_expand_light<false>, dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
-                       heavy, nheavy, partials);
-  hipLaunchKernelGGL(k_heavy_offsets, dim3(1), dim3(1024), 0, s, heavy, nheavy, ooff, hoff);
-  if (slots)
-    hipLaunchKernelGGL(k_expand_heavy_flat<true>, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub, heavy,
-                       nheavy, hoff, out, out_cap, res);
-  else
-    hipLaunchKernelGGL(k_expand_heavy_flat<false>, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub, heavy,
-                       nheavy, hoff, out, out_cap, res);
+    hipLaunchKernelGGL(k_heavy_offsets, dim3(1), dim3(1024), 0, s, heavy, nheavy, ooff, hoff);
+    hipLaunchKernelGGL((k_expand_heavy_flat<SL, CK>), dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub,
+                       heavy, nheavy, hoff, out, out_cap, res);
+  };
+  using T = std::true_type;
+  using F = std::false_type;
+  if (slots) {
+    if (ck) launch(T{}, T{});
+    else launch(T{}, F{});
+  } else {
+    if (ck) launch(F{}, T{});
+    else launch(F{}, F{});
+  }
   return hipGetLastError();
 }
 
@@ -696,8 +707,10 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
                      nullptr, 0, cnt, mid, nullptr, nullptr, res);
   if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
   SlotSrc src{v, mid, mains, nullptr, nullptr};
-  if ((e = expand(ctx, src, false, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess) return e;
-  return reduce_partials(partials, nblk, kProbeFields, 1, res, s);
+  const bool ck = flags & HJ3D_PROBE_CHECKSUM;
+  if ((e = expand(ctx, src, false, ck, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess)
+    return e;
+  return ck ? reduce_partials(partials, nblk, kProbeFields, 1, res, s) : hipSuccess;
 }
 
 bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe) {
@@ -792,8 +805,10 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   partials = ctx->scratch[kScrPartial].as<uint64_t>();
   if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
   SlotSrc src{view_of(r), nullptr, mains, zo, po};
-  if ((e = expand(ctx, src, true, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess) return e;
-  return reduce_partials(partials, nblk, kProbeFields, 1, res, s);
+  const bool ck = flags & HJ3D_PROBE_CHECKSUM;
+  if ((e = expand(ctx, src, true, ck, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess)
+    return e;
+  return ck ? reduce_partials(partials, nblk, kProbeFields, 1, res, s) : hipSuccess;
 }
 
 }  // namespace hj3d
