@@ -222,76 +222,9 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
   }
 }
 
-// One workgroup per build partition of kBuildSlice2 buckets: count (LDS atomics), scan, then rank
-// every pair into an LDS stage in bucket order, sort the small buckets by row in LDS, and write
-// the partition's CSR slice out coalesced. A partition with more pairs than the stage holds
-// (skewed keys) scatters to HBM instead and sorts its small buckets there.
+// Staged build partitions: kBuildSlice2 buckets, at most kBuildStage pairs through LDS.
 constexpr uint32_t kBuildSlice2 = 8192;
 constexpr uint32_t kBuildStage = 15000;
-[[maybe_unused]] __global__ __launch_bounds__(kJBlock) void k_rp_build2(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                       FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W,
-                                                       uint32_t* __restrict__ off, uint2* __restrict__ ent) {
-  __shared__ uint32_t cnt[kBuildSlice2];
-  __shared__ uint2 stage[kBuildStage];
-  __shared__ uint32_t wsum[kJBlock / kWave];
-  const uint32_t p = blockIdx.x;
-  const uint32_t b0 = p * W;
-  const uint32_t nbs = min(W, nbl - b0);
-  const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
-  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
-  __syncthreads();
-  for (uint32_t i0 = s0; i0 < s1; i0 += kJBlock * 4) {
-    uint32_t h[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + u * kJBlock + threadIdx.x;
-      h[u] = i < s1 ? pairs[i].x : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (i0 + u * kJBlock + threadIdx.x < s1) atomicAdd(&cnt[fm.mod(h[u]) - lo - b0], 1u);
-  }
-  __syncthreads();
-  lds_excl_scan(cnt, nbs, wsum);
-  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
-  if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
-  __syncthreads();
-  const bool staged = m <= kBuildStage;
-  for (uint32_t i0 = s0; i0 < s1; i0 += kJBlock * 4) {
-    uint2 e[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint32_t i = i0 + u * kJBlock + threadIdx.x;
-      e[u] = i < s1 ? pairs[i] : make_uint2(0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (i0 + u * kJBlock + threadIdx.x >= s1) continue;
-      const uint32_t pos = atomicAdd(&cnt[fm.mod(e[u].x) - lo - b0], 1u);  // cnt[b] walks to b's end
-      if (staged) stage[pos] = e[u];
-      else ent[s0 + pos] = e[u];
-    }
-  }
-  __syncthreads();
-  // buckets of 2..kSortedMax entries sorted by row; bucket k = [k ? cnt[k-1] : 0, cnt[k])
-  for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) {
-    const uint32_t bs = k ? cnt[k - 1] : 0u, n = cnt[k] - bs;
-    if (n < 2 || n > kSortedMax) continue;
-    uint2* E = staged ? stage + bs : ent + s0 + bs;
-    for (uint32_t q = 1; q < n; ++q) {
-      const uint2 x = E[q];
-      uint32_t j = q;
-      while (j > 0 && E[j - 1].y > x.y) {
-        E[j] = E[j - 1];
-        --j;
-      }
-      E[j] = x;
-    }
-  }
-  if (!staged) return;
-  __syncthreads();
-  for (uint32_t k = threadIdx.x; k < m; k += kJBlock) ent[s0 + k] = stage[k];
-}
 
 // The staged build as a persistent kernel (one 1024-thread workgroup per CU takes partitions
 // blockIdx.x, blockIdx.x + gridDim.x, ...): the next partition's pairs are loaded into registers
@@ -300,8 +233,8 @@ constexpr uint32_t kBuildStage = 15000;
 // scan to bucket starts (-> the directory slice), stage every pair at start + arrival rank, then
 // every staged pair takes its final slot = bucket start + the rank of its row among the bucket's
 // rows (buckets of 2..kSortedMax entries come out sorted by row, with no sort pass; longer ones
-// stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) fall back to
-// k_rp_build2's scatter through HBM for that partition.
+// stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) scatter
+// through HBM instead (sorting their small buckets there).
 constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12288 pairs
 __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
@@ -1135,14 +1068,9 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   if (nbl && staged) {
-#ifdef HJ3D_BUILD2
-    hipLaunchKernelGGL(k_rp_build2, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo),
-                       nbl, pl.W, t->off.as<uint32_t>(), t->ent.as<uint2>());
-#else
     const uint32_t g = pl.P < uint32_t(ctx->num_cus) ? pl.P : uint32_t(ctx->num_cus);
     hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
                        pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
-#endif
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
     hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
