@@ -7,7 +7,7 @@
 // order of the mains inside a bucket nor the order of the rows inside a key matters: the probe
 // derives the reference's comparison count from first-row ranks and unnest output is order-free.
 // So instead of sorting all tuples by key (3 LSD passes at 16 B/tuple each, nested.hip):
-//   1. partition the build tuples into (hash, row) pairs by ranges of kAggW buckets
+//   1. partition the build tuples into (hash, row) pairs by ranges of W <= kAggW buckets
 //      (radix_partition_pairs: one histogram pass, one LDS-staged scatter pass);
 //   2. one workgroup per partition inserts the partition's keys into an LDS hash table (count +
 //      min row per key; a hot key's lanes are aggregated per wave first, so Zipf skew costs one
@@ -26,7 +26,7 @@ namespace hj3d {
 namespace {
 
 constexpr int kAggBlock = 1024;
-constexpr uint32_t kAggW = 6144;     // buckets per partition (one LDS table round at fill <= ~1.3)
+constexpr uint32_t kAggW = 6144;     // max buckets per partition (one LDS table round at fill <= ~1.3)
 // LDS hash table slots, prime: with double hashing every probe step visits all slots (double
 // hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6)
 constexpr uint32_t kAggCap = 10223;
@@ -124,7 +124,7 @@ __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
 // Writes: off[b0 + k] = partition-local main offset of bucket k; mtmp[ps[p] + i] the partition's
 // main records in bucket order (i < its key count, with sub_off global); sub rows; dcount[p].
 __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                    FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global,
+                                                    FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                                     uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
                                                     uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
                                                     unsigned long long* __restrict__ maxlen,
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
   __shared__ uint32_t wsum[kWavesA];
   __shared__ uint32_t nkeys, ovf;
   const uint32_t p = order[blockIdx.x];
-  const uint32_t b0 = p * kAggW, nbs = min(kAggW, nbl - b0);
+  const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
   const uint32_t e0 = ps[p], e1 = ps[p + 1];
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -341,11 +341,11 @@ __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict_
 // off[b] += first main of b's partition; main records moved to their final slots.
 // k_nagg_rebase / k_nagg_mains / k_nagg_counts run only when no partition gave up (`fail`: the
 // sort build replaces the table then; the host checks the flag once, after the whole build).
-__global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ off, uint32_t nbl,
+__global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ off, uint32_t nbl, FastDiv32 dw,
                                                         const uint32_t* __restrict__ mbase,
                                                         const uint32_t* __restrict__ fail) {
   if (*fail) return;
-  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[b / kAggW];
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[dw.div(b)];
 }
 
 __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
@@ -372,7 +372,7 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   const uint32_t nbl = t->nb_local;
   // small inputs and tables that one partition would cover (no free bucket for the LDS table's
   // empty marker) take the sort-based build
-  if (ctx->force_direct || n < (ctx->radix_min >> 4) || n >= (1ull << 31) || nbl <= kAggW ||
+  if (ctx->force_direct || n < (ctx->radix_min >> 4) || n >= (1ull << 31) || nbl <= 1024 ||
       t->desc.num_buckets >= (1ull << 32))
     return hipErrorNotSupported;
   hipError_t e;
@@ -380,7 +380,11 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   if ((e = t->main.ensure(n * sizeof(uint4))) != hipSuccess) return e;
   if ((e = t->sub.ensure(n * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = t->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
-  const uint32_t P = (nbl + kAggW - 1) / kAggW;
+  // partition width: kAggW buckets, narrower when that would leave the chip with fewer than two
+  // partitions per CU (config E: 2M buckets -> 512 partitions of 4K instead of 342 of 6K)
+  uint32_t W = uint32_t((uint64_t(nbl) + 2 * ctx->num_cus - 1) / (2 * ctx->num_cus));
+  W = W < 1024 ? 1024 : W > kAggW ? kAggW : W;
+  const uint32_t P = (nbl + W - 1) / W;
   // scratch: pairs (n uint2) | main records before compaction (n uint4) | starts, key counts
   if ((e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
@@ -391,7 +395,7 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   uint32_t* dcount = ps + P + 2;  // P + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + P + 1;
   uint32_t np = 0;
-  if ((e = radix_partition_pairs(ctx, t, r, kAggW, pairs, ps, &np, s)) != hipSuccess) return e;
+  if ((e = radix_partition_pairs(ctx, t, r, W, pairs, ps, &np, s)) != hipSuccess) return e;
   if (np != P) return hipErrorNotSupported;
   uint64_t* counts = t->counts.as<uint64_t>();
   uint32_t* off = t->off.as<uint32_t>();
@@ -399,12 +403,13 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
   hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
   hipLaunchKernelGGL(k_nagg, dim3(P), dim3(kAggBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
-                     uint32_t(t->desc.num_buckets), off, mtmp, t->sub.as<uint32_t>(), dcount,
+                     uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
                      reinterpret_cast<unsigned long long*>(counts + 2), fail, order);
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // and the caller, which reads the counts once after the build, runs the sort build instead
   if ((e = exclusive_scan_u32(ctx, dcount, dcount, P, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl, dcount, fail);
+  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl,
+                     FastDiv32::make(W), dcount, fail);
   hipLaunchKernelGGL(k_nagg_mains, dim3(P), dim3(kBlock), 0, s, mtmp, ps, dcount, t->main.as<uint4>(), fail);
   hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(1), 0, s, ps, dcount, P, nbl, off, counts);
   t->n_build = n;
