@@ -275,8 +275,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
 
 // ---- k_pk_probe ----
 constexpr uint32_t kLdsWords = kProbeLdsWords;
-constexpr int kItems = 8;  // pairs per lane and chunk (the next chunk in flight)
-constexpr int kGroup = 4;  // items whose LDS lookups are batched
+#ifndef HJ3D_PK_ITEMS
+#define HJ3D_PK_ITEMS 8
+#endif
+#ifndef HJ3D_PK_GROUP
+#define HJ3D_PK_GROUP 8
+#endif
+constexpr int kItems = HJ3D_PK_ITEMS;  // pairs per lane and chunk (the next chunk in flight)
+constexpr int kGroup = HJ3D_PK_GROUP;  // items whose LDS lookups are batched
+static_assert(kItems % kGroup == 0 && kItems <= 32, "items per chunk: a multiple of the group, <= 32 (valid mask)");
 
 // Unique probe of one lane's items against the LDS slice: directory word (start << 16 | count),
 // entries {q, row} sorted by row inside buckets of <= 32. Walk position c = 0, 1, 2 (sorted index
