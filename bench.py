@@ -684,16 +684,24 @@ def reference_columns_cached(nR, nS, maker, barrier):
         except (OSError, ValueError):
             return False
 
+    import hj3d
     if maker and not (valid(pr) and valid(ps)):
-        import hj3d
-        os.makedirs(d, exist_ok=True)
-        Rk, Sa = hj3d.gen_exp1_ref(nR, nS)
-        relfile.save(pr, Rk.reshape(-1, 1), 0, meta)
-        relfile.save(ps, Sa.reshape(-1, 1), 0, meta)
-        del Rk, Sa
+        try:
+            os.makedirs(d, exist_ok=True)
+            Rk, Sa = hj3d.gen_exp1_ref(nR, nS)
+            relfile.save(pr, Rk.reshape(-1, 1), 0, meta)
+            relfile.save(ps, Sa.reshape(-1, 1), 0, meta)
+            del Rk, Sa
+        except OSError as e:  # no room for the cache: every rank generates for itself below
+            print(f"relation cache under {d} not written ({e})", file=sys.stderr)
+            for f in (pr, ps, pr + ".tmp", ps + ".tmp"):
+                try:
+                    os.remove(f)
+                except OSError:
+                    pass
     barrier()
     if not (valid(pr) and valid(ps)):
-        raise SystemExit(f"reference relation cache missing under {d}")
+        return hj3d.gen_exp1_ref(nR, nS)
     return relfile.load(pr, verify=False)[0][:, 0], relfile.load(ps, verify=False)[0][:, 0]
 
 
