@@ -190,20 +190,26 @@ bool rccl_ready(hj3d_ctx* ctx) {
 hj3d_comm_state* st(hj3d_ctx* ctx) { return ctx ? ctx->comm : nullptr; }
 
 // grouped send / recv of per-peer blocks (an all-to-all with per-peer sizes); counts in elements
-// of elem bytes, displacements = prefix sums of the counts
+// of elem bytes, displacements = prefix sums of the counts. Blocks move as 8- or 4-byte words
+// when their size allows, in pieces of at most 2^27 words (matched in order per peer), so no
+// RCCL count approaches 2^31 (a 2.5e8-pair chunk is 2e9 bytes).
 ncclResult_t alltoallv(hj3d_comm_state* c, const char* send, const int64_t* sc, char* recv, const int64_t* rc,
                        size_t elem, hipStream_t s) {
   Rccl* r = rccl();
+  const size_t word = elem % 8 == 0 ? 8 : elem % 4 == 0 ? 4 : 1;
+  const ncclDataType_t dt = word == 8 ? ncclUint64 : word == 4 ? ncclUint32 : ncclUint8;
+  constexpr size_t kPiece = size_t(1) << 27;  // words per send / recv
   ncclResult_t e = r->groupStart();
   if (e != ncclSuccess) return e;
   size_t so = 0, ro = 0;
-  for (int p = 0; p < c->world; ++p) {
-    const size_t ns = size_t(sc[p]) * elem, nr = size_t(rc[p]) * elem;
-    if (ns) e = r->send(send + so, ns, ncclUint8, p, c->comm, s);
-    if (e == ncclSuccess && nr) e = r->recv(recv + ro, nr, ncclUint8, p, c->comm, s);
-    if (e != ncclSuccess) break;
-    so += ns;
-    ro += nr;
+  for (int p = 0; p < c->world && e == ncclSuccess; ++p) {
+    const size_t ns = size_t(sc[p]) * elem / word, nr = size_t(rc[p]) * elem / word;
+    for (size_t k = 0; k < ns && e == ncclSuccess; k += kPiece)
+      e = r->send(send + so + k * word, ns - k < kPiece ? ns - k : kPiece, dt, p, c->comm, s);
+    for (size_t k = 0; k < nr && e == ncclSuccess; k += kPiece)
+      e = r->recv(recv + ro + k * word, nr - k < kPiece ? nr - k : kPiece, dt, p, c->comm, s);
+    so += ns * word;
+    ro += nr * word;
   }
   const ncclResult_t g = r->groupEnd();
   return e != ncclSuccess ? e : g;

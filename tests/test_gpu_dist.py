@@ -190,3 +190,17 @@ def test_bench_dist_path_on_rccl_equals_reference(plan, tmp_path):
     assert line["verified_bit_exact"], v
     assert "exp1_R1048576_S8388608_uni.json" in v["against"]
     assert line["config"]["exchange"].startswith("libhj3d")
+
+
+def test_rccl_exchange_large_message(ctx, comm):
+    """One chunk of more than 2^31 bytes (2^28 + 12345 pairs) arrives intact: the exchange moves
+    8-byte words in pieces (a 2e9-byte chunk of config D once came out corrupted as one message)."""
+    import torch
+    n = (1 << 28) + 12345
+    send = torch.randint(-2**31, 2**31 - 1, (n, 2), dtype=torch.int32, device="cuda")
+    recv = torch.empty_like(send)
+    got, _ = comm.exchange(send, [n], [n], recv, asynchronous=False)
+    ctx.sync()
+    assert got.shape[0] == n and torch.equal(got, send)
+    del send, recv, got
+    torch.cuda.empty_cache()
