@@ -32,6 +32,11 @@ def use_comm(comm) -> None:
     _comm = comm
 
 
+def current_comm():
+    """The hj3d.Comm set by use_comm, or None."""
+    return _comm
+
+
 def comm_from_torch(ctx, group=None):
     """An hj3d.Comm over the ranks of the initialised torch.distributed group: rank 0 creates the
     RCCL id, torch.distributed broadcasts it (the only thing it carries), every rank joins."""

@@ -318,6 +318,16 @@ def main():
         # torch.distributed only hands over its id and times (barriers, max over ranks). World
         # size 1 (--dist-path): RCCL ships every chunk to this rank itself.
         hdist.use_comm(hdist.comm_from_torch(ctx) if world > 1 else hj3d.Comm(ctx, hj3d.Comm.unique_id(ctx), 0, 1))
+
+    def teardown():
+        # the library's communicator before torch's process group (both hold RCCL state)
+        comm = hdist.current_comm()
+        if comm is not None:
+            torch.cuda.synchronize()
+            comm.close()
+            hdist.use_comm(None)
+        if world > 1:
+            torch.distributed.destroy_process_group()
     packed = args.probe_path == "packed" and plan == "Csr"
     ctx.packed_probe(packed)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
@@ -547,8 +557,7 @@ def main():
             per_gpu[k] = {"min": mn, "max": mx, "max_over_mean": mx / (sm / world) if sm else None}
 
     if rank != 0:
-        if world > 1:
-            torch.distributed.destroy_process_group()
+        teardown()
         if not verified:
             raise SystemExit(f"rank {rank}: verification failed")
         return
@@ -661,8 +670,7 @@ def main():
             S_host = S[:m].cpu().numpy().view("uint32")
             line["cpu_baseline"] = cpu_baseline_port(R_host, S_host, nb, args.cpu_reps)
     _emit(line, args)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    teardown()
     if not verified:
         raise SystemExit(f"verification failed: {verify}")
 
