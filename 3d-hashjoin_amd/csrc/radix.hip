@@ -236,7 +236,7 @@ constexpr uint32_t kBuildStage = 15000;
 // stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) scatter
 // through HBM instead (sorting their small buckets there).
 constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12288 pairs
-__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps, uint32_t pst,
                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
                                                        uint32_t* __restrict__ off, uint2* __restrict__ ent) {
   __shared__ uint32_t cnt[kBuildSlice2 + 1];
@@ -247,7 +247,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
   uint2 ea[kB3Per], eb[kB3Per];
   auto load = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
     if (p >= P) return;
-    const uint32_t s0 = ps[p], s1 = ps[p + 1];
+    const uint32_t s0 = ps[p * pst], s1 = ps[(p + 1) * pst];
     if (s1 - s0 > kCap) return;
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
   auto build = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
     const uint32_t b0 = p * W;
     const uint32_t nbs = min(W, nbl - b0);
-    const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
+    const uint32_t s0 = ps[p * pst], s1 = ps[(p + 1) * pst], m = s1 - s0;
     for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
     __syncthreads();
     if (m > kCap) {  // skewed partition: scatter through HBM, sort the small buckets there
@@ -982,8 +982,10 @@ Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
 
 // Partition `r` into (hash, row) pairs by bucket range; ps[0..P] = partition starts.
 // t_hist / t_scatter: timer phases of the two streaming kernels (-1: untimed).
+// starts = false: ps[] is not written; partition p then starts at hist[p * G] of the scanned
+// histogram (kScrPHist, G = the persistent workgroup count), which k_rp_build3 reads directly.
 hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
-                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1) {
+                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1, bool starts = true) {
   hipError_t e;
   // G persistent workgroups in both passes, one histogram column per workgroup
   const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
@@ -1004,7 +1006,7 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
                        pl.ntiles, hist, out);
   }
   if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
-  hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, g, pl.P, ps);
+  if (starts) hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, g, pl.P, ps);
   return hipGetLastError();
 }
 
@@ -1066,11 +1068,16 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
-  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
+  // the staged build reads the partition starts straight from the scanned histogram
+  const bool direct_starts = nbl && staged && r.n;
+  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s, -1, -1, !direct_starts)) != hipSuccess) return e;
+  const uint32_t pg = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
+  const uint32_t* starts = direct_starts ? ctx->scratch[kScrPHist].as<const uint32_t>() : ps;
+  const uint32_t pst = direct_starts ? pg : 1u;
   if (nbl && staged) {
     const uint32_t g = pl.P < uint32_t(ctx->num_cus) ? pl.P : uint32_t(ctx->num_cus);
-    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
-                       pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
+    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, starts, pst, t->fm,
+                       uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
     hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
