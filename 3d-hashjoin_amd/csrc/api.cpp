@@ -148,6 +148,10 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_NESTED_SORT: ctx->nested_sort = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SEL_UNFUSED: ctx->sel_unfused = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PACKED_PROBE: ctx->pk_off = value == 0; return HJ3D_OK;
+    case HJ3D_OPT_PROBE_ITEMS:
+      if (value != 0 && (value < 5 || value > 8)) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PROBE_ITEMS: 0 or 5..8");
+      ctx->pk_items = int(value);
+      return HJ3D_OK;
     default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
   }
 }

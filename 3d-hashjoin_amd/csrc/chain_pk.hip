@@ -275,31 +275,27 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
 
 // ---- k_pk_probe ----
 constexpr uint32_t kLdsWords = kProbeLdsWords;
-#ifndef HJ3D_PK_ITEMS
-#define HJ3D_PK_ITEMS 8
-#endif
-#ifndef HJ3D_PK_GROUP
-#define HJ3D_PK_GROUP 8
-#endif
-constexpr int kItems = HJ3D_PK_ITEMS;  // pairs per lane and chunk (the next chunk in flight)
-constexpr int kGroup = HJ3D_PK_GROUP;  // items whose LDS lookups are batched
-static_assert(kItems % kGroup == 0 && kItems <= 32, "items per chunk: a multiple of the group, <= 32 (valid mask)");
+// K = pairs per lane and chunk (the next chunk in flight), chosen per probe from the expected
+// region length (pk_items): a region of L pairs costs ceil(L / 64K) chunks of 64K item slots, so
+// K = 7 walks config B's ~384-pair regions in one 448-slot chunk where K = 8 spends 512 slots.
+// All K items of a chunk have their LDS lookups batched.
+constexpr int kItemsMin = 5, kItemsMax = 8;
 
 // Unique probe of one lane's items against the LDS slice: directory word (start << 16 | count),
 // entries {q, row} sorted by row inside buckets of <= 32. Walk position c = 0, 1, 2 (sorted index
-// 0, n-1, n-2) batched over kGroup items, the rest per item.
-template <int MODE, bool CK>
-__device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[kItems], uint32_t valid, uint64_t slot0,
+// 0, n-1, n-2) batched over K items, the rest per item.
+template <int K, int MODE, bool CK>
+__device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t valid, uint64_t slot0,
                                                const uint32_t* ldir, const uint2* lent, const PkGeom& pk,
                                                uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
                                                uint64_t out_cap, uint2* __restrict__ sink) {
   uint32_t nm = 0, sc = 0, nv = 0;
 #pragma unroll
-  for (int g = 0; g < kItems; g += kGroup) {
-    uint32_t d[kGroup], match[kGroup], cmps[kGroup], q[kGroup];
-    bool live[kGroup];
+  for (int g = 0; g < K; g += K) {
+    uint32_t d[K], match[K], cmps[K], q[K];
+    bool live[K];
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) {
+    for (int j = 0; j < K; ++j) {
       const bool ok = (valid >> (g + j)) & 1u;
       const uint32_t x = uint32_t(v[g + j]);
       q[j] = x & pk.qmask;
@@ -312,7 +308,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[kItems], uint
 #pragma unroll
     for (uint32_t c = 0; c < 3; ++c) {
 #pragma unroll
-      for (int j = 0; j < kGroup; ++j) {
+      for (int j = 0; j < K; ++j) {
         const uint32_t nn = d[j] & 0xFFFFu;
         const bool ok = live[j] && c < nn;
         const uint2 e = lent[ok ? (d[j] >> 16) + (c == 0 ? 0u : nn - c) : 0u];
@@ -323,7 +319,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[kItems], uint
       }
     }
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) {
+    for (int j = 0; j < K; ++j) {
       const uint32_t nn = d[j] & 0xFFFFu, s = d[j] >> 16;
       if (live[j] && nn > 3) {
         for (uint32_t c = 3; c < nn; ++c) {
@@ -357,7 +353,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[kItems], uint
       }
     }
 #pragma unroll
-    for (int j = 0; j < kGroup; ++j) {
+    for (int j = 0; j < K; ++j) {
       const bool ok = (valid >> (g + j)) & 1u;
       const uint32_t row = uint32_t(v[g + j] >> 32);
       const bool m = match[j] != kInvalid;
@@ -469,7 +465,7 @@ __device__ __forceinline__ void pk_stage(const uint32_t* __restrict__ off, const
   }
 }
 
-template <int MODE, bool CK>
+template <int K, int MODE, bool CK>
 __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__ region,
                                                        const uint32_t* __restrict__ counts, uint32_t G, uint32_t cap,
                                                        uint32_t splits, bool flat, const uint32_t* __restrict__ off,
@@ -515,14 +511,14 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   auto len_at = [&](uint32_t k) __attribute__((always_inline)) { return uint32_t(__builtin_amdgcn_readlane(int(my_len), int(k))); };
   auto src_of = [&](uint32_t k) __attribute__((always_inline)) { return region + (g_lo + wid + kWaves * k) * P * cap + p * cap; };
 
-  // one chunk = kItems x 64 consecutive items of the wave's stream (flat: regions concatenated;
+  // one chunk = K x 64 consecutive items of the wave's stream (flat: regions concatenated;
   // otherwise a chunk stays inside one region). Loads and stores of the steady-state loops are
   // unconditional (clamped addresses, absent items stored to the sink): with a fixed count per chunk
   // the wait for the next chunk's pairs leaves this chunk's stores in flight.
   uint32_t rb = 0;  // flat: last region starting at or before the block of 64
-  auto load_flat = [&](uint64_t (&v)[kItems], uint32_t f0) __attribute__((always_inline)) {
+  auto load_flat = [&](uint64_t (&v)[K], uint32_t f0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
+    for (int j = 0; j < K; ++j) {
       // block start and item clamped into the stream (the last prefetch re-reads the last chunk)
       const uint32_t b = min(f0 + j * 64, wtotal - 1), f = min(f0 + j * 64 + lane, wtotal - 1);
       if (pre_at(rb) > b) rb = 0;
@@ -545,16 +541,16 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     ++r;
     len = r < nr ? len_at(r) : 0u;
   }
-  auto load_reg = [&](uint64_t (&v)[kItems], uint32_t rr, uint32_t q0, uint32_t ll) __attribute__((always_inline)) {
+  auto load_reg = [&](uint64_t (&v)[K], uint32_t rr, uint32_t q0, uint32_t ll) __attribute__((always_inline)) {
     const uint2* src = rr < nr ? src_of(rr) : region;
     const uint32_t last = ll ? ll - 1 : 0u;
 #pragma unroll
-    for (int j = 0; j < kItems; ++j)
+    for (int j = 0; j < K; ++j)
       v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + min(q0 + j * 64 + lane, last)));
   };
-  auto probe_hbm_chunk = [&](const uint64_t (&v)[kItems], uint32_t valid, uint64_t slot0) __attribute__((always_inline)) {
+  auto probe_hbm_chunk = [&](const uint64_t (&v)[K], uint32_t valid, uint64_t slot0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < kItems; ++j) {
+    for (int j = 0; j < K; ++j) {
       if (!((valid >> j) & 1u)) continue;
       const uint32_t x = uint32_t(v[j]), bl = b0 + (x >> pk.qbits);
       const uint32_t s = off[bl];
@@ -565,22 +561,22 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   // the walk: probe(v, valid mask, wave-local stream offset of the lane's item 0); stage() runs
   // (followed by a barrier) once the first chunk's loads are issued, so their latency overlaps it
   auto walk = [&](auto&& stage, auto&& probe) __attribute__((always_inline)) {
-    constexpr uint32_t kChunk = 64 * kItems;
-    uint64_t cur[kItems];
+    constexpr uint32_t kChunk = 64 * K;
+    uint64_t cur[K];
     if (flat) {
       if (wtotal) load_flat(cur, 0);
       stage();
       __syncthreads();
       if (wtotal == 0) return;
       for (uint32_t f0 = 0; f0 < wtotal; f0 += kChunk) {
-        uint64_t nxt[kItems];
-        load_flat(nxt, min(f0 + kChunk, (wtotal - 1) & ~(kChunk - 1)));
+        uint64_t nxt[K];
+        load_flat(nxt, min(f0 + kChunk, (wtotal - 1) / kChunk * kChunk));
         uint32_t vm = 0;
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) vm |= uint32_t(f0 + j * 64 + lane < wtotal) << j;
+        for (int j = 0; j < K; ++j) vm |= uint32_t(f0 + j * 64 + lane < wtotal) << j;
         probe(cur, vm, f0 + lane);
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
+        for (int j = 0; j < K; ++j) cur[j] = nxt[j];
       }
     } else {
       load_reg(cur, r, qq, len);
@@ -593,28 +589,28 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
           nq = 0;
           nl = nr_ < nr ? len_at(nr_) : 0u;
         }
-        uint64_t nxt[kItems];
+        uint64_t nxt[K];
         load_reg(nxt, nr_, nq, nl);
         uint32_t vm = 0;
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) vm |= uint32_t(qq + j * 64 + lane < len) << j;
+        for (int j = 0; j < K; ++j) vm |= uint32_t(qq + j * 64 + lane < len) << j;
         probe(cur, vm, pre_at(r) + qq + lane);
         r = nr_;
         qq = nq;
         len = nl;
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) cur[j] = nxt[j];
+        for (int j = 0; j < K; ++j) cur[j] = nxt[j];
       }
     }
   };
   if (fits) {
     walk([&]() __attribute__((always_inline)) { pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent); },
-         [&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
-           pk_probe_items<MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
+         [&](const uint64_t (&v)[K], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+           pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
          });
   } else {
     walk([&]() __attribute__((always_inline)) {},
-         [&](const uint64_t (&v)[kItems], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
+         [&](const uint64_t (&v)[K], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
            probe_hbm_chunk(v, valid, bbase + wpre + srel);
          });
   }
@@ -703,6 +699,33 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
 
 }  // namespace
 
+// Pairs per lane and chunk for the region walk: the K in [kItemsMin, kItemsMax] with the fewest
+// expected item slots per region, region lengths ~ N(L, L) (a region gets each of L * (#regions)
+// tuples with probability 1 / #regions); ties go to the larger K (fewer chunks).
+static int pk_items(double L) {
+#ifdef HJ3D_PK_ITEMS
+  return HJ3D_PK_ITEMS;
+#endif
+  int best = kItemsMax;
+  double best_slots = 0.0;
+  const double sd = std::sqrt(L > 1.0 ? L : 1.0);
+  for (int K = kItemsMax; K >= kItemsMin; --K) {
+    const double c = 64.0 * K;
+    double slots = 0.0, wsum = 0.0;
+    for (int z = -40; z <= 40; ++z) {  // normal quadrature over +-4 sigma
+      const double x = L + 0.1 * z * sd, w = std::exp(-0.005 * z * z);
+      slots += w * std::ceil((x < 1.0 ? 1.0 : x) / c) * c;
+      wsum += w;
+    }
+    slots /= wsum;
+    if (K == kItemsMax || slots < best_slots * 0.999) {
+      best = K;
+      best_slots = slots;
+    }
+  }
+  return best;
+}
+
 bool pk_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe, uint32_t flags) {
   return t->desc.kind == HJ3D_CHAIN && (flags & HJ3D_PROBE_UNIQUE) && !ctx->force_direct && !ctx->pk_off &&
          n_probe >= ctx->radix_min && n_probe > 0 && t->nb_local >= 64 && t->desc.num_buckets >= 2 &&
@@ -776,21 +799,30 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   const int acc = (flags & HJ3D_PROBE_ACCUMULATE) ? 1 : 0;
   const bool flat = HJ3D_PK_FLAT || double(r.n) / double(nreg) < 256.0;
+  const int items = ctx->pk_items ? ctx->pk_items : flat ? kItemsMax : pk_items(double(r.n) / double(nreg));
   uint2* o = static_cast<uint2*>(out);
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
   {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
-#define HJ3D_PK_LAUNCH(MODE, CK)                                                                                     \
-  hipLaunchKernelGGL((k_pk_probe<MODE, CK>), dim3(nblocks), dim3(kPkBlock), 0, s, region, counts, G, uint32_t(cap), \
+#define HJ3D_PK_LAUNCH(K, MODE, CK)                                                                                  \
+  hipLaunchKernelGGL((k_pk_probe<K, MODE, CK>), dim3(nblocks), dim3(kPkBlock), 0, s, region, counts, G, uint32_t(cap), \
                      splits, flat, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pk, t->fm, o, out_cap, ovf, \
                      ctl, partials, res, acc, reinterpret_cast<uint2*>(ctl + 64))
+#define HJ3D_PK_LAUNCH_K(MODE, CK)               \
+  switch (items) {                               \
+    case 5: HJ3D_PK_LAUNCH(5, MODE, CK); break;  \
+    case 6: HJ3D_PK_LAUNCH(6, MODE, CK); break;  \
+    case 7: HJ3D_PK_LAUNCH(7, MODE, CK); break;  \
+    default: HJ3D_PK_LAUNCH(8, MODE, CK); break; \
+  }
     if (emit) {
-      if (ck) HJ3D_PK_LAUNCH(1, true);
-      else HJ3D_PK_LAUNCH(1, false);
+      if (ck) HJ3D_PK_LAUNCH_K(1, true)
+      else HJ3D_PK_LAUNCH_K(1, false)
     } else {
-      if (ck) HJ3D_PK_LAUNCH(0, true);
-      else HJ3D_PK_LAUNCH(0, false);
+      if (ck) HJ3D_PK_LAUNCH_K(0, true)
+      else HJ3D_PK_LAUNCH_K(0, false)
     }
+#undef HJ3D_PK_LAUNCH_K
 #undef HJ3D_PK_LAUNCH
   }
   return hipGetLastError();

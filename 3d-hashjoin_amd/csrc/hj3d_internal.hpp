@@ -78,6 +78,7 @@ struct hj3d_ctx {
   bool nested_sort = false;       // HJ3D_OPT_NESTED_SORT
   bool sel_unfused = false;       // HJ3D_OPT_SEL_UNFUSED
   hj3d::DevBuf sel;               // hj3d_probe_sel: passing (key, row) pairs when not fused
+  int pk_items = 0;                // HJ3D_OPT_PROBE_ITEMS: packed probe pairs per lane and chunk (0 = chosen per probe)
   bool pk_off = false;            // HJ3D_OPT_PACKED_PROBE = 0: the unique chaining probe on (hash, row) pairs
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores

@@ -26,6 +26,7 @@ HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
+OPT_PROBE_ITEMS = 7
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -349,6 +350,10 @@ class Context:
     def packed_probe(self, on: bool = True):
         """A/B switch: the unique chaining probe on packed pairs (default) or on (hash, row) pairs."""
         self.set_option(OPT_PACKED_PROBE, int(on))
+
+    def probe_items(self, k: int = 0):
+        """A/B switch: pairs per lane and chunk of the packed probe's region walk (0 = automatic, 5..8)."""
+        self.set_option(OPT_PROBE_ITEMS, int(k))
 
     def sel_unfused(self, on: bool = True):
         """A/B switch: hj3d_probe_sel selects first instead of fusing into the partitioner."""

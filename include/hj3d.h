@@ -160,7 +160,10 @@ enum {
   /* HJ3D_OPT_PACKED_PROBE (0/1, default 1): the unique chaining probe partitions the probe side into
    * packed {bucket-in-slice | hash / NB, row} pairs and finishes in two launches; 0 keeps the
    * {hash, row} partitioned probe (A/B measurements). */
-  HJ3D_OPT_PACKED_PROBE = 6
+  HJ3D_OPT_PACKED_PROBE = 6,
+  /* HJ3D_OPT_PROBE_ITEMS (0 or 5..8, default 0): pairs per lane and chunk in the packed probe's
+   * region walk; 0 picks it from the expected region length (tests and A/B measurements). */
+  HJ3D_OPT_PROBE_ITEMS = 7
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

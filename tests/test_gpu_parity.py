@@ -367,3 +367,29 @@ def test_chaining_build_skewed_partition(ctx, theta):
         assert {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_c": 0, "sum_h": r.sum_h, "xor_h": r.xor_h} == e.out
         st = t.stats()
         assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
+
+
+@pytest.mark.parametrize("items", [5, 6, 7, 8])
+def test_packed_probe_items_per_lane(ctx, items):
+    """The packed unique probe gives the reference's counters and output pairs for every chunk
+    width of its region walk (HJ3D_OPT_PROBE_ITEMS; config B's default is 7)."""
+    import torch
+    import hj3d
+    cases = [x for x in EXP1 if x[1]["nR"] >= 64 and x[1]["nS"] <= 9_000_000]
+    ctx.radix_min(0)
+    ctx.probe_items(items)
+    try:
+        for name, g in cases:
+            R, S, b = exp1_rel(g)
+            dR, dS = dev(R), dev(S)
+            nb = hj3d.num_buckets_exp1("Csr", len(R), g["numDvSa"], b)
+            ref = g["plans"]["Csr"]
+            out = torch.zeros((max(len(S), 1), 2), dtype=torch.int32, device="cuda")
+            got = hj3d.exp1_plan(ctx, "Csr", dR, dS, nb, out=out, stats=False)
+            assert (got["c_probe"], got["c_cmp"], got["c_top"]) == (ref["c_probe"], ref["c_cmp"], ref["c_top"]), name
+            host = out.cpu().numpy().view(np.uint32)
+            host = host[host[:, 1] != 0xFFFFFFFF]
+            assert host_checksums(host) == ref["out"], name
+    finally:
+        ctx.probe_items(0)
+        ctx.radix_min(1 << 20)
