@@ -114,6 +114,7 @@ void hj3d_ctx_destroy(hj3d_ctx* ctx) {
   ctx->misc.release();
   ctx->ctl.release();
   ctx->scan_status.release();
+  ctx->part_cur.release();
   for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;

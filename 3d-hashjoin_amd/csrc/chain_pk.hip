@@ -36,7 +36,7 @@ constexpr int kPkBlock = 1024;
 #define HJ3D_PK_AHEAD 1   // tiles of keys in flight: 1 (loaded after the stage is built) or 2
 #endif
 #ifndef HJ3D_PK_FLAT
-#define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (else only short ones)
+#define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (1; measured slower at config B) or only short ones
 #endif
 #ifndef HJ3D_PK_SINK
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
@@ -476,6 +476,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
                                                        int accumulate, uint2* __restrict__ sink) {
   __shared__ uint32_t lds[kLdsWords];
   __shared__ uint32_t wtot[kPkBlock / kWave];
+  __shared__ uint32_t rpre[kPkBlock / kWave][65];
   __shared__ uint64_t bbase;
   __shared__ uint64_t red[kPkBlock / kWave][kProbeFields];
   __shared__ uint32_t flag;
@@ -499,6 +500,8 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   uint32_t wtotal;
   const uint32_t my_pre = wave_excl_scan(my_len, &wtotal);  // wave-local stream offset of region `lane`
   if (lane == 0) wtot[wid] = wtotal;
+  rpre[wid][lane] = uint32_t(lane) < nr ? my_pre : ~0u;  // region starts of the wave's stream
+  if (lane == 0) rpre[wid][64] = ~0u;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint32_t t = 0;
@@ -515,24 +518,23 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   // otherwise a chunk stays inside one region). Loads and stores of the steady-state loops are
   // unconditional (clamped addresses, absent items stored to the sink): with a fixed count per chunk
   // the wait for the next chunk's pairs leaves this chunk's stores in flight.
-  uint32_t rb = 0;  // flat: last region starting at or before the block of 64
+  // flat: each lane keeps its own cursor, region cr holding stream positions [its start, nst), and
+  // steps it forward (positions only grow, the region starts come from rpre): a compare per item
+  const auto src_off = [&](uint32_t k) __attribute__((always_inline)) {
+    return int64_t((uint64_t(g_lo + wid + kWaves * k) * P + p) * cap);
+  };
+  uint32_t cr = 0, nst = rpre[wid][1];
+  int64_t cbase = src_off(0);  // region cr's first pair - its stream start
   auto load_flat = [&](uint64_t (&v)[K], uint32_t f0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < K; ++j) {
-      // block start and item clamped into the stream (the last prefetch re-reads the last chunk)
-      const uint32_t b = min(f0 + j * 64, wtotal - 1), f = min(f0 + j * 64 + lane, wtotal - 1);
-      if (pre_at(rb) > b) rb = 0;
-      while (rb + 1 < nr && pre_at(rb + 1) <= b) ++rb;
-      uint32_t rr = rb, pr = pre_at(rb);
-      for (uint32_t t = rb + 1; t < nr; ++t) {  // region starts inside the block
-        const uint32_t pt = pre_at(t);
-        if (pt > b + 63) break;
-        if (pt <= f) {
-          rr = t;
-          pr = pt;
-        }
+      const uint32_t f = min(f0 + j * 64 + lane, wtotal - 1);  // clamped (the last prefetch re-reads)
+      while (f >= nst) {
+        ++cr;
+        cbase = src_off(cr) - int64_t(nst);
+        nst = rpre[wid][cr + 1];
       }
-      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src_of(rr) + (f - pr)));
+      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(region + (cbase + int64_t(f))));
     }
   };
   // non-flat cursor: region r, offset qq

@@ -85,6 +85,10 @@ struct hj3d_ctx {
   hj3d::DevBuf ctl;
   uint32_t scan_epoch = 0;  // tags the look-back status words of exclusive_scan_u32 (scan.hip)
   hj3d::DevBuf scan_status;  // its per-tile status words (no other use)
+  // partition cursors of the build partitioner (radix.hip partition_pairs): two sets of 2049 words,
+  // call k counts into set k & 1 and clears set (k + 1) & 1 for the next call; zeroed once here
+  hj3d::DevBuf part_cur;
+  uint32_t part_parity = 0;
   hipError_t ensure_ctl() {
     if (ctl.p) return hipSuccess;
     hipError_t e = ctl.ensure(128 * sizeof(uint64_t));  // 8 control words; [64, 128): store sink

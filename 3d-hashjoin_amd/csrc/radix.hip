@@ -55,11 +55,14 @@ inline FastDiv make_div(uint32_t d) {
 }
 
 // Partition sizes per scatter workgroup: workgroup g of the G = gridDim.x persistent workgroups
-// counts the tiles g, g + G, ... that k_rp_scatter's workgroup g will write, so one column per
-// workgroup (hist[p * G + g]) instead of one per tile: P x G counters, whose partition-major
-// write-out is then small (a per-tile column costs a 64-B line per counter: P x ntiles lines).
+// counts the tiles g, g + G, ... that k_rp_scatter's workgroup g will write, then claims its run
+// inside every partition with one atomic on the partition's cursor (cur[p] ends as the partition's
+// size) and keeps the run's offset in its row hist[g * P + p]. The order of the workgroups' runs
+// inside a partition is the atomics' order: no counter depends on it (build3 places rows by rank,
+// the nested builds aggregate), and no scan over the P x G counts is needed.
 __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
-                                                     uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist) {
+                                                     uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist,
+                                                     uint32_t* __restrict__ cur) {
   __shared__ uint32_t cnt[kMaxParts];
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
   __syncthreads();
@@ -87,7 +90,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
       if (bl[j] < nbl) atomicAdd(&cnt[fw.div(bl[j])], 1u);
   }
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) hist[uint64_t(p) * gridDim.x + blockIdx.x] = cnt[p];
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
+    const uint32_t c = cnt[p];
+    hist[uint64_t(blockIdx.x) * P + p] = c ? atomicAdd(&cur[p], c) : 0u;
+  }
 }
 
 template <int BLOCK = kJBlock>
@@ -100,9 +106,12 @@ __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
 // the probe's fan-out, instead of one scattered 8-B store per tuple.
 // Persistent over tiles (one workgroup per CU, LDS-bound): the next tile's keys are loaded
 // before the current tile's write-out, so the CU's reads and writes overlap.
+// Partition starts: an LDS scan of the P partition sizes (k_rp_hist's cursors) in every workgroup;
+// workgroup 0 writes them to ps[0..P] and clears the other cursor set for the next call.
 __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
-                                                        uint2* __restrict__ out) {
+                                                        const uint32_t* __restrict__ cur, uint32_t* __restrict__ cur_next,
+                                                        uint32_t* __restrict__ ps, uint2* __restrict__ out) {
   __shared__ uint2 stage[kPTile];
   __shared__ uint32_t loc[kMaxParts];   // local counts, then local run starts
   __shared__ uint32_t gb[kMaxParts];    // global run start of each partition for this tile
@@ -113,8 +122,18 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
   }
-  // this workgroup's write cursor per partition (its column of the scanned k_rp_hist counts)
-  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = offs[uint64_t(p) * gridDim.x + blockIdx.x];
+  // this workgroup's write cursor per partition: partition start + its run's offset (k_rp_hist)
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = cur[p];
+  __syncthreads();
+  const uint32_t total = lds_excl_scan<kPBlock>(gb, P, wsum);
+  for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
+    if (blockIdx.x == 0) ps[p] = gb[p];
+    gb[p] += offs[uint64_t(blockIdx.x) * P + p];
+  }
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) ps[P] = total;
+    for (uint32_t p = threadIdx.x; p <= kMaxParts; p += kPBlock) cur_next[p] = 0;
+  }
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     for (uint32_t p = threadIdx.x; p < P; p += kPBlock) loc[p] = 0;
     const uint64_t base = uint64_t(tile) * kPTile;
@@ -157,11 +176,6 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
       gb[p] += (p + 1 < P ? loc[p + 1] : m) - loc[p];
     __syncthreads();
   }
-}
-
-__global__ void k_rp_starts(const uint32_t* __restrict__ offs, uint32_t G, uint32_t P, uint32_t* __restrict__ ps) {
-  for (uint32_t p = blockIdx.x * blockDim.x + threadIdx.x; p <= P; p += gridDim.x * blockDim.x)
-    ps[p] = offs[uint64_t(p) * G];
 }
 
 // Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. BLOCK threads.
@@ -236,7 +250,7 @@ constexpr uint32_t kBuildStage = 15000;
 // stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) scatter
 // through HBM instead (sorting their small buckets there).
 constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12288 pairs
-__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps, uint32_t pst,
+__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
                                                        uint32_t* __restrict__ off, uint2* __restrict__ ent) {
   __shared__ uint32_t cnt[kBuildSlice2 + 1];
@@ -247,7 +261,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
   uint2 ea[kB3Per], eb[kB3Per];
   auto load = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
     if (p >= P) return;
-    const uint32_t s0 = ps[p * pst], s1 = ps[(p + 1) * pst];
+    const uint32_t s0 = ps[p], s1 = ps[p + 1];
     if (s1 - s0 > kCap) return;
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
@@ -258,7 +272,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
   auto build = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
     const uint32_t b0 = p * W;
     const uint32_t nbs = min(W, nbl - b0);
-    const uint32_t s0 = ps[p * pst], s1 = ps[(p + 1) * pst], m = s1 - s0;
+    const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
     for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
     __syncthreads();
     if (m > kCap) {  // skewed partition: scatter through HBM, sort the small buckets there
@@ -980,33 +994,36 @@ Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
   return pl;
 }
 
-// Partition `r` into (hash, row) pairs by bucket range; ps[0..P] = partition starts.
+// Partition `r` into (hash, row) pairs by bucket range; ps[0..P] = partition starts. Two launches:
+// k_rp_hist (sizes, runs claimed on the partition cursors) and k_rp_scatter (starts, pairs).
 // t_hist / t_scatter: timer phases of the two streaming kernels (-1: untimed).
-// starts = false: ps[] is not written; partition p then starts at hist[p * G] of the scanned
-// histogram (kScrPHist, G = the persistent workgroup count), which k_rp_build3 reads directly.
 hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
-                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1, bool starts = true) {
+                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1) {
   hipError_t e;
-  // G persistent workgroups in both passes, one histogram column per workgroup
+  if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
+  // G persistent workgroups in both passes, one row of run offsets per workgroup
   const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
-  const uint64_t hn = uint64_t(pl.P) * g + 1;
-  if ((e = ctx->scratch[kScrPHist].ensure(hn * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPHist].ensure(uint64_t(pl.P) * g * sizeof(uint32_t))) != hipSuccess) return e;
   uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
+  if (!ctx->part_cur.p) {
+    if ((e = ctx->part_cur.ensure(2 * (kMaxParts + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(ctx->part_cur.p, 0, ctx->part_cur.bytes, s)) != hipSuccess) return e;
+  }
+  uint32_t* cur = ctx->part_cur.as<uint32_t>() + (ctx->part_parity & 1u) * (kMaxParts + 1);
+  uint32_t* cur_next = ctx->part_cur.as<uint32_t>() + ((ctx->part_parity + 1) & 1u) * (kMaxParts + 1);
+  ctx->part_parity ^= 1u;
   const RelView v = view_of(r);
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
-  if (r.n) {
+  {
     PhaseTimer tm(ctx, t_hist);
     hipLaunchKernelGGL(k_rp_hist, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P, pl.ntiles,
-                       hist);
+                       hist, cur);
   }
-  if ((e = exclusive_scan_u32(ctx, hist, hist, hn - 1, s)) != hipSuccess) return e;
-  if (r.n) {
+  {
     PhaseTimer tm(ctx, t_scatter);
     hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
-                       pl.ntiles, hist, out);
+                       pl.ntiles, hist, cur, cur_next, ps, out);
   }
-  if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
-  if (starts) hipLaunchKernelGGL(k_rp_starts, dim3((pl.P + 256) / 256), dim3(256), 0, s, hist, g, pl.P, ps);
   return hipGetLastError();
 }
 
@@ -1068,15 +1085,10 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
-  // the staged build reads the partition starts straight from the scanned histogram
-  const bool direct_starts = nbl && staged && r.n;
-  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s, -1, -1, !direct_starts)) != hipSuccess) return e;
-  const uint32_t pg = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
-  const uint32_t* starts = direct_starts ? ctx->scratch[kScrPHist].as<const uint32_t>() : ps;
-  const uint32_t pst = direct_starts ? pg : 1u;
+  if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   if (nbl && staged) {
     const uint32_t g = pl.P < uint32_t(ctx->num_cus) ? pl.P : uint32_t(ctx->num_cus);
-    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, starts, pst, t->fm,
+    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, ps, t->fm,
                        uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
