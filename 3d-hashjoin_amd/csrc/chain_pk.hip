@@ -45,12 +45,18 @@ constexpr int kPkBlock = 1024;
 #define HJ3D_PK_GUARD 1   // partition: key loads and rank atomics guarded per tuple (else clamped, unconditional)
 #endif
 constexpr int kPkRounds = HJ3D_PK_ROUNDS;
+#ifndef HJ3D_PK_SEG
+#define HJ3D_PK_SEG 16    // pairs per region segment (16: 128 B)
+#endif
+#ifndef HJ3D_PK_STAGE
+#define HJ3D_PK_STAGE 17408  // LDS stage (pairs): the tile + the carried pairs (< SEG per slice)
+#endif
 constexpr int kPkTile = kPkBlock * kPkRounds;
-static_assert((kPkTile & (kPkTile - 1)) == 0, "tile must be a power of two");
-constexpr int kPkTBits = __builtin_ctz(kPkTile);
-constexpr uint32_t kPkSeg = 16;                // 128-B region segments
-// tile + carried pairs (< 16 per slice, ~7.5 on average): 14336 pairs at 4096-tuple tiles
-constexpr uint32_t kPkStage = kPkTile + 10240 > 17408 ? 17408 : kPkTile + 10240;
+constexpr int kPkTBits = 32 - __builtin_clz(uint32_t(kPkTile - 1));  // bits of a rank inside the tile
+constexpr uint32_t kPkSeg = HJ3D_PK_SEG;
+static_assert(kPkSeg == 8 || kPkSeg == 16, "64- or 128-B segments");
+constexpr uint32_t kPkStage = kPkTile + (kPkSeg - 1) * 1024 > HJ3D_PK_STAGE ? HJ3D_PK_STAGE : kPkTile + (kPkSeg - 1) * 1024;
+static_assert(kPkTile <= kPkStage && kPkStage < 65536, "the tile alone fits the stage; stage offsets in 16 bits");
 constexpr uint32_t kSortedMaxPk = 32;
 constexpr uint32_t kOvfFlag = 0x80000000u;
 
@@ -226,7 +232,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       if (rk[j] == kInvalid) continue;
       const uint32_t li = uint32_t(j) * kPkBlock + me;
       const uint32_t row = IMPLICIT ? rb + li : r.row(uint64_t(base) + li);
-      stage[sbase[rk[j] >> kPkTBits] + (rk[j] & (kPkTile - 1))] = make_uint2(h[j], row);
+      stage[sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1))] = make_uint2(h[j], row);
     }
     load(h, pw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
     __syncthreads();
