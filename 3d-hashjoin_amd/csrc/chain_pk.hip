@@ -793,13 +793,13 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   const RelView v = view_of(r);
   const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
   {
-    PhaseTimer tm(ctx, HJ3D_T_SCATTER);
+    KernelSpan tm(ctx, HJ3D_T_SCATTER);
     if (sel) {
-      if (imp) hipLaunchKernelGGL((k_pk_part<true, true>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
-      else hipLaunchKernelGGL((k_pk_part<false, true>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      if (imp) tm.launch(k_pk_part<true, true>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      else tm.launch(k_pk_part<false, true>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
     } else {
-      if (imp) hipLaunchKernelGGL((k_pk_part<true, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
-      else hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      if (imp) tm.launch(k_pk_part<true, false>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      else tm.launch(k_pk_part<false, false>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
     }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -811,9 +811,9 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   uint2* o = static_cast<uint2*>(out);
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
   {
-    PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
+    KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
 #define HJ3D_PK_LAUNCH(K, MODE, CK)                                                                                  \
-  hipLaunchKernelGGL((k_pk_probe<K, MODE, CK>), dim3(nblocks), dim3(kPkBlock), 0, s, region, counts, G, uint32_t(cap), \
+  tk.launch(k_pk_probe<K, MODE, CK>, dim3(nblocks), dim3(kPkBlock), s, region, counts, G, uint32_t(cap),        \
                      splits, flat, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pk, t->fm, o, out_cap, ovf, \
                      ctl, partials, res, acc, reinterpret_cast<uint2*>(ctl + 64))
 #define HJ3D_PK_LAUNCH_K(MODE, CK)               \

@@ -2,6 +2,7 @@
 // translation units. Not installed; the public surface is include/hj3d.h.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -345,6 +346,38 @@ struct PhaseTimer {
     if (!b) return;
     (void)hipEventRecord(b, ctx->stream);
     ctx->spans[phase].push_back({a, b});
+  }
+};
+
+// One kernel's span for the per-kernel timers: the two events travel with the dispatch
+// (hipExtLaunchKernel), so timing a kernel puts no marker packet between it and its neighbours.
+// launch(kernel, grid, block, stream, args...) launches with or without them.
+#ifndef HJ3D_EXT_TIMING
+#define HJ3D_EXT_TIMING 1
+#endif
+struct KernelSpan {
+  hj3d_ctx* ctx;
+  int phase;
+  hipEvent_t a = nullptr, b = nullptr;
+  PhaseTimer* marker = nullptr;  // HJ3D_EXT_TIMING = 0: the marker-event form, for A/B
+  KernelSpan(hj3d_ctx* c, int p) : ctx(c), phase(p) {
+    if (!ctx->timing || p < 0) return;
+    if (!HJ3D_EXT_TIMING) {
+      marker = new PhaseTimer(c, p);
+      return;
+    }
+    a = take_event(ctx);
+    b = a ? take_event(ctx) : nullptr;
+    if (!b) a = nullptr;
+  }
+  ~KernelSpan() {
+    delete marker;
+    if (a && b) ctx->spans[phase].push_back({a, b});
+  }
+  template <typename F, typename... Args>
+  void launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    if (a) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
+    else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
   }
 };
 
