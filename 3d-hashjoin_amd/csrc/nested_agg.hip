@@ -38,6 +38,9 @@ constexpr uint32_t kAggRounds = 1;  // initial rounds per partition (2, 3: slowe
 constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
 constexpr int kAggU = 8;             // pairs per thread and step (the next step's in flight)
 constexpr int kWavesA = kAggBlock / kWave;
+#ifndef HJ3D_NAGG_WAVES
+#define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
+#endif
 
 __device__ __forceinline__ uint32_t slot_of(uint32_t h) { return __umulhi(h * 0x9E3779B1u, kAggCap); }
 // per-key probe step in [1, kAggCap) (double hashing: no primary clusters, so the longest probe
@@ -382,8 +385,17 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   if ((e = t->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
   // partition width: kAggW buckets, narrower when that would leave the chip with fewer than two
   // partitions per CU (config E: 2M buckets -> 512 partitions of 4K instead of 342 of 6K)
-  uint32_t W = uint32_t((uint64_t(nbl) + 2 * ctx->num_cus - 1) / (2 * ctx->num_cus));
+  // Then the count is rounded up to whole waves of workgroups (one k_nagg workgroup per CU at a
+  // time, latency-bound, so a last wave of a few partitions costs as long as a full one): config C
+  // 9.6M buckets -> 1792 partitions of 5357 (7 waves) instead of 1563 of 6144 (6.1 waves, run as 7).
+  const uint32_t G = uint32_t(ctx->num_cus);
+  uint32_t W = uint32_t((uint64_t(nbl) + 2 * G - 1) / (2 * G));
   W = W < 1024 ? 1024 : W > kAggW ? kAggW : W;
+  {
+    const uint64_t P0 = (uint64_t(nbl) + W - 1) / W, P1 = (P0 + G - 1) / G * G;
+    const uint64_t W1 = (uint64_t(nbl) + P1 - 1) / P1;
+    if (HJ3D_NAGG_WAVES && P1 <= 2048 && W1 >= 1024) W = uint32_t(W1);
+  }
   const uint32_t P = (nbl + W - 1) / W;
   // scratch: pairs (n uint2) | main records before compaction (n uint4) | starts, key counts
   if ((e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
