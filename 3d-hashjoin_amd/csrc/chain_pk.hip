@@ -41,6 +41,9 @@ constexpr int kPkBlock = 1024;
 #ifndef HJ3D_PK_SINK
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
 #endif
+#ifndef HJ3D_PK_FEWBAR
+#define HJ3D_PK_FEWBAR 0  // partition: five barriers per tile instead of seven (1: A/B variant)
+#endif
 #ifndef HJ3D_PK_GUARD
 #define HJ3D_PK_GUARD 1   // partition: key loads and rank atomics guarded per tuple (else clamped, unconditional)
 #endif
@@ -170,10 +173,13 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   };
   uint32_t npassed = 0;
   auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1]) __attribute__((always_inline)) {
-    loc[me] = 0;
+    // HJ3D_PK_FEWBAR: loc[me] is cleared right after its count is read (nothing touches it again
+    // in the tile) and no barrier ends the tile: the next tile's first LDS writes (stage, seginfo,
+    // sbase) come after its ranking barrier, which every thread reaches only when done reading
+    if (!HJ3D_PK_FEWBAR) loc[me] = 0;
     const uint32_t base = tile * kPkTile;
     uint32_t rk[kPkRounds];
-    __syncthreads();
+    if (!HJ3D_PK_FEWBAR) __syncthreads();
     // hash, bucket, slice, rank: the LDS atomics are unconditional (invalid tuples add 0 to slot 0)
 #pragma unroll
     for (int j = 0; j < kPkRounds; ++j) {
@@ -203,6 +209,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     }
     __syncthreads();
     const uint32_t my_c = me < P ? loc[me] : 0u;
+    if (HJ3D_PK_FEWBAR) loc[me] = 0;
     const auto seg_counts = [&]() __attribute__((always_inline)) {
       const uint32_t L = my_kc + my_c;
       return (L << 16) | (L / kPkSeg);
@@ -254,8 +261,12 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       my_cur += F;
       my_kc = my_len - F;
     }
-    __syncthreads();
+    if (!HJ3D_PK_FEWBAR) __syncthreads();
   };
+  if (HJ3D_PK_FEWBAR) {
+    loc[me] = 0;
+    __syncthreads();
+  }
   load(ha, pa, blockIdx.x);
   if constexpr (HJ3D_PK_AHEAD == 2) {
     load(hb, pb, blockIdx.x + gridDim.x);
