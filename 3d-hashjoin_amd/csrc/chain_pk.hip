@@ -42,7 +42,7 @@ constexpr int kPkBlock = 1024;
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
 #endif
 #ifndef HJ3D_PK_FEWBAR
-#define HJ3D_PK_FEWBAR 0  // partition: five barriers per tile instead of seven (1: A/B variant)
+#define HJ3D_PK_FEWBAR 1  // partition: five barriers per tile instead of seven (0: A/B variant)
 #endif
 #ifndef HJ3D_PK_GUARD
 #define HJ3D_PK_GUARD 1   // partition: key loads and rank atomics guarded per tuple (else clamped, unconditional)
