@@ -153,6 +153,14 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       if (value != 0 && (value < 5 || value > 8)) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PROBE_ITEMS: 0 or 5..8");
       ctx->pk_items = int(value);
       return HJ3D_OK;
+    case HJ3D_OPT_PK_SLICE:
+      if (value < 0 || value == 1 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_SLICE: 0 or >= 2");
+      ctx->pk_slice_max = uint32_t(value);
+      return HJ3D_OK;
+    case HJ3D_OPT_PK_STAGE:
+      if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
+      ctx->pk_stage = uint32_t(value);
+      return HJ3D_OK;
     default: return fail(ctx, HJ3D_EINVAL, "hj3d_ctx_set_option: unknown option");
   }
 }
@@ -502,6 +510,17 @@ hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out) {
   if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe2_result");
   static_assert(sizeof(hj3d_probe2_res) == 12 * sizeof(uint64_t), "probe2 result layout");
   std::memcpy(out, h, sizeof(hj3d_probe2_res));
+  return HJ3D_OK;
+}
+
+hj3d_status hj3d_probe_geometry(hj3d_ctx* ctx, uint64_t nb_local, uint64_t n_build, uint32_t out[5]) {
+  if (!ctx || !out || nb_local == 0 || nb_local >= (1ull << 32)) return HJ3D_EINVAL;
+  const PkPlan pl = pk_plan(ctx, uint32_t(nb_local), n_build);
+  out[0] = pl.W;
+  out[1] = pl.P;
+  out[2] = pl.C;
+  out[3] = pl.W1;
+  out[4] = pl.P1;
   return HJ3D_OK;
 }
 

@@ -100,7 +100,7 @@ template <bool IMPLICIT, bool SEL>
 __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint32_t ntiles, uint32_t cap,
                                                       uint2* __restrict__ region, uint32_t* __restrict__ counts,
                                                       uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
-                                                      SelRange sel) {
+                                                      SelRange sel, uint32_t stage_lim) {
   __shared__ uint2 stage[kPkStage];
   __shared__ uint32_t loc[kPkBlock];
   __shared__ uint32_t sbase[kPkBlock];
@@ -110,7 +110,10 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint32_t my_reg = (blockIdx.x * P + me) * cap;  // region of slice `me` (host: G * P * cap < 2^31)
   uint2 creg[kPkSeg - 1];
-  uint32_t my_kc = 0, my_cur = 0;
+  // my_cur: pairs taken by slice `me`'s region so far; my_end: where its region stopped taking
+  // pairs (cap, or the start of the first segment that did not fit: after a mid-stream carry flush
+  // the cursor is no longer segment-aligned, so a segment may straddle the region's end)
+  uint32_t my_kc = 0, my_cur = 0, my_end = cap;
 #pragma unroll
   for (int j = 0; j < int(kPkSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
   uint32_t ha[kPkRounds], hb[kPkRounds], pa[SEL ? kPkRounds : 1], pb[SEL ? kPkRounds : 1];
@@ -144,8 +147,8 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     for (int j = 0; j < int(kPkSeg) - 1; ++j) {
       const bool v = me < P && uint32_t(j) < my_kc;
       const uint32_t o = my_cur + j;
-      if (v && o < cap) region[my_reg + o] = creg[j];
-      to_ovf(creg[j], me, v && o >= cap);
+      if (v && o < my_end) region[my_reg + o] = creg[j];
+      to_ovf(creg[j], me, v && o >= my_end);
     }
     my_cur += my_kc;
     my_kc = 0;
@@ -216,7 +219,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     };
     uint32_t tot;
     uint32_t pre = scan(seg_counts(), &tot);
-    if ((tot >> 16) > kPkStage) {  // too many carried pairs: write them out; the tile alone fits
+    if ((tot >> 16) > stage_lim) {  // too many carried pairs: write them out; the tile alone fits
       flush_carry();
       pre = scan(seg_counts(), &tot);
     }
@@ -228,8 +231,12 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       for (int j = 0; j < int(kPkSeg) - 1; ++j)
         if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
       for (uint32_t sg = 0; sg < my_len / kPkSeg; ++sg) {
-        const uint32_t o = my_cur + sg * kPkSeg;  // segment-aligned; cap is a multiple of kPkSeg
-        seginfo[my_fseg + sg] = make_uint2(o < cap ? my_reg + o : (kOvfFlag | me), my_loc + sg * kPkSeg);
+        // segment-aligned (cap is a multiple of kPkSeg) unless a mid-stream flush moved the cursor:
+        // a segment goes to the region only whole, else (all of it) to the overflow list
+        const uint32_t o = my_cur + sg * kPkSeg;
+        const bool fit = o + kPkSeg <= my_end;
+        if (!fit && o < my_end) my_end = o;
+        seginfo[my_fseg + sg] = make_uint2(fit ? my_reg + o : (kOvfFlag | me), my_loc + sg * kPkSeg);
       }
     }
     __syncthreads();
@@ -278,7 +285,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa);
   }
   flush_carry();
-  if (me < P) counts[blockIdx.x * P + me] = min(my_cur, cap);
+  if (me < P) counts[blockIdx.x * P + me] = min(my_cur, my_end);
   // n_probe: every scanned tuple (the reference's probe count), or the selection's passing tuples
   if constexpr (SEL) {
     uint32_t c = npassed;
@@ -290,8 +297,145 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   }
 }
 
+// ---- k_pk_split: the second partition level (more than 1024 slices) ----
+// k_pk_part then partitions by coarse ranges of C slices (its packed word holds the bucket inside
+// the coarse range); workgroup (p1, s) takes the pass-1 regions g in [G1 s / S2, G1 (s + 1) / S2) of
+// coarse range p1 as one stream, re-packs every pair for its slice p = p1 C + c (bucket inside the
+// slice) and writes it to the fine region (s, p) at fine[(s * P + p) * cap2], counts2[s * P + p]
+// pairs: exactly the region layout k_pk_probe walks (G = S2 regions per slice). Per 8192-pair tile:
+// rank by slice with a wave-level multi-split (one ballot per bit of c, one LDS atomic per slice and
+// wave), stage the tile slice-major in LDS, write each slice's run out with consecutive lanes on
+// consecutive pairs. Pairs past a fine region's capacity go to the overflow list as {h, row}.
+constexpr int kSpRounds = 8;
+constexpr int kSpTile = kPkBlock * kSpRounds;
+constexpr uint32_t kSpMaxC = 64;
+__global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__ reg1,
+                                                       const uint32_t* __restrict__ cnt1, uint32_t G1, uint32_t P1,
+                                                       uint32_t cap1, uint32_t S2, PkGeom pk, uint32_t C,
+                                                       uint32_t cbits, uint32_t cap2, uint2* __restrict__ reg2,
+                                                       uint32_t* __restrict__ cnt2, uint2* __restrict__ ovf,
+                                                       uint64_t* __restrict__ ctl) {
+  __shared__ uint2 stage[kSpTile];
+  __shared__ uint8_t cof[kSpTile];
+  __shared__ uint32_t rstart[66];
+  __shared__ uint32_t tcnt[2][kSpMaxC];
+  __shared__ uint32_t tstart[kSpMaxC];
+  __shared__ uint2 dlim[kSpMaxC];  // {fine index of stage position 0 of the slice's run, region end}
+  __shared__ uint32_t cur[kSpMaxC];
+  const uint32_t me = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const uint32_t p1 = blockIdx.x / S2, s = blockIdx.x % S2;
+  const uint32_t g_lo = uint32_t(uint64_t(G1) * s / S2), g_hi = uint32_t(uint64_t(G1) * (s + 1) / S2);
+  const uint32_t nr = g_hi - g_lo;  // <= 64 (host: G1 <= 64 * S2)
+  const uint32_t pbase = p1 * C;    // first fine slice of the coarse range
+  if (me < 64) {
+    const uint32_t len = uint32_t(lane) < nr ? cnt1[uint64_t(g_lo + lane) * P1 + p1] : 0u;
+    uint32_t tot;
+    const uint32_t pre = wave_excl_scan(len, &tot);
+    if (uint32_t(lane) < nr) rstart[lane] = pre;
+    if (lane == 0) {
+      rstart[nr] = tot;
+      rstart[nr + 1] = tot;
+    }
+  }
+  if (me < kSpMaxC) {
+    tcnt[0][me] = 0;
+    tcnt[1][me] = 0;
+    cur[me] = 0;
+  }
+  __syncthreads();
+  const uint32_t total = rstart[nr];
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  // per-lane stream cursor: region cr holds stream positions [rstart[cr], nst)
+  uint32_t cr = 0, nst = rstart[1];
+  const uint2* rsrc = reg1 + (uint64_t(g_lo) * P1 + p1) * cap1;
+  auto load = [&](uint2 (&v)[kSpRounds], uint32_t t0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kSpRounds; ++j) {
+      const uint32_t f = t0 + uint32_t(j) * kPkBlock + me;
+      v[j] = make_uint2(0, 0);
+      if (f < total) {
+        while (f >= nst) {
+          ++cr;
+          nst = rstart[cr + 1];
+          rsrc = reg1 + (uint64_t(g_lo + cr) * P1 + p1) * cap1;
+        }
+        v[j] = rsrc[f - rstart[cr]];
+      }
+    }
+  };
+  uint2 cv[kSpRounds];
+  load(cv, 0);
+  uint32_t par = 0;
+  for (uint32_t t0 = 0; t0 < total; t0 += kSpTile, par ^= 1u) {
+    uint2 nv[kSpRounds];
+    load(nv, t0 + kSpTile);
+    uint32_t cc[kSpRounds], rk[kSpRounds];
+#pragma unroll
+    for (int j = 0; j < kSpRounds; ++j) {
+      const bool valid = t0 + uint32_t(j) * kPkBlock + me < total;
+      const uint32_t bic = cv[j].x >> pk.qbits;  // bucket inside the coarse range
+      const uint32_t c = valid ? pk.dw.div(bic) : 0u;
+      cv[j].x = ((bic - c * pk.W) << pk.qbits) | (cv[j].x & pk.qmask);
+      cc[j] = c;
+      // lanes of this wave with the same slice: one ballot per bit of c
+      uint64_t m = __ballot(valid);
+      for (uint32_t b = 0; b < cbits; ++b) {
+        const uint64_t mb = __ballot(valid && ((c >> b) & 1u));
+        m &= ((c >> b) & 1u) ? mb : ~mb;
+      }
+      const bool leader = (m & lt) == 0;
+      uint32_t base = 0;
+      if (valid && leader) base = atomicAdd(&tcnt[par][c], uint32_t(__popcll(m)));
+      base = __shfl(base, valid ? __ffsll((unsigned long long)m) - 1 : lane, kWave);
+      rk[j] = valid ? base + uint32_t(__popcll(m & lt)) : kInvalid;
+    }
+    __syncthreads();
+    if (me < 64) {  // slice runs of the tile: starts in the stage, destinations, cursors
+      uint32_t run_pre = 0;
+      for (uint32_t c0 = 0; c0 < C; c0 += 64) {
+        const uint32_t c = c0 + lane;
+        const uint32_t n = c < C ? tcnt[par][c] : 0u;
+        uint32_t tot;
+        const uint32_t pre = wave_excl_scan(n, &tot) + run_pre;
+        if (c < C) {
+          const uint32_t fb = (s * pk.P + pbase + c) * cap2;
+          tstart[c] = pre;
+          dlim[c] = make_uint2(fb + cur[c] - pre, fb + cap2);
+          cur[c] += n;
+          tcnt[par ^ 1u][c] = 0;
+        }
+        run_pre += tot;
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kSpRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint32_t k = tstart[cc[j]] + rk[j];
+      stage[k] = cv[j];
+      cof[k] = uint8_t(cc[j]);
+    }
+    __syncthreads();
+    const uint32_t tn = min(uint32_t(kSpTile), total - t0);
+    for (uint32_t k = me; k < tn; k += kPkBlock) {
+      const uint32_t c = cof[k];
+      const uint2 dl = dlim[c];
+      const uint2 e = stage[k];
+      const uint32_t d = dl.x + k;
+      const bool fit = d < dl.y;
+      if (fit) reg2[d] = e;
+      pk_ovf_append(!fit, make_uint2(pk.hash_of(e.x, pbase + c), e.y), ovf, ctl);
+    }
+#pragma unroll
+    for (int j = 0; j < kSpRounds; ++j) cv[j] = nv[j];
+  }
+  __syncthreads();
+  if (me < C && pbase + me < pk.P) cnt2[uint64_t(s) * pk.P + pbase + me] = min(cur[me], cap2);
+}
+
 // ---- k_pk_probe ----
-constexpr uint32_t kLdsWords = kProbeLdsWords;
+constexpr uint32_t kLdsWords = kPkLdsWords;
 // K = pairs per lane and chunk (the next chunk in flight), chosen per probe from the expected
 // region length (pk_items): a region of L pairs costs ceil(L / 64K) chunks of 64K item slots, so
 // K = 7 walks config B's ~384-pair regions in one 448-slot chunk where K = 8 spends 512 slots.
@@ -751,80 +895,143 @@ bool pk_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_pr
          n_probe < (1ull << 32) && t->built;
 }
 
+// The largest slice width W (buckets) whose LDS image (W directory words, two words per entry,
+// ~W * fill entries) fits kPkLdsWords with 6 sigma of headroom on the entry count.
+static uint32_t pk_slice_width(double fill) {
+  double W = double(kPkLdsWords) / (1.0 + 2.0 * fill);
+  for (int i = 0; i < 6; ++i) W = (double(kPkLdsWords) - 2.0 - 12.0 * std::sqrt(W * fill)) / (1.0 + 2.0 * fill);
+  return W < 64.0 ? 64u : uint32_t(W);
+}
+
+PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nbl, uint64_t n_build) {
+  PkPlan pl;
+  const double fill = n_build ? double(n_build) / double(nbl) : 0.0;
+  uint32_t W = pk_slice_width(fill);
+  if (ctx->pk_slice_max && W > ctx->pk_slice_max) W = ctx->pk_slice_max;
+  if (W > nbl) W = nbl;
+  uint32_t P = (nbl + W - 1) / W;
+  // whole waves of probe workgroups (one per CU): the slice count rounded up to a multiple of the
+  // CUs, staying at one partition level when that is possible
+  const uint32_t ncu = uint32_t(ctx->num_cus);
+  if (P >= ncu / 2) {
+    uint32_t Pq = (P + ncu - 1) / ncu * ncu;
+    if (P <= uint32_t(kPkBlock) && Pq > uint32_t(kPkBlock)) Pq = kPkBlock;
+    P = Pq;
+    W = (nbl + P - 1) / P;
+    P = (nbl + W - 1) / W;
+  }
+  pl.W = W;
+  pl.P = P;
+  pl.C = (P + kPkBlock - 1) / kPkBlock;  // slices per coarse range of the first level
+  pl.W1 = W * pl.C;
+  pl.P1 = (nbl + pl.W1 - 1) / pl.W1;
+  return pl;
+}
+
 hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out, uint64_t out_cap,
                     uint64_t* res, hipStream_t s, const SelArgs* sel) {
   hipError_t e;
   const uint32_t nbl = t->nb_local, nb = uint32_t(t->desc.num_buckets);
-  // slice width: 80% of the LDS slice budget at the table's mean bucket fill
-  const double fill = t->n_build ? double(t->n_build) / double(nbl) : 0.0;
-  uint32_t W = uint32_t(0.8 * kLdsWords / (1.0 + 2.0 * fill));
-  if (W < 64) W = 64;
-  if (W > nbl) W = nbl;
-  const uint32_t P = (nbl + W - 1) / W;
-  if (P > uint32_t(kPkBlock)) return hipErrorNotSupported;  // one slice per partitioning thread
-  // the packed word: bucket in slice (bits of W - 1) and the quotient h / NB (bits of its max)
+  const PkPlan pl = pk_plan(ctx, nbl, t->n_build);
+  const bool two = pl.C > 1;
+  if (pl.C > kSpMaxC) return hipErrorNotSupported;
+  // the packed word: bucket in the (first-level) slice and the quotient h / NB (bits of its max)
   auto bits = [](uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; };
-  const uint32_t qbits = bits(0xFFFFFFFFull / nb), wbits = bits(W - 1);
+  const uint32_t qbits = bits(0xFFFFFFFFull / nb), wbits = bits(pl.W1 - 1);
   if (qbits + wbits > 32) return hipErrorNotSupported;
   SelRange sr{};
   if (sel && !SelRange::from(*sel, &sr)) return hipErrorNotSupported;
   const uint32_t ntiles = uint32_t((r.n + kPkTile - 1) / kPkTile);
   const uint32_t G = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
   // region capacity: expected pairs per (workgroup, slice) + 8 sigma + slack, whole segments
+  auto capacity = [](double ex) {
+    uint64_t c = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
+    return (c + kPkSeg - 1) / kPkSeg * kPkSeg;
+  };
   const uint64_t per_g = uint64_t((ntiles + G - 1) / G) * kPkTile;
-  const double ex = double(per_g < r.n ? per_g : r.n) / P;
-  uint64_t cap = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
-  cap = (cap + kPkSeg - 1) / kPkSeg * kPkSeg;
-  const uint64_t nreg = uint64_t(G) * P;
+  const uint64_t cap = capacity(double(per_g < r.n ? per_g : r.n) / pl.P1);
+  const uint64_t nreg = uint64_t(G) * pl.P1;
   if (nreg * cap >= (1ull << 31)) return hipErrorNotSupported;
+  // second level: S2 workgroups per coarse range, each writing one fine region per slice
+  const uint32_t S2 = two ? (G < 16u ? G : 16u) : 0u;
+  const uint64_t cap2 = two ? capacity(double(r.n) / (double(S2) * pl.P)) : 0;
+  const uint64_t nreg2 = uint64_t(S2) * pl.P;
+  if (two && nreg2 * cap2 >= (1ull << 31)) return hipErrorNotSupported;
   if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPHist].ensure(nreg * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  if (two) {
+    if ((e = ctx->scratch[kScrPk2].ensure(nreg2 * cap2 * sizeof(uint2))) != hipSuccess) return e;
+    if ((e = ctx->scratch[kScrPk2Cnt].ensure(nreg2 * sizeof(uint32_t))) != hipSuccess) return e;
+  }
   const uint32_t want_blocks = uint32_t(ctx->num_cus) * 2;
-  uint32_t splits = P < want_blocks ? (want_blocks + P - 1) / P : 1u;
-  if (splits > G) splits = G;
-  const uint32_t nblocks = P * splits;
+  const uint32_t Gp = two ? S2 : G;  // regions per slice that the probe walks
+  uint32_t splits = pl.P < want_blocks ? (want_blocks + pl.P - 1) / pl.P : 1u;
+  if (splits > Gp) splits = Gp;
+  const uint32_t nblocks = pl.P * splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
-  PkGeom pk;
-  pk.dnb = FastDiv32::make(nb);
-  pk.dw = W >= 2 ? FastDiv32::make(W) : FastDiv32{};
-  pk.nb = nb;
-  pk.lo = uint32_t(t->desc.bucket_lo);
-  pk.nbl = nbl;
-  pk.W = W;
-  pk.P = P;
-  pk.qbits = qbits;
-  pk.qmask = qbits >= 32 ? 0xFFFFFFFFu : ((1u << qbits) - 1);
+  auto geom = [&](uint32_t W, uint32_t P) {
+    PkGeom g;
+    g.dnb = FastDiv32::make(nb);
+    g.dw = W >= 2 ? FastDiv32::make(W) : FastDiv32{};
+    g.nb = nb;
+    g.lo = uint32_t(t->desc.bucket_lo);
+    g.nbl = nbl;
+    g.W = W;
+    g.P = P;
+    g.qbits = qbits;
+    g.qmask = qbits >= 32 ? 0xFFFFFFFFu : ((1u << qbits) - 1);
+    return g;
+  };
+  const PkGeom pk1 = geom(pl.W1, pl.P1), pk = geom(pl.W, pl.P);
   uint2* region = ctx->scratch[kScrPairs].as<uint2>();
   uint32_t* counts = ctx->scratch[kScrPHist].as<uint32_t>();
   uint2* ovf = ctx->scratch[kScrSortV].as<uint2>();
   uint64_t* ctl = ctx->ctl.as<uint64_t>();
   const RelView v = view_of(r);
   const bool imp = r.row_off == HJ3D_ROW_IMPLICIT;
+  const uint32_t slim = ctx->pk_stage ? (ctx->pk_stage < kPkStage ? ctx->pk_stage : kPkStage) : kPkStage;
   {
     KernelSpan tm(ctx, HJ3D_T_SCATTER);
+    const uint32_t c32 = uint32_t(cap);
     if (sel) {
-      if (imp) tm.launch(k_pk_part<true, true>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
-      else tm.launch(k_pk_part<false, true>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      if (imp) tm.launch(k_pk_part<true, true>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
+      else tm.launch(k_pk_part<false, true>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
     } else {
-      if (imp) tm.launch(k_pk_part<true, false>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
-      else tm.launch(k_pk_part<false, false>, dim3(G), dim3(kPkBlock), s, v, pk, ntiles, uint32_t(cap), region, counts, ovf, ctl, sr);
+      if (imp) tm.launch(k_pk_part<true, false>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
+      else tm.launch(k_pk_part<false, false>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
     }
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  const uint2* pregion = region;
+  const uint32_t* pcounts = counts;
+  uint32_t pcap = uint32_t(cap);
+  if (two) {
+    uint2* fine = ctx->scratch[kScrPk2].as<uint2>();
+    uint32_t* fcnt = ctx->scratch[kScrPk2Cnt].as<uint32_t>();
+    KernelSpan ts(ctx, HJ3D_T_HIST);
+    ts.launch(k_pk_split, dim3(pl.P1 * S2), dim3(kPkBlock), s, static_cast<const uint2*>(region),
+              static_cast<const uint32_t*>(counts), G, pl.P1, uint32_t(cap), S2, pk, pl.C, bits(pl.C - 1),
+              uint32_t(cap2), fine, fcnt, ovf, ctl);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    pregion = fine;
+    pcounts = fcnt;
+    pcap = uint32_t(cap2);
+  }
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   const int acc = (flags & HJ3D_PROBE_ACCUMULATE) ? 1 : 0;
-  const bool flat = HJ3D_PK_FLAT || double(r.n) / double(nreg) < 256.0;
-  const int items = ctx->pk_items ? ctx->pk_items : flat ? kItemsMax : pk_items(double(r.n) / double(nreg));
+  const uint64_t preg = uint64_t(Gp) * pl.P;
+  const bool flat = HJ3D_PK_FLAT || double(r.n) / double(preg) < 256.0;
+  const int items = ctx->pk_items ? ctx->pk_items : flat ? kItemsMax : pk_items(double(r.n) / double(preg));
   uint2* o = static_cast<uint2*>(out);
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
   {
     KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
 #define HJ3D_PK_LAUNCH(K, MODE, CK)                                                                                  \
-  tk.launch(k_pk_probe<K, MODE, CK>, dim3(nblocks), dim3(kPkBlock), s, region, counts, G, uint32_t(cap),        \
+  tk.launch(k_pk_probe<K, MODE, CK>, dim3(nblocks), dim3(kPkBlock), s, pregion, pcounts, Gp, pcap,              \
                      splits, flat, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pk, t->fm, o, out_cap, ovf, \
                      ctl, partials, res, acc, reinterpret_cast<uint2*>(ctl + 64))
 #define HJ3D_PK_LAUNCH_K(MODE, CK)               \

@@ -62,7 +62,7 @@ struct hj3d_ctx {
   int num_cus = 256;
   std::string last_error;
   // scratch arena slots (see api for their use)
-  hj3d::DevBuf scratch[12];
+  hj3d::DevBuf scratch[14];
   hj3d::DevBuf res;       // device result slot (u64 fields) for probe / probe2
   hj3d::DevBuf misc;      // small device reductions (statistics)
   uint32_t res_flags = 0;     // flags of the last probe (overflow check in hj3d_probe_result)
@@ -81,6 +81,8 @@ struct hj3d_ctx {
   hj3d::DevBuf sel;               // hj3d_probe_sel: passing (key, row) pairs when not fused
   int pk_items = 0;                // HJ3D_OPT_PROBE_ITEMS: packed probe pairs per lane and chunk (0 = chosen per probe)
   bool pk_off = false;            // HJ3D_OPT_PACKED_PROBE = 0: the unique chaining probe on (hash, row) pairs
+  uint32_t pk_slice_max = 0;      // HJ3D_OPT_PK_SLICE: cap on the packed probe's slice width (0 = LDS-sized)
+  uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
@@ -263,6 +265,13 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
 bool pk_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe, uint32_t flags);
 hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                     uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr);
+// Slice geometry of the packed probe: P slices of W buckets (a slice's directory + entries fit the
+// probe workgroup's LDS); above 1024 slices, two partition levels: k_pk_part into P1 coarse ranges
+// of C slices (W1 = C * W buckets), then k_pk_split by slice.
+struct PkPlan {
+  uint32_t W = 0, P = 0, C = 1, W1 = 0, P1 = 0;
+};
+PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nb_local, uint64_t n_build);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
@@ -312,7 +321,10 @@ enum ScratchSlot {
   kScrPairs = 8,    // radix-partitioned (hash, row) pairs
   kScrPHist = 9,    // radix partition histograms / offsets
   kScrPartial = 10, // per-block result partials
-  kScrPStart = 11   // partition starts of the probe side
+  kScrPStart = 11,  // partition starts of the probe side
+  kScrPk2 = 12,     // packed probe, second partition level: fine regions
+  kScrPk2Cnt = 13,  // and their pair counts
+  kScrSlots = 14
 };
 
 // Per-block result partials: kernels store their block totals (block_store) to

@@ -20,6 +20,8 @@ __host__ __device__ __forceinline__ uint64_t region_idx(uint32_t g, uint32_t p, 
 
 constexpr int kJBlock = 1024;               // build / probe workgroups (16 waves, 1 per CU)
 constexpr uint32_t kProbeLdsWords = 36864;  // 144 KB LDS table slice per probe workgroup
+// the packed probe (chain_pk.hip): everything of the 160 KB LDS but its ~5.3 KB of walk state
+constexpr uint32_t kPkLdsWords = 39552;
 constexpr int kSegItems = 8;                // pairs per lane and step of the region walk (4, 12, 16: slower)
 
 // Walks the regions of partition p assigned to share sp (of `splits`): wave w takes regions

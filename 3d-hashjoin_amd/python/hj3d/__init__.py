@@ -27,6 +27,7 @@ PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
 OPT_PROBE_ITEMS = 7
+OPT_PK_SLICE, OPT_PK_STAGE = 8, 9
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -122,6 +123,7 @@ def lib():
         "hj3d_partition": (st, [p, R, u64, u32, p, p]),
         "hj3d_partition_sel": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, p]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
+        "hj3d_probe_geometry": (C.c_int, [C.c_void_p, u64, u64, C.POINTER(u32)]),
         "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
         "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
         "hj3d_select": (st, [p, R, C.POINTER(_SelPred), u32, p, p]),
@@ -354,6 +356,23 @@ class Context:
     def probe_items(self, k: int = 0):
         """A/B switch: pairs per lane and chunk of the packed probe's region walk (0 = automatic, 5..8)."""
         self.set_option(OPT_PROBE_ITEMS, int(k))
+
+    def pk_slice_max(self, w: int = 0):
+        """Test hook: upper bound on the packed probe's slice width in buckets (0 = LDS-sized); a
+        small bound puts small tables on the two-level (k_pk_part + k_pk_split) path."""
+        self.set_option(OPT_PK_SLICE, int(w))
+
+    def pk_stage(self, pairs: int = 0):
+        """Test hook: the packed partitioner's carry-flush threshold (0 = its whole LDS stage; 1 =
+        write the carried partial segments out after every tile)."""
+        self.set_option(OPT_PK_STAGE, int(pairs))
+
+    def pk_plan(self, nb_local: int, n_build: int) -> dict:
+        """The packed probe's slice geometry for a table of nb_local buckets and n_build entries
+        (hj3d_probe_geometry): {W, P, C, W1, P1}."""
+        out = (C.c_uint32 * 5)()
+        self._check(lib().hj3d_probe_geometry(self.h, nb_local, n_build, out), "hj3d_probe_geometry")
+        return dict(zip(("W", "P", "C", "W1", "P1"), list(out)))
 
     def sel_unfused(self, on: bool = True):
         """A/B switch: hj3d_probe_sel selects first instead of fusing into the partitioner."""
@@ -609,5 +628,5 @@ class Table:
             pass
 
 
-from .plans import (EXP1_PLANS, exp1_plan, exp1_relations_ref, exp4_plan, exp4_relations_ref,  # noqa: E402,F401
-                    num_buckets_exp1)
+from .plans import (EXP1_PLANS, exp1_plan, exp1_plan_sharded, exp1_relations_ref, exp4_plan,  # noqa: E402,F401
+                    exp4_relations_ref, merge_shard_stats, num_buckets_exp1)

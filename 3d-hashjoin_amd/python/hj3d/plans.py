@@ -59,6 +59,100 @@ def exp1_plan(ctx: Context, plan: str, R, S, nb: int, out=None, table: Table | N
     return res
 
 
+STAT_ADD = ("nb", "empty", "entries", "distinct", "cc0_sum", "cc0_cnt", "cc1_sum", "cc1_cnt")
+
+
+def merge_shard_stats(parts: list) -> dict:
+    """HtStatistics of a table split into disjoint bucket ranges, from the shards' own: counts add,
+    extremes take max / min (a shard without a non-empty bucket has no cc1_min), i.e. the
+    single-table statistics (the merge dist.allreduce_stats does across ranks)."""
+    out = {k: sum(st[k] for st in parts) for k in STAT_ADD}
+    out["cc0_max"] = max(st["cc0_max"] for st in parts)
+    out["cc1_max"] = max(st["cc1_max"] for st in parts)
+    out["cc0_min"] = min(st["cc0_min"] for st in parts)
+    mins = [st["cc1_min"] for st in parts if st["cc1_cnt"]]
+    out["cc1_min"] = min(mins) if mins else 0
+    return out
+
+
+def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=None, stats: bool = True,
+                      checksum: bool = True, timing: list | None = None) -> dict:
+    """The multi-GPU split of SURVEY §8(e) emulated on ONE device, owner after owner: both
+    relations are partitioned into `parts` bucket ranges by the exchange partitioner
+    (hj3d_partition, as every rank does before the all-to-all), then for each owner p a table over
+    its range [lo, hi) is built from its build pairs and probed with its probe pairs (explicit global
+    row ids, as received). This is each rank's compute at its real geometry (bucket_lo != 0,
+    |R| / parts buckets), without the exchange; the counters add up to the single-table run's and
+    are returned in exp1_plan's form. timing (a list): one dict of per-owner phase times (ms, the
+    library's HIP-event timers) is appended per owner, plus {"owner": "partition", ...} first."""
+    import torch
+    from . import (T_BUILD, T_HIST, T_PARTITION, T_PROBE, T_PROBE_KERNEL, T_SCATTER, MASK64, part_range)
+    kind, bside, bkey, pkey, unique, unnest = EXP1_PLANS[plan]
+    build = Rel(R if bside == "R" else S, key_word=bkey)
+    probe = Rel(S if bside == "R" else R, key_word=pkey)
+    dev = R.device
+    bp = torch.empty((max(build.n, 1), 2), dtype=torch.int32, device=dev)
+    pp = torch.empty((max(probe.n, 1), 2), dtype=torch.int32, device=dev)
+    bc = torch.zeros(parts, dtype=torch.int64, device=dev)
+    pc = torch.zeros(parts, dtype=torch.int64, device=dev)
+    phases = {"build": T_BUILD, "probe": T_PROBE, "part_kernel": T_SCATTER, "split_kernel": T_HIST,
+              "probe_kernel": T_PROBE_KERNEL, "partition": T_PARTITION}
+
+    def timers():
+        ctx.sync()
+        d = {}
+        for k, ph in phases.items():
+            ms, cnt = ctx.timer(ph)
+            if cnt:
+                d[k] = ms
+        ctx.timer_reset()
+        return d
+    if timing is not None:
+        ctx.timing(True)
+        ctx.timer_reset()
+    ctx.partition(build, nb, parts, bp, bc)
+    ctx.partition(probe, nb, parts, pp, pc)
+    if timing is not None:
+        timing.append(dict(owner="partition", **timers()))
+    bcs = [0] + torch.cumsum(bc, 0).tolist()
+    pcs = [0] + torch.cumsum(pc, 0).tolist()
+    tot = {"c_probe": 0, "c_cmp": 0, "c_unnest": 0, "c_top": 0, "n": 0, "sum_a": 0, "sum_b": 0, "sum_c": 0,
+           "sum_h": 0, "xor_h": 0, "overflow": False}
+    shard_stats = []
+    ooff = 0
+    for p in range(parts):
+        lo, hi = part_range(nb, parts, p)
+        t = Table(ctx, kind, nb, lo, hi)
+        nbp, npp = bcs[p + 1] - bcs[p], pcs[p + 1] - pcs[p]
+        t.reserve(max(nbp, 1))
+        t.build(Rel(bp[bcs[p]:bcs[p + 1]], key_word=0, row_word=1, n=nbp))
+        o = out[ooff:] if out is not None else None
+        r = ctx.probe(t, Rel(pp[pcs[p]:pcs[p + 1]], key_word=0, row_word=1, n=npp), unique=unique, unnest=unnest,
+                      out=o, checksum=checksum)
+        if kind == HJ3D_CHAIN:
+            c_probe, c_unnest, c_top = r.n_out, 0, r.n_out
+            ooff += npp
+        else:
+            c_probe, c_unnest, c_top = r.n_matched, (r.n_out if unnest else 0), (r.n_out if unnest else r.n_matched)
+            ooff += r.n_out
+        for k, v in (("c_probe", c_probe), ("c_cmp", r.n_cmps), ("c_unnest", c_unnest), ("c_top", c_top),
+                     ("n", r.n_out), ("sum_a", r.sum_a), ("sum_b", r.sum_b), ("sum_c", r.sum_c), ("sum_h", r.sum_h)):
+            tot[k] = (tot[k] + v) & MASK64
+        tot["xor_h"] ^= r.xor_h
+        tot["overflow"] = tot["overflow"] or r.overflow
+        if stats:
+            shard_stats.append(t.stats())
+        if timing is not None:
+            timing.append(dict(owner=p, bucket_lo=lo, bucket_hi=hi, build_tuples=nbp, probe_tuples=npp, **timers()))
+        t.close()
+    res = {"nb": nb, "c_build": build.n, "c_probe": tot["c_probe"], "c_cmp": tot["c_cmp"],
+           "c_unnest": tot["c_unnest"], "c_top": tot["c_top"], "overflow": tot["overflow"],
+           "out": {k: tot[k] for k in ("n", "sum_a", "sum_b", "sum_c", "sum_h", "xor_h")}}
+    if stats:
+        res["stats"] = merge_shard_stats(shard_stats)
+    return res
+
+
 def exp1_relations_ref(nR: int, nS: int, skew: bool = False, theta: float = 1.0, t: int = 0, device="cuda"):
     """The reference's experiment-1 relations R {k,0,0}, S {i,a,0} (main_experiment1.cc:415-457,
     495-515) from the bit-exact generator (hj3d_gen_exp1_ref), as (n, 3) int32 device tensors:

@@ -468,7 +468,8 @@ def main():
     kern_avg = {}
     kprobe = "k_pk_probe" if packed else ("k_rp_probe_seg" if unique else "k_rn_probe_seg")
     kpart = "k_pk_part" if packed else "k_rp_part1"
-    for name, ph in ((kprobe, hj3d.T_PROBE_KERNEL), (kpart, hj3d.T_SCATTER)):
+    for name, ph in ((kprobe, hj3d.T_PROBE_KERNEL), (kpart, hj3d.T_SCATTER)) + \
+            ((("k_pk_split", hj3d.T_HIST),) if packed else ()):
         ms, cnt = ctx.timer(ph)
         kern_avg[name] = ms / cnt if cnt else None
     # verification step (outside the timed region): the same step once more with the
@@ -565,6 +566,8 @@ def main():
     # ---- roofline of the dominant kernel ----
     # Algorithmic bytes per launch, n = probe tuples of this rank per launch:
     #   k_pk_part (k_rp_part1)      n * (12 + 8)   read the S tuple (AoS {k,a,b}), write the packed pair
+    #   k_pk_split (tables of more than 1024 LDS slices: the second partition level)
+    #                               n * (8 + 8)    read the coarse pair, write the fine pair
     #   k_pk_probe (k_rp_probe_seg) n * (8 + 8) + |R| * 8 + nb * 4   read the pair, write the output pair, stage
     #                                                    the table slices (entries + directory) once
     #   k_rn_probe_seg  (3D plans, unnest materialised): n * (8 + 16) read the pair, write the slot's
@@ -575,7 +578,7 @@ def main():
     n = probe_n_local / launches
     tuple_bytes = 8 if sharded else 12
     if unique:
-        alg = {kpart: n * (tuple_bytes + 8),
+        alg = {kpart: n * (tuple_bytes + 8), "k_pk_split": n * 16,
                kprobe: n * (8 + (8 if emit else 0)) + (nR_tot // world) * 8 + (nb // world) * 4}
     else:
         n_keys = dv if plan == "Nrs" else nR_tot
@@ -637,6 +640,9 @@ def main():
             "exchange": ("libhj3d hj3d_comm_* over RCCL" if sharded and not args.rehearse else
                          "torch.distributed gloo, host-staged (rehearsal)" if sharded else None),
             "rehearsal_one_gpu": bool(args.rehearse),
+            # the packed probe's LDS-slice geometry on this rank: P slices of W buckets; C > 1 = two
+            # partition levels (k_pk_part into P1 ranges of C slices, k_pk_split by slice)
+            "probe_slices": ctx.pk_plan(max(nb // world, 1), max(nB, 1)) if packed else None,
         },
         "build_ms": build_ms,
         "probe_ms": probe_ms,

@@ -163,7 +163,16 @@ enum {
   HJ3D_OPT_PACKED_PROBE = 6,
   /* HJ3D_OPT_PROBE_ITEMS (0 or 5..8, default 0): pairs per lane and chunk in the packed probe's
    * region walk; 0 picks it from the expected region length (tests and A/B measurements). */
-  HJ3D_OPT_PROBE_ITEMS = 7
+  HJ3D_OPT_PROBE_ITEMS = 7,
+  /* HJ3D_OPT_PK_SLICE (buckets, 0 or >= 2; default 0): upper bound on the packed probe's slice
+   * width (normally the largest that fits one workgroup's LDS). Tables of more than 1024 slices
+   * take the two-level partition (k_pk_part into coarse ranges, k_pk_split by slice), so a small
+   * bound puts small tables on that path (tests). */
+  HJ3D_OPT_PK_SLICE = 8,
+  /* HJ3D_OPT_PK_STAGE (pairs, default 0 = the whole LDS stage): the packed partitioner writes its
+   * carried partial segments out early once the carries plus a tile exceed this many pairs
+   * (tests: 1 flushes after every tile). */
+  HJ3D_OPT_PK_STAGE = 9
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
@@ -175,7 +184,8 @@ enum {
   HJ3D_T_PROBE_KERNEL = 2,  /* the join-probe kernel launches only (radix path: k_rp_probe) */
   HJ3D_T_PARTITION = 3,     /* hj3d_partition (multi-GPU exchange partitioner) */
   HJ3D_T_SCATTER = 4,       /* radix probe path: probe-side partition scatter kernel */
-  HJ3D_T_HIST = 5,          /* radix probe path: probe-side partition histogram kernel */
+  HJ3D_T_HIST = 5,          /* radix probe path: probe-side partition histogram kernel; packed probe
+                             * of more than 1024 slices: its second partition level (k_pk_split) */
   HJ3D_T_NTIMERS = 6
 };
 hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
@@ -241,6 +251,12 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
                                uint64_t num_buckets, uint32_t nparts, void* out_pairs_dev, void* counts_dev);
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
+/* Slice geometry the packed unique probe takes for a chaining table of nb_local buckets holding
+ * n_build entries (diagnostic; no device work): out = {W, P, C, W1, P1}: P slices of W buckets
+ * (one slice's directory + entries fill one probe workgroup's LDS); C > 1: two partition levels,
+ * P1 coarse ranges of W1 = C * W buckets. Replaces nothing of the reference (whose chains are not
+ * partitioned); bench.py reports it beside config D's line. */
+hj3d_status hj3d_probe_geometry(hj3d_ctx* ctx, uint64_t nb_local, uint64_t n_build, uint32_t out[5]);
 
 /* ---- the exchange itself: RCCL over xGMI, one communicator per context ----
  * One process (or host thread) per GPU, one context per process. RCCL is resolved at run time: a

@@ -1,0 +1,100 @@
+#!/usr/bin/env python3
+"""Config D's 8-GPU split emulated on ONE GPU: per-rank compute at the real geometry, timed.
+
+The reference relations (|R| = 1e8, |S| = 1e9, hj3d_gen_exp1_ref) are split into `--parts` owner
+bucket ranges by the exchange partitioner (hj3d_partition), then each owner in turn builds its
+table over [lo, hi) from its build pairs and probes it with its probe pairs (explicit global
+rows), as every rank does after the all-to-all (hj3d.exp1_plan_sharded). The counters summed over
+the owners are checked against the reference binary's fixture. Prints one JSON line: per owner the
+build / probe phase times and the probe kernels' times with their roofline fractions (algorithmic
+bytes as bench.py counts them for a received-pair probe side: k_pk_part 8 + 8 B per pair,
+k_pk_probe 8 + 8 B per pair + the table slices once), and the exchange partitioner's time.
+Per-rank compute, exchange not included: NOT a scaling number.
+
+Usage: python scripts/d_shards.py [--parts 8] [--plan Csr] [--reps 3] [--nR 1e8 --nS 1e9]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
+PEAK = 8000.0  # GB/s
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--parts", type=int, default=8)
+    ap.add_argument("--plan", default="Csr", choices=["Csr", "Nsr"])
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--nR", type=float, default=1e8)
+    ap.add_argument("--nS", type=float, default=1e9)
+    a = ap.parse_args()
+    import torch
+    import hj3d
+    nR, nS = int(a.nR), int(a.nS)
+    t0 = time.perf_counter()
+    R, S = hj3d.exp1_relations_ref(nR, nS)
+    gen_s = time.perf_counter() - t0
+    ctx = hj3d.Context(0)
+    nb = hj3d.num_buckets_exp1(a.plan, nR, 0, 1)
+    out = torch.empty((nS, 2), dtype=torch.int32, device="cuda") if a.plan == "Csr" else None
+    hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False)  # warm-up
+    runs = []
+    for _ in range(a.reps):
+        tm = []
+        hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False, timing=tm)
+        runs.append(tm)
+    got = hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out)  # verification run
+    fx_path = os.path.join(ROOT, "tests", "golden", f"exp1_R{nR}_S{nS}_uni.json")
+    verify = None
+    if os.path.exists(fx_path):
+        ref = json.load(open(fx_path))["plans"].get(a.plan)
+        if ref:
+            verify = (got["c_cmp"] == ref["c_cmp"] and got["out"] == ref["out"] and got["c_top"] == ref["c_top"] and
+                      all(got["stats"][k] == ref["stats"][k] for k in ref["stats"] if k in got["stats"]))
+
+    def avg(owner, key):
+        v = [r[i][key] for r in runs for i in range(len(r)) if r[i]["owner"] == owner and key in r[i]]
+        return sum(v) / len(v) if v else None
+    owners = []
+    for p in range(a.parts):
+        first = runs[0][p + 1]
+        npp, nbp = first["probe_tuples"], first["build_tuples"]
+        d = {"owner": p, "bucket_lo": first["bucket_lo"], "bucket_hi": first["bucket_hi"],
+             "build_tuples": nbp, "probe_tuples": npp}
+        for k in ("build", "probe", "part_kernel", "split_kernel", "probe_kernel"):
+            d[k + "_ms"] = avg(p, k)
+        if a.plan == "Csr":
+            nbl = first["bucket_hi"] - first["bucket_lo"]
+            d["slices"] = ctx.pk_plan(nbl, nbp)
+            alg = {"part_kernel": npp * 16, "split_kernel": npp * 16, "probe_kernel": npp * 16 + nbp * 8 + nbl * 4}
+            for k, b in alg.items():
+                ms = d[k + "_ms"]
+                if ms:
+                    d[k + "_frac"] = b / (ms * 1e-3) / 1e9 / PEAK
+            d["probe_phase_frac"] = (npp * (16 + 8)) / (d["probe_ms"] * 1e-3) / 1e9 / PEAK
+        owners.append(d)
+    part_ms = avg("partition", "partition")
+    line = {
+        "what": f"config D {a.parts}-owner split emulated on one GPU, plan {a.plan}: per-rank compute at the "
+                f"{a.parts}-GPU geometry, owners run one after another; exchange (xGMI) NOT included; not a "
+                "scaling number",
+        "nR": nR, "nS": nS, "num_buckets": nb, "reps": a.reps, "input_generation_s": gen_s,
+        "exchange_partition_ms_both_relations": part_ms,
+        "exchange_partition_frac": ((nR + nS) * 20) / (part_ms * 1e-3) / 1e9 / PEAK if part_ms else None,
+        "owners": owners,
+        "max_owner_probe_ms": max(o["probe_ms"] for o in owners),
+        "max_owner_build_ms": max(o["build_ms"] for o in owners),
+        "counters": {"c_cmp": got["c_cmp"], "c_top": got["c_top"]},
+        "verified_against_reference_fixture": verify,
+    }
+    print(json.dumps(line))
+    if verify is False:
+        sys.exit("verification failed")
+
+
+if __name__ == "__main__":
+    main()

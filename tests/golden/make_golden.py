@@ -36,8 +36,8 @@ EXP1 = [
     # the headline configs at their exact sizes (BASELINE configs B and C; ~7 min each)
     ("exp1_R10000000_S100000000_uni", [10000000, 100000000, 0, 1.0, 0, 1]),
     ("exp1_R10000000_S100000000_zipf08", [10000000, 100000000, 1, 0.8, 0, 1]),
-    # config D (|R| = 1e8, |S| = 1e9; the Csr plan only: ~12 min, ~30 GB of host memory)
-    ("exp1_R100000000_S1000000000_uni", [100000000, 1000000000, 0, 1.0, 0, 1, "nodump", "Csr"]),
+    # config D (|R| = 1e8, |S| = 1e9; the Csr plan and the 3D plan Nsr: ~25 min, ~30 GB of host memory)
+    ("exp1_R100000000_S1000000000_uni", [100000000, 1000000000, 0, 1.0, 0, 1, "nodump", "Csr,Nsr"]),
 ]
 EXP4 = [
     ("exp4_R3_a2_A2_b2_B1", [3, 2, 2, 2, 1, "dump"]),   # App. A print-relations case
