@@ -38,6 +38,9 @@ constexpr int kPkBlock = 1024;
 #ifndef HJ3D_PK_FLAT
 #define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (1; measured slower at config B) or only short ones
 #endif
+#ifndef HJ3D_PK_DIAG
+#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups
+#endif
 #ifndef HJ3D_PK_SINK
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
 #endif
@@ -256,7 +259,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       const uint32_t j = kk % kPkSeg;
       const uint2 e = stage[si.y + j];
       const bool spill = si.x & kOvfFlag;
-      if (!spill) region[si.x + j] = e;
+      if (!spill && HJ3D_PK_DIAG != 1) region[si.x + j] = e;
       to_ovf(e, si.x & ~kOvfFlag, spill);
     }
     // the run's tail (< one segment) becomes the slice's carry
@@ -460,7 +463,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t 
       const bool ok = (valid >> (g + j)) & 1u;
       const uint32_t x = uint32_t(v[g + j]);
       q[j] = x & pk.qmask;
-      const uint32_t w = ldir[ok ? x >> pk.qbits : 0u];
+      const uint32_t w = HJ3D_PK_DIAG == 2 ? 0u : ldir[ok ? x >> pk.qbits : 0u];
       d[j] = ok ? w : 0u;
       match[j] = kInvalid;
       cmps[j] = d[j] & 0xFFFFu;

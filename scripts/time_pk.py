@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""Kernel timing of the packed unique probe (and the chaining build) on device-generated key/FK
+relations of a given size, with the library's per-kernel HIP-event timers: for A/B sweeps over
+variant builds (HJ3D_LIB) and diagnostic variants (HJ3D_PK_DIAG: results not checked).
+Prints one JSON line: mean ms of build, k_pk_part, k_pk_split, k_pk_probe, probe phase."""
+import argparse
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--nR", type=float, default=1e7)
+    ap.add_argument("--nS", type=float, default=1e8)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-emit", action="store_true")
+    ap.add_argument("--label", default=os.path.basename(os.path.dirname(os.environ.get("HJ3D_LIB", "default/x"))))
+    a = ap.parse_args()
+    import torch
+    import hj3d
+    nR, nS = int(a.nR), int(a.nS)
+    ctx = hj3d.Context(0)
+    R = torch.zeros((nR, 3), dtype=torch.int32, device="cuda")
+    S = torch.zeros((nS, 3), dtype=torch.int32, device="cuda")
+    ctx.gen_keys(R, 0, 0, nR, 11)
+    ctx.gen_keys(S, 0, 0, 0, 0)
+    ctx.gen_fk(S, 1, 0, nR, 12)
+    out = None if a.no_emit else torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+    t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nR)
+    t.reserve(nR)
+    relR, relS = hj3d.Rel(R, 0), hj3d.Rel(S, 1)
+    for _ in range(3):
+        t.build(relR)
+        ctx.probe(t, relS, unique=True, out=out, fetch=False)
+    ctx.sync()
+    ctx.timing(True)
+    ctx.timer_reset()
+    for _ in range(a.reps):
+        t.build(relR)
+        ctx.probe(t, relS, unique=True, out=out, fetch=False)
+    ctx.sync()
+    res = {"label": a.label, "nR": nR, "nS": nS, "emit": out is not None}
+    for k, ph in (("build", hj3d.T_BUILD), ("probe", hj3d.T_PROBE), ("k_pk_part", hj3d.T_SCATTER),
+                  ("k_pk_split", hj3d.T_HIST), ("k_pk_probe", hj3d.T_PROBE_KERNEL)):
+        ms, cnt = ctx.timer(ph)
+        if cnt:
+            res[k] = round(ms / cnt, 4)
+    r = ctx.probe_result()
+    res["n_out"] = r.n_out
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()
