@@ -155,8 +155,8 @@ struct hj3d_comm_state {
   hipStream_t xstream = nullptr;     // exchange stream (asynchronous exchanges)
   hipEvent_t ready = nullptr;        // "the context stream reached this exchange"
   static constexpr uint32_t kTickets = 64;
-  hipEvent_t done[kTickets] = {};    // "exchange t has landed", on xstream
-  uint32_t next_ticket = 0;
+  hipEvent_t done[kTickets] = {};    // "exchange t has landed", on xstream (slot t % kTickets)
+  uint32_t next_ticket = 0;          // tickets count up; slot t % kTickets holds the latest one
   DevBuf counts;                     // transposed send / received counts
 };
 
@@ -289,6 +289,11 @@ hj3d_status hj3d_comm_rank(const hj3d_ctx* ctx, int* rank, int* world) {
 
 hj3d_status hj3d_comm_counts(hj3d_ctx* ctx, const void* counts_dev, uint32_t chunks, int64_t* send_host,
                              int64_t* recv_host) {
+  return hj3d_comm_counts_cap(ctx, counts_dev, chunks, ~0ull, send_host, recv_host);
+}
+
+hj3d_status hj3d_comm_counts_cap(hj3d_ctx* ctx, const void* counts_dev, uint32_t chunks, uint64_t recv_cap,
+                                 int64_t* send_host, int64_t* recv_host) {
   hj3d_comm_state* c = st(ctx);
   if (!c || !counts_dev || !chunks || !recv_host) return HJ3D_EINVAL;
   const uint32_t P = uint32_t(c->world);
@@ -309,11 +314,32 @@ hj3d_status hj3d_comm_counts(hj3d_ctx* ctx, const void* counts_dev, uint32_t chu
              "count download");
   if (s == HJ3D_OK) s = hip_ok(ctx, hipStreamSynchronize(ctx->stream), "count download");
   if (s != HJ3D_OK) return s;
+  uint64_t total = 0;
   for (uint32_t p = 0; p < P; ++p)
     for (uint32_t k = 0; k < chunks; ++k) {  // back to [chunk][peer]
       if (send_host) send_host[size_t(k) * P + p] = h[size_t(p) * chunks + k];
       recv_host[size_t(k) * P + p] = h[n + size_t(p) * chunks + k];
+      total += uint64_t(h[n + size_t(p) * chunks + k]);
     }
+  if (recv_cap == ~0ull) return HJ3D_OK;
+  // every rank learns whether ANY rank's receive buffer is short, so all refuse together before
+  // the first pair collective (a one-sided refusal would leave the peers waiting in it)
+  int64_t* flag = tx;  // the transposed counts are downloaded already
+  const int64_t mine = total > recv_cap ? 1 : 0;
+  s = hip_ok(ctx, hipMemcpyAsync(flag, &mine, sizeof(mine), hipMemcpyHostToDevice, ctx->stream), "overflow flag");
+  if (s != HJ3D_OK) return s;
+  if ((s = nccl_ok(ctx, rccl()->allReduce(flag, flag, 1, ncclInt64, ncclMax, c->comm, ctx->stream),
+                   "overflow flag all-reduce")) != HJ3D_OK)
+    return s;
+  int64_t any = 0;
+  s = hip_ok(ctx, hipMemcpyAsync(&any, flag, sizeof(any), hipMemcpyDeviceToHost, ctx->stream), "overflow flag");
+  if (s == HJ3D_OK) s = hip_ok(ctx, hipStreamSynchronize(ctx->stream), "overflow flag");
+  if (s != HJ3D_OK) return s;
+  if (any)
+    return comm_fail(ctx, HJ3D_EOVERFLOW,
+                     mine ? "hj3d_comm_counts_cap: " + std::to_string(total) + " elements arrive at this rank, its "
+                                "receive buffer holds " + std::to_string(recv_cap)
+                          : std::string("hj3d_comm_counts_cap: another rank's receive buffer is short"));
   return HJ3D_OK;
 }
 
@@ -345,16 +371,21 @@ hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_
                         elem_bytes, s),
               "pair exchange");
   if (r != HJ3D_OK || !ticket) return r;
-  const uint32_t t = c->next_ticket++ % hj3d_comm_state::kTickets;
-  if ((r = hip_ok(ctx, hipEventRecord(c->done[t], s), "hipEventRecord")) != HJ3D_OK) return r;
+  const uint32_t t = c->next_ticket++;
+  if ((r = hip_ok(ctx, hipEventRecord(c->done[t % hj3d_comm_state::kTickets], s), "hipEventRecord")) != HJ3D_OK)
+    return r;
   *ticket = t;
   return HJ3D_OK;
 }
 
 hj3d_status hj3d_comm_wait(hj3d_ctx* ctx, uint32_t ticket) {
   hj3d_comm_state* c = st(ctx);
-  if (!c || ticket >= hj3d_comm_state::kTickets) return HJ3D_EINVAL;
-  return hip_ok(ctx, hipStreamWaitEvent(ctx->stream, c->done[ticket], 0), "hipStreamWaitEvent");
+  // a ticket never issued is refused; an older one whose slot a later exchange took waits for that
+  // later exchange instead: the exchanges run in issue order on the exchange stream, so the event
+  // in the slot is recorded after the ticket's own exchange (waits on it are never too early)
+  if (!c || ticket >= c->next_ticket) return HJ3D_EINVAL;
+  return hip_ok(ctx, hipStreamWaitEvent(ctx->stream, c->done[ticket % hj3d_comm_state::kTickets], 0),
+                "hipStreamWaitEvent");
 }
 
 hj3d_status hj3d_comm_allreduce_u64(hj3d_ctx* ctx, void* buf_dev, uint64_t n, int op) {

@@ -124,6 +124,7 @@ def lib():
         "hj3d_partition_sel": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, p]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe_geometry": (C.c_int, [C.c_void_p, u64, u64, C.POINTER(u32)]),
+        "hj3d_comm_counts_cap": (st, [p, p, u32, u64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "hj3d_key_bitmap": (st, [p, R, u64, p, p]),
         "hj3d_bitmap_or_popcount": (st, [p, p, u32, u64, p]),
         "hj3d_select": (st, [p, R, C.POINTER(_SelPred), u32, p, p]),
@@ -533,15 +534,19 @@ class Comm:
         ctx._check(lib().hj3d_comm_unique_id(ctx.h, buf), "hj3d_comm_unique_id")
         return buf.raw
 
-    def counts(self, counts):
+    def counts(self, counts, recv_cap: Optional[int] = None):
         """All-to-all of per-destination counts, int64 device tensor [C, world] (row c = the counts
-        hj3d_partition wrote for chunk c): host lists (send[c][p], recv[c][p]). Synchronous."""
+        hj3d_partition wrote for chunk c): host lists (send[c][p], recv[c][p]). Synchronous. With
+        recv_cap (elements this rank can receive over the chunks), every rank raises together when
+        any rank's total exceeds its capacity (hj3d_comm_counts_cap), before any pair exchange."""
         Cn, P = counts.shape
         if P != self.world or not counts.is_contiguous():
             raise ValueError("counts must be a contiguous [chunks, world] int64 tensor")
         snd = (C.c_int64 * (Cn * P))()
         rcv = (C.c_int64 * (Cn * P))()
-        self.ctx._check(lib().hj3d_comm_counts(self.ctx.h, counts.data_ptr(), Cn, snd, rcv), "hj3d_comm_counts")
+        cap = MASK64 if recv_cap is None else int(recv_cap)
+        self.ctx._check(lib().hj3d_comm_counts_cap(self.ctx.h, counts.data_ptr(), Cn, cap, snd, rcv),
+                        "hj3d_comm_counts_cap")
         return ([list(snd[c * P:(c + 1) * P]) for c in range(Cn)], [list(rcv[c * P:(c + 1) * P]) for c in range(Cn)])
 
     def exchange(self, send, sc, rc, recv_buf, asynchronous: bool = True):

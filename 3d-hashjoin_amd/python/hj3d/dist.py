@@ -98,14 +98,26 @@ def exchange(send_pairs: torch.Tensor, send_counts: torch.Tensor, recv_buf: torc
     return out
 
 
-def exchange_counts(send_counts: torch.Tensor, group=None):
+class ExchangeOverflow(RuntimeError):
+    """Raised on EVERY rank when any rank's receive capacity is below what arrives at it."""
+
+
+def exchange_counts(send_counts: torch.Tensor, group=None, recv_cap: int | None = None):
     """All-to-all of the per-destination counts of several partitioned chunks at once (one
     collective, one host synchronisation for a whole probe strand, instead of one per chunk).
 
     send_counts: int64 [C, P] (row c = hj3d_partition's counts of chunk c). Returns host lists
-    (send[c][p], recv[c][p]): recv[c][p] = pairs rank p sends this rank in chunk c."""
+    (send[c][p], recv[c][p]): recv[c][p] = pairs rank p sends this rank in chunk c.
+    recv_cap: this rank's receive capacity over the C chunks; the ranks agree (one max all-reduce)
+    whether any rank is short and then all raise ExchangeOverflow before any pair collective."""
     if _comm is not None:
-        return _comm.counts(send_counts.contiguous())
+        import hj3d
+        try:
+            return _comm.counts(send_counts.contiguous(), recv_cap)
+        except hj3d.Hj3dError as e:
+            if e.status == hj3d.HJ3D_EOVERFLOW:
+                raise ExchangeOverflow(str(e)) from e
+            raise
     world = dist.get_world_size(group)
     C = send_counts.shape[0]
     src = send_counts.t().contiguous()  # [P, C]: the block for destination p is contiguous
@@ -115,6 +127,14 @@ def exchange_counts(send_counts: torch.Tensor, group=None):
     dist.all_to_all_single(recv, src, group=group)
     sc = send_counts.cpu().tolist()
     rc = recv.view(world, C).t().cpu().tolist()
+    if recv_cap is not None:
+        total = sum(sum(r) for r in rc)
+        flag = torch.tensor([1 if total > recv_cap else 0], dtype=torch.int64,
+                            device=send_counts.device if not _host_staged(group) else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=group)
+        if int(flag.item()):
+            raise ExchangeOverflow(f"exchange: {total} pairs arrive at this rank, it holds {recv_cap}"
+                                   if total > recv_cap else "exchange: another rank's receive buffer is short")
     return sc, rc
 
 

@@ -416,7 +416,8 @@ def main():
             ctx.probe(table, pRel, unique=unique, unnest=unnest, out=out, fetch=False, checksum=state.get("ck", False))
         else:
             ctx.partition(bRel, nb, world, sendB, cntB[0])
-            scB, rcB = hdist.exchange_counts(cntB)
+            # with the receive capacity: every rank refuses together if any rank's buffer is short
+            scB, rcB = hdist.exchange_counts(cntB, recv_cap=recvB.shape[0])
             rB, work = hdist.exchange_pairs_async(sendB, scB[0], rcB[0], recvB)
             if work is not None:
                 work.wait()
@@ -429,7 +430,7 @@ def main():
             # accumulate into one probe strand
             for c in range(C):
                 ctx.partition(pRel_c[c], nb, world, sendP[sb[c]:sb[c + 1]], cntP[c])
-            scP, rcP = hdist.exchange_counts(cntP)
+            scP, rcP = hdist.exchange_counts(cntP, recv_cap=recvP.shape[0])
             pend, roff = [], 0
             for c in range(C):
                 rS, work = hdist.exchange_pairs_async(sendP[sb[c]:sb[c + 1]], scP[c], rcP[c], recvP[roff:])

@@ -270,16 +270,22 @@ hj3d_status hj3d_probe_geometry(hj3d_ctx* ctx, uint64_t nb_local, uint64_t n_bui
  *                        one row per chunk); send_host / recv_host = host i64 [chunks][world],
  *                        recv[c][p] = elements rank p sends this rank in chunk c (synchronous: the
  *                        one host synchronisation of an exchange strand; collective);
+ *   hj3d_comm_counts_cap the same, with this rank's receive capacity (elements it can take over
+ *                        the chunks): the ranks agree by an all-reduce whether any rank's total
+ *                        exceeds its capacity, and then EVERY rank returns HJ3D_EOVERFLOW, before
+ *                        any pair collective (recv_cap = UINT64_MAX: hj3d_comm_counts);
  *   hj3d_comm_exchange   grouped send / recv of one chunk: send_dev holds send_counts[p] elements of
  *                        elem_bytes for every peer p back to back (hj3d_partition's layout), recv_dev
  *                        receives recv_counts[p] elements from every peer in rank order. A receive
  *                        total above recv_cap returns HJ3D_EOVERFLOW BEFORE the collective: every
  *                        rank knows its totals from hj3d_comm_counts, so size recv_dev from them
- *                        (a rank that skips the call leaves its peers waiting). ticket == NULL:
+ *                        (a rank that skips the call leaves its peers waiting; hj3d_comm_counts_cap
+ *                        makes that refusal collective). ticket == NULL:
  *                        enqueued on the context stream. ticket != NULL: enqueued on the context's
  *                        exchange stream after the work already on the context stream, so probes of
  *                        earlier chunks overlap it; hj3d_comm_wait(ticket) orders the context stream
- *                        after it (tickets recycle after 64 exchanges). Collective;
+ *                        after it (tickets count up; a ticket older than the 64 latest waits for a
+ *                        later exchange of the same stream, never too early). Collective;
  *   hj3d_comm_allreduce_u64 / hj3d_comm_allgather  merge the per-rank result slots and statistics
  *                        (u64 counters add, extremes max / min; xor via all-gather), on the context
  *                        stream. Collective. */
@@ -291,6 +297,8 @@ hj3d_status hj3d_comm_destroy(hj3d_ctx* ctx);
 hj3d_status hj3d_comm_rank(const hj3d_ctx* ctx, int* rank, int* world);
 hj3d_status hj3d_comm_counts(hj3d_ctx* ctx, const void* counts_dev, uint32_t chunks, int64_t* send_host,
                              int64_t* recv_host);
+hj3d_status hj3d_comm_counts_cap(hj3d_ctx* ctx, const void* counts_dev, uint32_t chunks, uint64_t recv_cap,
+                                 int64_t* send_host, int64_t* recv_host);
 hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_t* send_counts, void* recv_dev,
                                const int64_t* recv_counts, uint64_t recv_cap, uint32_t elem_bytes,
                                uint32_t* ticket);

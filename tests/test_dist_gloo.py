@@ -169,3 +169,46 @@ def test_bucket_range_exchange_world2(case):
         for k in ("nb", "empty", "entries", "distinct", "cc0_sum", "cc0_cnt", "cc1_sum", "cc1_cnt", "cc0_max",
                   "cc1_max", "cc1_min"):
             assert red[k] == st[k], (plan, k, red[k], st[k])
+
+
+def _short_worker(rank, port, q):
+    import torch
+    import torch.distributed as dist
+    from hj3d import dist as hdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        # every rank sends 10 pairs to each peer; rank 1's receive buffer holds only 15
+        counts = torch.full((2, WORLD), 5, dtype=torch.int64)
+        cap = 15 if rank == 1 else 20
+        outcome = "ok"
+        try:
+            hdist.exchange_counts(counts, recv_cap=cap)
+        except hdist.ExchangeOverflow as e:
+            outcome = "short" if "arrive at this rank" in str(e) else "peer short"
+        # the process group is still usable: a full-size exchange afterwards goes through
+        sc, rc = hdist.exchange_counts(counts, recv_cap=20)
+        q.put((rank, outcome, sum(map(sum, rc))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exchange_refusal_is_collective():
+    """ADVICE / VERDICT r2: a short receive buffer on ONE rank makes EVERY rank refuse the exchange
+    before any pair collective (exchange_counts with recv_cap: the ranks agree by one all-reduce),
+    instead of the short rank refusing alone and its peers waiting in the pair all-to-all."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_short_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = {r: (o, n) for r, o, n in (q.get(timeout=120) for _ in range(WORLD))}
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert res == {0: ("peer short", 20), 1: ("short", 20)}

@@ -175,6 +175,36 @@ def test_rccl_exchange_short_buffer_is_refused(ctx, comm):
     assert v.shape[0] == 99
 
 
+def test_rccl_counts_cap_refuses_before_the_exchange(ctx, comm):
+    """hj3d_comm_counts_cap: with a receive capacity below the exchanged total the count exchange
+    itself returns HJ3D_EOVERFLOW on every rank (agreed by an all-reduce), before any pair
+    collective; tickets count up and an old ticket still orders the stream after its exchange."""
+    import torch
+    import hj3d
+    from hj3d import dist as hdist
+    counts = torch.tensor([[40], [60]], dtype=torch.int64, device="cuda")
+    hdist.use_comm(comm)
+    try:
+        with pytest.raises(hdist.ExchangeOverflow):
+            hdist.exchange_counts(counts, recv_cap=99)
+        sc, rc = hdist.exchange_counts(counts, recv_cap=100)
+        assert rc == [[40], [60]]
+    finally:
+        hdist.use_comm(None)
+    send = torch.arange(200, dtype=torch.int32, device="cuda").view(100, 2)
+    recv = torch.empty((100, 2), dtype=torch.int32, device="cuda")
+    tickets = []
+    for _ in range(70):  # more exchanges than ticket slots
+        _, t = comm.exchange(send, [100], [100], recv, asynchronous=True)
+        tickets.append(t)
+    assert tickets == list(range(tickets[0], tickets[0] + 70))
+    comm.wait(tickets[0])  # its slot was reused: waits for a later exchange of the same stream
+    ctx.sync()
+    assert torch.equal(recv, send)
+    with pytest.raises(hj3d.Hj3dError):
+        comm.wait(tickets[-1] + 1)  # never issued
+
+
 @pytest.mark.parametrize("plan", ["Csr", "Nsr", "Nrs"])
 def test_bench_dist_path_on_rccl_equals_reference(plan, tmp_path):
     """bench.py's multi-GPU strand with the exchange on libhj3d's RCCL communicator (--dist-path,
