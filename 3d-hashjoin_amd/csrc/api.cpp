@@ -157,6 +157,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       if (value < 0 || value == 1 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_SLICE: 0 or >= 2");
       ctx->pk_slice_max = uint32_t(value);
       return HJ3D_OK;
+    case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);
@@ -292,9 +293,14 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   hipError_t e;
   if (t->desc.kind == HJ3D_CHAIN) {
     bool sorted = false;
-    e = (!ctx->force_direct && build->n >= (ctx->radix_min >> 4) && build->n > 0 && t->nb_local >= 64)
+    e = (!ctx->force_direct && !ctx->pk_build && build->n >= (ctx->radix_min >> 4) && build->n > 0 &&
+         t->nb_local >= 64)
             ? radix_build(ctx, t, *build, ctx->stream, &sorted)
             : hipErrorNotSupported;
+    if (e == hipErrorNotSupported && build->n >= (ctx->radix_min >> 4)) {
+      e = pk_build(ctx, t, *build, ctx->stream);  // tables beyond the radix build's 2048 x 16384 buckets
+      sorted = e == hipSuccess;
+    }
     if (e == hipErrorNotSupported) e = chain_build(ctx, t, *build, ctx->stream);
     if (e == hipSuccess && !sorted) e = sort_small_buckets(ctx, t, ctx->stream);
   } else {

@@ -863,6 +863,170 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   if (threadIdx.x < kCtlWords) __hip_atomic_store(ctl + threadIdx.x, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- the chaining build of tables beyond the radix build's range (config D: 1e8 buckets) ----
+// R is partitioned like a probe side: k_pk_part into coarse ranges, k_pk_split into slices of
+// kPbW buckets (S2 fine regions per slice). k_pk_slice_sums totals each slice's regions (then an
+// exclusive scan gives its CSR base ps[p]); k_pk_build, one persistent 1024-thread workgroup per
+// CU, builds slice after slice as k_rp_build3 does (radix.hip): the slice's pairs gathered into
+// registers (the next slice's loads in flight while the current one is built), counted per bucket
+// with LDS atomics (each pair keeps its arrival rank), bucket starts by an LDS scan, the pairs
+// staged in bucket order, then each written to its row rank inside its bucket (the reference's
+// chain order is arithmetic in row order: buckets of <= 32 entries sorted by row). Larger slices
+// (skewed keys) go through HBM in the same kernel. Region overflows are not built here: the host
+// checks the overflow count and falls back to the direct build (chain.hip).
+constexpr uint32_t kPbW = 8192;       // buckets per build slice (bucket << 16 | rank packing: < 2^16)
+constexpr int kPbPer = 11;            // pairs per lane in registers: fine regions of <= 704 pairs
+constexpr uint32_t kPbStage = 12288;  // LDS stage of a slice's pairs
+static_assert(kPbPer * kPkBlock <= int(kPbStage), "a register-held slice fits the stage");
+
+__global__ __launch_bounds__(256) void k_pk_slice_sums(const uint32_t* __restrict__ cnt2, uint32_t S2, uint32_t P,
+                                                       uint32_t* __restrict__ tot) {
+  const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= P) return;
+  uint32_t t = 0;
+  for (uint32_t s = 0; s < S2; ++s) t += cnt2[uint64_t(s) * P + p];
+  tot[p] = t;
+}
+
+// exclusive scan of n <= kPbW + 1 LDS words by one 1024-thread workgroup
+__device__ __forceinline__ void pb_lds_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
+  constexpr int kPer = (kPbW + kPkBlock) / kPkBlock;  // 9 words per thread
+  const uint32_t t0 = threadIdx.x * kPer;
+  uint32_t v[kPer], loc = 0;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    v[k] = t0 + k < n ? a[t0 + k] : 0u;
+    loc += v[k];
+  }
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t wt;
+  const uint32_t pre = wave_excl_scan(loc, &wt);
+  if (lane == 0) wsum[wid] = wt;
+  __syncthreads();
+  uint32_t base = 0;
+  for (int w = 0; w < wid; ++w) base += wsum[w];
+  uint32_t run = base + pre;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    if (t0 + k < n) a[t0 + k] = run;
+    run += v[k];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(kPkBlock) void k_pk_build(const uint2* __restrict__ fine, const uint32_t* __restrict__ cnt2,
+                                                       uint32_t S2, uint32_t cap2, const uint32_t* __restrict__ ps,
+                                                       PkGeom pk, uint32_t* __restrict__ off, uint2* __restrict__ ent) {
+  __shared__ uint32_t cnt[kPbW + 1];
+  __shared__ uint2 stage[kPbStage];
+  __shared__ uint32_t wsum[kPkBlock / kWave];
+  constexpr uint32_t kCap = kPbPer * kPkBlock;
+  const uint32_t P = pk.P, nbl = pk.nbl, W = pk.W;
+  // pair i of slice p: fine[i + delta] with the delta of the last region starting at or before i
+  auto gather = [&](uint32_t p, uint32_t i) __attribute__((always_inline)) {
+    uint32_t run = 0;
+    int64_t d = int64_t(uint64_t(p) * cap2);
+    for (uint32_t sg = 0; sg < S2; ++sg) {
+      if (i >= run) d = int64_t((uint64_t(sg) * P + p) * cap2) - int64_t(run);
+      run += cnt2[uint64_t(sg) * P + p];
+    }
+    return fine[int64_t(i) + d];
+  };
+  // fast form: wave w holds fine region (w, p) (<= kPbPer * 64 pairs; S2 <= 16 regions per slice)
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  auto fits = [&](uint32_t p) __attribute__((always_inline)) {
+    bool ok = true;
+    for (uint32_t sg = 0; sg < S2; ++sg) ok = ok && cnt2[uint64_t(sg) * P + p] <= uint32_t(kPbPer) * 64u;
+    return ok;
+  };
+  uint2 ea[kPbPer], eb[kPbPer];
+  auto load = [&](uint2 (&e)[kPbPer], uint32_t p) __attribute__((always_inline)) {
+    if (p >= P || !fits(p)) return;
+    const uint32_t c = uint32_t(wid) < S2 ? cnt2[uint64_t(wid) * P + p] : 0u;
+    const uint2* src = fine + (uint64_t(wid) * P + p) * cap2;
+#pragma unroll
+    for (int u = 0; u < kPbPer; ++u) {
+      const uint32_t i = uint32_t(u) * 64u + lane;
+      e[u] = i < c ? src[i] : make_uint2(0, 0);
+    }
+  };
+  auto build = [&](uint2 (&e)[kPbPer], uint32_t p) __attribute__((always_inline)) {
+    const uint32_t b0 = p * W;
+    const uint32_t nbs = min(W, nbl - b0);
+    const uint32_t s0 = ps[p], m = ps[p + 1] - s0;
+    for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) cnt[k] = 0;
+    __syncthreads();
+    if (!fits(p) || m > kCap) {  // skewed slice: scatter through HBM, sort the small buckets there
+      for (uint32_t i = threadIdx.x; i < m; i += kPkBlock) atomicAdd(&cnt[gather(p, i).x >> pk.qbits], 1u);
+      __syncthreads();
+      pb_lds_scan(cnt, nbs, wsum);
+      for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) off[b0 + k] = s0 + cnt[k];
+      if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s0 + m;
+      __syncthreads();
+      for (uint32_t i = threadIdx.x; i < m; i += kPkBlock) {
+        const uint2 x = gather(p, i);
+        ent[s0 + atomicAdd(&cnt[x.x >> pk.qbits], 1u)] = make_uint2(pk.hash_of(x.x, p), x.y);
+      }
+      __syncthreads();
+      for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) {
+        const uint32_t bs = k ? cnt[k - 1] : 0u, n = cnt[k] - bs;
+        if (n < 2 || n > kSortedMaxPk) continue;
+        uint2* E = ent + s0 + bs;
+        for (uint32_t q = 1; q < n; ++q) {
+          const uint2 x = E[q];
+          uint32_t j = q;
+          while (j > 0 && E[j - 1].y > x.y) {
+            E[j] = E[j - 1];
+            --j;
+          }
+          E[j] = x;
+        }
+      }
+      __syncthreads();
+      return;
+    }
+    uint32_t rk[kPbPer];  // bucket << 16 | arrival rank
+    const uint32_t c = uint32_t(wid) < S2 ? cnt2[uint64_t(wid) * P + p] : 0u;
+#pragma unroll
+    for (int u = 0; u < kPbPer; ++u) {
+      const bool v = uint32_t(u) * 64u + lane < c;
+      const uint32_t b = v ? e[u].x >> pk.qbits : 0u;
+      rk[u] = v ? (b << 16) | atomicAdd(&cnt[b], 1u) : kInvalid;
+    }
+    __syncthreads();
+    pb_lds_scan(cnt, nbs, wsum);
+    if (threadIdx.x == 0) cnt[nbs] = m;
+    for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) off[b0 + k] = s0 + cnt[k];
+    if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s0 + m;
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kPbPer; ++u)
+      if (rk[u] != kInvalid) stage[cnt[rk[u] >> 16] + (rk[u] & 0xFFFFu)] = e[u];
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < m; q += kPkBlock) {
+      const uint2 x = stage[q];
+      const uint32_t b = x.x >> pk.qbits;
+      const uint32_t bs = cnt[b], n = cnt[b + 1] - bs;
+      uint32_t pos = q;
+      if (n >= 2 && n <= kSortedMaxPk) {
+        uint32_t rr = 0;
+        for (uint32_t k = bs; k < bs + n; ++k) rr += stage[k].y < x.y;
+        pos = bs + rr;
+      }
+      ent[s0 + pos] = make_uint2(pk.hash_of(x.x, p), x.y);
+    }
+    __syncthreads();
+  };
+  load(ea, blockIdx.x);
+  for (uint32_t p = blockIdx.x; p < P; p += 2 * gridDim.x) {
+    load(eb, p + gridDim.x);
+    build(ea, p);
+    if (p + gridDim.x >= P) break;
+    load(ea, p + 2 * gridDim.x);
+    build(eb, p + gridDim.x);
+  }
+}
+
 }  // namespace
 
 // Pairs per lane and chunk for the region walk: the K in [kItemsMin, kItemsMax] with the fewest
@@ -1055,6 +1219,92 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
 #undef HJ3D_PK_LAUNCH
   }
   return hipGetLastError();
+}
+
+
+hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+  hipError_t e;
+  const uint32_t nbl = t->nb_local, nb = uint32_t(t->desc.num_buckets);
+  if (ctx->force_direct || nbl < 64 || r.n == 0 || r.n >= (1ull << 31)) return hipErrorNotSupported;
+  const uint32_t W = kPbW, P = (nbl + W - 1) / W;
+  const uint32_t C = (P + kPkBlock - 1) / kPkBlock;
+  if ((C < 2 && !ctx->pk_build) || C > kSpMaxC) return hipErrorNotSupported;  // one level: the radix build's range
+  const uint32_t W1 = W * C, P1 = (nbl + W1 - 1) / W1;
+  auto bits = [](uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; };
+  const uint32_t qbits = bits(0xFFFFFFFFull / nb);
+  if (qbits + bits(W1 - 1) > 32) return hipErrorNotSupported;
+  const uint32_t ntiles = uint32_t((r.n + kPkTile - 1) / kPkTile);
+  const uint32_t G = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
+  auto capacity = [](double ex) {
+    uint64_t c = uint64_t(ex + 8.0 * std::sqrt(ex) + 32.0);
+    return (c + kPkSeg - 1) / kPkSeg * kPkSeg;
+  };
+  const uint64_t per_g = uint64_t((ntiles + G - 1) / G) * kPkTile;
+  const uint64_t cap = capacity(double(per_g < r.n ? per_g : r.n) / P1);
+  const uint64_t nreg = uint64_t(G) * P1;
+  const uint32_t S2 = G < 16u ? G : 16u;
+  const uint64_t cap2 = capacity(double(r.n) / (double(S2) * P));
+  const uint64_t nreg2 = uint64_t(S2) * P;
+  if (nreg * cap >= (1ull << 31) || nreg2 * cap2 >= (1ull << 31)) return hipErrorNotSupported;
+  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->ent.ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPHist].ensure(nreg * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPk2].ensure(nreg2 * cap2 * sizeof(uint2))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPk2Cnt].ensure(nreg2 * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
+  auto geom = [&](uint32_t w, uint32_t p) {
+    PkGeom g;
+    g.dnb = FastDiv32::make(nb);
+    g.dw = FastDiv32::make(w);
+    g.nb = nb;
+    g.lo = uint32_t(t->desc.bucket_lo);
+    g.nbl = nbl;
+    g.W = w;
+    g.P = p;
+    g.qbits = qbits;
+    g.qmask = qbits >= 32 ? 0xFFFFFFFFu : ((1u << qbits) - 1);
+    return g;
+  };
+  const PkGeom pk1 = geom(W1, P1), pk = geom(W, P);
+  uint2* region = ctx->scratch[kScrPairs].as<uint2>();
+  uint32_t* counts = ctx->scratch[kScrPHist].as<uint32_t>();
+  uint2* ovf = ctx->scratch[kScrSortV].as<uint2>();
+  uint2* fine = ctx->scratch[kScrPk2].as<uint2>();
+  uint32_t* fcnt = ctx->scratch[kScrPk2Cnt].as<uint32_t>();
+  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
+  uint64_t* ctl = ctx->ctl.as<uint64_t>();
+  const RelView v = view_of(r);
+  SelRange sr{};
+  if (r.row_off == HJ3D_ROW_IMPLICIT)
+    hipLaunchKernelGGL((k_pk_part<true, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
+                       counts, ovf, ctl, sr, kPkStage);
+  else
+    hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
+                       counts, ovf, ctl, sr, kPkStage);
+  // (C = 1, forced: the split only regroups each slice's G regions into S2)
+  hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kPkBlock), 0, s, static_cast<const uint2*>(region),
+                     static_cast<const uint32_t*>(counts), G, P1, uint32_t(cap), S2, pk, C, bits(C - 1), uint32_t(cap2),
+                     fine, fcnt, ovf, ctl);
+  hipLaunchKernelGGL(k_pk_slice_sums, dim3((P + 255) / 256), dim3(256), 0, s, static_cast<const uint32_t*>(fcnt), S2, P, ps);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = exclusive_scan_u32(ctx, ps, ps, P, s)) != hipSuccess) return e;
+  const uint32_t g2 = P < uint32_t(ctx->num_cus) ? P : uint32_t(ctx->num_cus);
+  hipLaunchKernelGGL(k_pk_build, dim3(g2), dim3(kPkBlock), 0, s, static_cast<const uint2*>(fine),
+                     static_cast<const uint32_t*>(fcnt), S2, uint32_t(cap2), static_cast<const uint32_t*>(ps), pk,
+                     t->off.as<uint32_t>(), t->ent.as<uint2>());
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  // pairs past a region's capacity (skewed keys) are not in the slices: then the direct build
+  // runs instead. The control words go back to zero (the probes' invariant) either way.
+  uint64_t novf = 0;
+  if ((e = hipMemcpyAsync(&novf, ctl + kCtlNovf, sizeof(novf), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(ctl, 0, kCtlWords * sizeof(uint64_t), s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  if (novf) return hipErrorNotSupported;
+  t->n_build = r.n;
+  return hipSuccess;
 }
 
 }  // namespace hj3d

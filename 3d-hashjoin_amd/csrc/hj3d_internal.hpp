@@ -83,6 +83,7 @@ struct hj3d_ctx {
   bool pk_off = false;            // HJ3D_OPT_PACKED_PROBE = 0: the unique chaining probe on (hash, row) pairs
   uint32_t pk_slice_max = 0;      // HJ3D_OPT_PK_SLICE: cap on the packed probe's slice width (0 = LDS-sized)
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
+  bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
@@ -272,6 +273,11 @@ struct PkPlan {
   uint32_t W = 0, P = 0, C = 1, W1 = 0, P1 = 0;
 };
 PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nb_local, uint64_t n_build);
+// The chaining build of tables beyond the radix build's range (> 2048 x 16384 buckets): R
+// partitioned by the packed partitioner's two levels into 8192-bucket slices, each built in LDS
+// (rows sorted inside buckets of <= 32). Synchronous (checks for region overflow);
+// hipErrorNotSupported when not applicable or on overflow (use chain_build).
+hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 // chain.hip
 hipError_t chain_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,

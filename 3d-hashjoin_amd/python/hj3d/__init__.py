@@ -27,7 +27,7 @@ PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
 OPT_PROBE_ITEMS = 7
-OPT_PK_SLICE, OPT_PK_STAGE = 8, 9
+OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD = 8, 9, 10
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -374,6 +374,10 @@ class Context:
         out = (C.c_uint32 * 5)()
         self._check(lib().hj3d_probe_geometry(self.h, nb_local, n_build, out), "hj3d_probe_geometry")
         return dict(zip(("W", "P", "C", "W1", "P1"), list(out)))
+
+    def pk_build(self, on: bool = True):
+        """Test hook: chaining builds take the two-level slice build (pk_build) whenever it applies."""
+        self.set_option(OPT_PK_BUILD, int(on))
 
     def sel_unfused(self, on: bool = True):
         """A/B switch: hj3d_probe_sel selects first instead of fusing into the partitioner."""

@@ -172,7 +172,12 @@ enum {
   /* HJ3D_OPT_PK_STAGE (pairs, default 0 = the whole LDS stage): the packed partitioner writes its
    * carried partial segments out early once the carries plus a tile exceed this many pairs
    * (tests: 1 flushes after every tile). */
-  HJ3D_OPT_PK_STAGE = 9
+  HJ3D_OPT_PK_STAGE = 9,
+  /* HJ3D_OPT_PK_BUILD (0/1, default 0): chaining builds take the slice build of tables beyond the
+   * radix build's range (R through the packed partitioner's two levels into 8192-bucket slices,
+   * each built in LDS; synchronous, region overflow falls back to the direct build) whenever it
+   * applies, not only above 2048 x 16384 buckets (tests). */
+  HJ3D_OPT_PK_BUILD = 10
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

@@ -52,6 +52,7 @@ def pk(ctx):
     yield ctx
     ctx.pk_slice_max(0)
     ctx.pk_stage(0)
+    ctx.pk_build(False)
     ctx.radix_min(1 << 20)
 
 
@@ -140,3 +141,61 @@ def test_pk_plan_geometry(ctx):
         # the slice image at fill n_build / nbl: W directory words + 2 words per entry (+ 6 sigma)
         fill = n_build / nbl
         assert pl["W"] * (1 + 2 * fill) + 12 * (pl["W"] * fill) ** 0.5 <= 39552, (nbl, pl)
+
+
+STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
+             "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
+
+
+@pytest.mark.parametrize("name", ["exp1_R1048576_S8388608_uni", "exp1_R131072_S1048576_zipf1",
+                                  "exp1_R65537_S1000000_zipf08"])
+def test_slice_build_equals_reference(pk, name):
+    """The two-level slice build (pk_build, the chaining build of tables beyond 2048 x 16384
+    buckets, i.e. config D's 1e8) forced on fixture tables: statistics and the counters and output
+    checksums of Csr / CsrUU / Crs equal the reference binary's. Crs builds on the skewed S.a: hot
+    keys overflow the partition regions there and the direct build takes over."""
+    import hj3d
+    pk.pk_build(True)
+    try:
+        g, R, S, b = rel_of(name)
+        dR, dS = dev(R), dev(S)
+        for plan in ("Csr", "CsrUU", "Crs"):
+            nb = hj3d.num_buckets_exp1(plan, len(R), g["numDvSa"], b)
+            got = hj3d.exp1_plan(pk, plan, dR, dS, nb)
+            ref = g["plans"][plan]
+            for k in ("c_build", "c_probe", "c_cmp", "c_top"):
+                assert got[k] == ref[k], (name, plan, k, got[k], ref[k])
+            assert {k: got["stats"][k] for k in STAT_KEYS} == {k: ref["stats"][k] for k in STAT_KEYS}, (name, plan)
+            assert got["out"] == ref["out"], (name, plan)
+    finally:
+        pk.pk_build(False)
+
+
+@pytest.mark.parametrize("fill", [1.0, 1.3])
+def test_slice_build_large_slices_vs_oracle(pk, fill):
+    """Slices whose fine regions exceed the register-held form (more than 704 pairs, frequent at
+    fill 1.3 with 8192-bucket slices) take the in-kernel HBM path of k_pk_build; random non-unique
+    keys; statistics and both probe forms equal the oracle's."""
+    import hj3d
+    rng = np.random.default_rng(int(fill * 10))
+    nb = 1 << 20
+    n = int(nb * fill)
+    Bk = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    Bk[rng.random(n) < 0.05] = 12345  # one key with ~5 % of the rows (a long bucket, arrival order)
+    Pk = np.concatenate([Bk[rng.integers(0, n, 600_000)], rng.integers(0, 1 << 32, 200_000, dtype=np.uint64).astype(np.uint32)])
+    B = O.tuples3(Bk, np.zeros(n, np.uint32))
+    Pt = O.tuples3(np.arange(len(Pk), dtype=np.uint32), Pk)
+    pk.pk_build(True)
+    try:
+        t = hj3d.Table(pk, hj3d.HJ3D_CHAIN, nb)
+        t.build(hj3d.Rel(dev(B), 0))
+        st = t.stats()
+        for unique in (True, False):
+            e = O.chain_plan(B, 0, Pt, 1, nb, unique)
+            r = pk.probe(t, hj3d.Rel(dev(Pt), 1), unique=unique)
+            assert (r.n_out, r.n_cmps) == (e.c_probe, e.c_cmp), unique
+            assert {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_c": 0, "sum_h": r.sum_h,
+                    "xor_h": r.xor_h} == e.out, unique
+        assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
+    finally:
+        pk.pk_build(False)
