@@ -309,10 +309,17 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
 // rank by slice with a wave-level multi-split (one ballot per bit of c, one LDS atomic per slice and
 // wave), stage the tile slice-major in LDS, write each slice's run out with consecutive lanes on
 // consecutive pairs. Pairs past a fine region's capacity go to the overflow list as {h, row}.
+#ifndef HJ3D_SP_BLOCK
+#define HJ3D_SP_BLOCK 256  // k_pk_split workgroup size (several per CU; 1024: 4.21 ms, 512: 3.50, 256: 3.39 at config D)
+#endif
+#ifndef HJ3D_SP_PREFETCH
+#define HJ3D_SP_PREFETCH 1  // k_pk_split: the next tile's pairs loaded while this one is split (A/B)
+#endif
+constexpr int kSpBlock = HJ3D_SP_BLOCK;
 constexpr int kSpRounds = 8;
-constexpr int kSpTile = kPkBlock * kSpRounds;
+constexpr int kSpTile = kSpBlock * kSpRounds;
 constexpr uint32_t kSpMaxC = 64;
-__global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__ reg1,
+__global__ __launch_bounds__(kSpBlock) void k_pk_split(const uint2* __restrict__ reg1,
                                                        const uint32_t* __restrict__ cnt1, uint32_t G1, uint32_t P1,
                                                        uint32_t cap1, uint32_t S2, PkGeom pk, uint32_t C,
                                                        uint32_t cbits, uint32_t cap2, uint2* __restrict__ reg2,
@@ -355,7 +362,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__
   auto load = [&](uint2 (&v)[kSpRounds], uint32_t t0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < kSpRounds; ++j) {
-      const uint32_t f = t0 + uint32_t(j) * kPkBlock + me;
+      const uint32_t f = t0 + uint32_t(j) * kSpBlock + me;
       v[j] = make_uint2(0, 0);
       if (f < total) {
         while (f >= nst) {
@@ -368,15 +375,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__
     }
   };
   uint2 cv[kSpRounds];
-  load(cv, 0);
+  if (HJ3D_SP_PREFETCH) load(cv, 0);
   uint32_t par = 0;
   for (uint32_t t0 = 0; t0 < total; t0 += kSpTile, par ^= 1u) {
     uint2 nv[kSpRounds];
-    load(nv, t0 + kSpTile);
+    load(HJ3D_SP_PREFETCH ? nv : cv, HJ3D_SP_PREFETCH ? t0 + kSpTile : t0);
     uint32_t cc[kSpRounds], rk[kSpRounds];
 #pragma unroll
     for (int j = 0; j < kSpRounds; ++j) {
-      const bool valid = t0 + uint32_t(j) * kPkBlock + me < total;
+      const bool valid = t0 + uint32_t(j) * kSpBlock + me < total;
       const uint32_t bic = cv[j].x >> pk.qbits;  // bucket inside the coarse range
       const uint32_t c = valid ? pk.dw.div(bic) : 0u;
       cv[j].x = ((bic - c * pk.W) << pk.qbits) | (cv[j].x & pk.qmask);
@@ -421,7 +428,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__
     }
     __syncthreads();
     const uint32_t tn = min(uint32_t(kSpTile), total - t0);
-    for (uint32_t k = me; k < tn; k += kPkBlock) {
+    for (uint32_t k = me; k < tn; k += kSpBlock) {
       const uint32_t c = cof[k];
       const uint2 dl = dlim[c];
       const uint2 e = stage[k];
@@ -430,8 +437,10 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_split(const uint2* __restrict__
       if (fit) reg2[d] = e;
       pk_ovf_append(!fit, make_uint2(pk.hash_of(e.x, pbase + c), e.y), ovf, ctl);
     }
+    if constexpr (HJ3D_SP_PREFETCH) {
 #pragma unroll
-    for (int j = 0; j < kSpRounds; ++j) cv[j] = nv[j];
+      for (int j = 0; j < kSpRounds; ++j) cv[j] = nv[j];
+    }
   }
   __syncthreads();
   if (me < C && pbase + me < pk.P) cnt2[uint64_t(s) * pk.P + pbase + me] = min(cur[me], cap2);
@@ -1179,7 +1188,7 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
     uint2* fine = ctx->scratch[kScrPk2].as<uint2>();
     uint32_t* fcnt = ctx->scratch[kScrPk2Cnt].as<uint32_t>();
     KernelSpan ts(ctx, HJ3D_T_HIST);
-    ts.launch(k_pk_split, dim3(pl.P1 * S2), dim3(kPkBlock), s, static_cast<const uint2*>(region),
+    ts.launch(k_pk_split, dim3(pl.P1 * S2), dim3(kSpBlock), s, static_cast<const uint2*>(region),
               static_cast<const uint32_t*>(counts), G, pl.P1, uint32_t(cap), S2, pk, pl.C, bits(pl.C - 1),
               uint32_t(cap2), fine, fcnt, ovf, ctl);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -1285,7 +1294,7 @@ hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t
     hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
                        counts, ovf, ctl, sr, kPkStage);
   // (C = 1, forced: the split only regroups each slice's G regions into S2)
-  hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kPkBlock), 0, s, static_cast<const uint2*>(region),
+  hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kSpBlock), 0, s, static_cast<const uint2*>(region),
                      static_cast<const uint32_t*>(counts), G, P1, uint32_t(cap), S2, pk, C, bits(C - 1), uint32_t(cap2),
                      fine, fcnt, ovf, ctl);
   hipLaunchKernelGGL(k_pk_slice_sums, dim3((P + 255) / 256), dim3(256), 0, s, static_cast<const uint32_t*>(fcnt), S2, P, ps);
