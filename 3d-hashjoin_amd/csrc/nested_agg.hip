@@ -25,42 +25,44 @@
 namespace hj3d {
 namespace {
 
-constexpr int kAggBlock = 1024;
 constexpr uint32_t kAggW = 6144;     // max buckets per partition (one LDS table round at fill <= ~1.3)
-// LDS hash table slots, prime: with double hashing every probe step visits all slots (double
-// hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6)
-constexpr uint32_t kAggCap = 10223;
-constexpr uint32_t kAggSlotsPer = (kAggCap + 1023) / 1024;  // slots per thread in the per-slot loops
-// new keys are admitted while fewer than this many are in the table: at most kAggBlock inserts
+// LDS hash table slots (prime, sized per build: ~1.6 slots per bucket of the partition + the insert
+// slack below; at most 10223): with double hashing every probe step visits all slots (double
+// hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6). The table
+// lives in dynamic LDS, so small partitions (config E) run two 512-thread workgroups per CU.
+constexpr uint32_t kAggCapMax = 10223;
+// new keys are admitted while fewer than cap - BLOCK - 64 are in the table: at most BLOCK inserts
 // race past the test, so the table never fills and every probe sequence ends
-constexpr uint32_t kAggLimit = kAggCap - kAggBlock - 64;
 constexpr uint32_t kAggRounds = 1;  // initial rounds per partition (2, 3: slower under Zipf, pairs re-read)
 constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
 constexpr int kAggU = 8;             // pairs per thread and step (the next step's in flight)
-constexpr int kWavesA = kAggBlock / kWave;
+#ifndef HJ3D_NAGG_SMALL
+#define HJ3D_NAGG_SMALL 1  // small partitions: two 512-thread workgroups per CU with a smaller table (0: A/B)
+#endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
 
-__device__ __forceinline__ uint32_t slot_of(uint32_t h) { return __umulhi(h * 0x9E3779B1u, kAggCap); }
-// per-key probe step in [1, kAggCap) (double hashing: no primary clusters, so the longest probe
+__device__ __forceinline__ uint32_t slot_of(uint32_t h, uint32_t cap) { return __umulhi(h * 0x9E3779B1u, cap); }
+// per-key probe step in [1, cap) (double hashing: no primary clusters, so the longest probe
 // sequence among a wave's 64 lanes, which the whole wave waits for, stays short)
-__device__ __forceinline__ uint32_t step_of(uint32_t h) { return 1u + __umulhi(h * 0x85EBCA6Bu, kAggCap - 1); }
-__device__ __forceinline__ uint32_t next_slot(uint32_t s, uint32_t st) {
+__device__ __forceinline__ uint32_t step_of(uint32_t h, uint32_t cap) { return 1u + __umulhi(h * 0x85EBCA6Bu, cap - 1); }
+__device__ __forceinline__ uint32_t next_slot(uint32_t s, uint32_t st, uint32_t cap) {
   s += st;
-  return s >= kAggCap ? s - kAggCap : s;
+  return s >= cap ? s - cap : s;
 }
 
 // Slot of key h, inserting it if absent (returns kInvalid when the table is at its limit: the
 // caller flags the round as overflowing).
-__device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t* nkeys) {
-  uint32_t s = slot_of(h);
-  const uint32_t st = step_of(h);
+__device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t* nkeys,
+                                               uint32_t cap, uint32_t limit) {
+  uint32_t s = slot_of(h, cap);
+  const uint32_t st = step_of(h, cap);
   for (;;) {
     const uint32_t k = tkey[s];
     if (k == h) return s;
     if (k == empty) {
-      if (*nkeys >= kAggLimit) return kInvalid;
+      if (*nkeys >= limit) return kInvalid;
       const uint32_t old = atomicCAS(&tkey[s], empty, h);
       if (old == empty) {
         atomicAdd(nkeys, 1u);
@@ -68,23 +70,24 @@ __device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint3
       }
       if (old == h) return s;
     }
-    s = next_slot(s, st);
+    s = next_slot(s, st, cap);
   }
 }
 
-// kAggU pairs per thread of the partition's pairs from i0 (coalesced: pair i0 + u * block + tid)
+// kAggU pairs per thread of the partition's pairs from i0 (coalesced: pair i0 + u * BLOCK + tid)
+template <int BLOCK>
 __device__ __forceinline__ void load_batch(const uint2* __restrict__ pairs, uint32_t i0, uint32_t e1, uint2 (&v)[kAggU]) {
 #pragma unroll
   for (int u = 0; u < kAggU; ++u) {
-    const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+    const uint32_t i = i0 + u * BLOCK + threadIdx.x;
     v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
   }
 }
 
-__device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h) {
-  uint32_t s = slot_of(h);
-  const uint32_t st = step_of(h);
-  while (tkey[s] != h) s = next_slot(s, st);
+__device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h, uint32_t cap) {
+  uint32_t s = slot_of(h, cap);
+  const uint32_t st = step_of(h, cap);
+  while (tkey[s] != h) s = next_slot(s, st, cap);
   return s;
 }
 
@@ -94,10 +97,12 @@ __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
   return v;
 }
 
-// Exclusive scan of a[0..n) in LDS by kAggBlock threads (contiguous chunks per thread); returns
+// Exclusive scan of a[0..n) in LDS by BLOCK threads (contiguous chunks per thread); returns
 // the total. All threads must call it.
+template <int BLOCK>
 __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
-  const uint32_t per = (n + kAggBlock - 1) / kAggBlock;
+  constexpr int kWavesA = BLOCK / kWave;
+  const uint32_t per = (n + BLOCK - 1) / BLOCK;
   const uint32_t b = threadIdx.x * per, e = min(n, b + per);
   uint32_t t = 0;
   for (uint32_t i = b; i < e; ++i) t += a[i];
@@ -126,18 +131,28 @@ __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
 // One workgroup per partition p (local buckets [b0, b0 + nbs), pairs [ps[p], ps[p+1])).
 // Writes: off[b0 + k] = partition-local main offset of bucket k; mtmp[ps[p] + i] the partition's
 // main records in bucket order (i < its key count, with sub_off global); sub rows; dcount[p].
-__global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                    FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
-                                                    uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
-                                                    uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
-                                                    unsigned long long* __restrict__ maxlen,
-                                                    uint32_t* __restrict__ fail, const uint32_t* __restrict__ order) {
-  __shared__ uint32_t tkey[kAggCap];
-  __shared__ uint32_t tcnt[kAggCap];  // count, then the sub cursor
-  __shared__ uint32_t tmin[kAggCap];  // min row, then (after the main records are written) unused
-  __shared__ uint32_t bcnt[kAggW];    // keys per bucket of the round, then their main offsets
-  __shared__ uint32_t wsum[kWavesA];
-  __shared__ uint32_t nkeys, ovf;
+// Dynamic LDS (agg_lds_bytes): tkey | tcnt | tmin [cap each] | bcnt [W] | wsum | nkeys, ovf.
+// SLOTS >= cap / BLOCK: table slots per thread in the per-slot loops.
+__host__ __device__ constexpr uint32_t agg_lds_words(uint32_t cap, uint32_t W, int block) {
+  return 3 * cap + W + uint32_t(block / 64) + 2;
+}
+template <int BLOCK, int SLOTS>
+__global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
+                                                uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
+                                                uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
+                                                unsigned long long* __restrict__ maxlen,
+                                                uint32_t* __restrict__ fail, const uint32_t* __restrict__ order,
+                                                uint32_t cap) {
+  extern __shared__ uint32_t agg_lds[];
+  uint32_t* tkey = agg_lds;
+  uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
+  uint32_t* tmin = tcnt + cap;   // min row, then (after the main records are written) unused
+  uint32_t* bcnt = tmin + cap;   // keys per bucket of the round, then their main offsets
+  uint32_t* wsum = bcnt + W;
+  uint32_t& nkeys = wsum[BLOCK / kWave];
+  uint32_t& ovf = wsum[BLOCK / kWave + 1];
+  const uint32_t limit = cap - BLOCK - 64;
   const uint32_t p = order[blockIdx.x];
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
   const uint32_t e0 = ps[p], e1 = ps[p + 1];
@@ -149,12 +164,12 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     const uint32_t c1 = min(nbs, c0 + span);
     // a hash that no key of this round has: its bucket lies outside [b0 + c0, b0 + c1)
     const uint32_t empty = uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
-    for (uint32_t s = threadIdx.x; s < kAggCap; s += kAggBlock) {
+    for (uint32_t s = threadIdx.x; s < cap; s += BLOCK) {
       tkey[s] = empty;
       tcnt[s] = 0;
       tmin[s] = kInvalid;
     }
-    for (uint32_t k = threadIdx.x; k < c1 - c0; k += kAggBlock) bcnt[k] = 0;
+    for (uint32_t k = threadIdx.x; k < c1 - c0; k += BLOCK) bcnt[k] = 0;
     if (threadIdx.x == 0) {
       nkeys = 0;
       ovf = 0;
@@ -162,19 +177,19 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     __syncthreads();
     // ---- pass A: count and min row per key ----
     uint2 v[kAggU], nv[kAggU];
-    load_batch(pairs, e0, e1, v);
-    for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
-      if (i0 + kAggBlock * kAggU < e1) load_batch(pairs, i0 + kAggBlock * kAggU, e1, nv);  // next batch in flight
+    load_batch<BLOCK>(pairs, e0, e1, v);
+    for (uint32_t i0 = e0; i0 < e1; i0 += BLOCK * kAggU) {
+      if (i0 + BLOCK * kAggU < e1) load_batch<BLOCK>(pairs, i0 + BLOCK * kAggU, e1, nv);  // next batch in flight
       // home slots of all items read together (one LDS latency for the batch); only items whose
       // key is not in its home slot walk the probe sequence
       bool act[kAggU];
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        const uint32_t i = i0 + u * BLOCK + threadIdx.x;
         const uint32_t lb = fm.mod(v[u].x) - lo - b0;
         act[u] = i < e1 && lb >= c0 && lb < c1;
-        k0[u] = tkey[act[u] ? slot_of(v[u].x) : 0u];
+        k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
@@ -187,7 +202,7 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
           if (__popcll(same) > 1) {
             const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
             if (lane == leader) {
-              const uint32_t s = tab_insert(tkey, hl, empty, &nkeys);
+              const uint32_t s = tab_insert(tkey, hl, empty, &nkeys, cap, limit);
               if (s == kInvalid) {
                 ovf = 1;
               } else {
@@ -199,7 +214,7 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
           }
         }
         if (act[u]) {
-          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x) : tab_insert(tkey, v[u].x, empty, &nkeys);
+          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_insert(tkey, v[u].x, empty, &nkeys, cap, limit);
           if (s == kInvalid) {
             ovf = 1;
           } else {
@@ -223,27 +238,27 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
     }
     // ---- main slots: rank of every key inside its bucket (registers), bucket offsets ----
     // (empty slots: tkey = empty, tcnt = 0, tmin = kInvalid)
-    uint32_t rank[kAggSlotsPer];
+    uint32_t rank[SLOTS];
 #pragma unroll
-    for (int j = 0; j < int(kAggSlotsPer); ++j) {
-      const uint32_t s = j * kAggBlock + threadIdx.x;
-      rank[j] = s < kAggCap && tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * BLOCK + threadIdx.x;
+      rank[j] = s < cap && tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
     }
     __syncthreads();
-    const uint32_t nk = block_scan_lds(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
+    const uint32_t nk = block_scan_lds<BLOCK>(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
     // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
-    uint32_t cnt[kAggSlotsPer];
+    uint32_t cnt[SLOTS];
 #pragma unroll
-    for (int j = 0; j < int(kAggSlotsPer); ++j) {
-      const uint32_t s = j * kAggBlock + threadIdx.x;
-      cnt[j] = s < kAggCap ? tcnt[s] : 0u;
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * BLOCK + threadIdx.x;
+      cnt[j] = s < cap ? tcnt[s] : 0u;
     }
     __syncthreads();
-    const uint32_t nrows = block_scan_lds(tcnt, kAggCap, wsum);
+    const uint32_t nrows = block_scan_lds<BLOCK>(tcnt, cap, wsum);
     // main records (partition-local slots, global sub offsets) and the round's directory words
 #pragma unroll
-    for (int j = 0; j < int(kAggSlotsPer); ++j) {
-      const uint32_t s = j * kAggBlock + threadIdx.x;
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * BLOCK + threadIdx.x;
       if (cnt[j]) {
         const uint32_t h = tkey[s];
         const uint32_t m = mrun + bcnt[fm.mod(h) - lo - b0 - c0] + rank[j];
@@ -253,20 +268,20 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
         mxlen = max(mxlen, cnt[j]);
       }
     }
-    for (uint32_t k = threadIdx.x; k < c1 - c0; k += kAggBlock) off[b0 + c0 + k] = mrun + bcnt[k];
+    for (uint32_t k = threadIdx.x; k < c1 - c0; k += BLOCK) off[b0 + c0 + k] = mrun + bcnt[k];
     __syncthreads();
     // ---- pass B: rows into their keys' sub ranges ----
-    load_batch(pairs, e0, e1, v);
-    for (uint32_t i0 = e0; i0 < e1; i0 += kAggBlock * kAggU) {
-      if (i0 + kAggBlock * kAggU < e1) load_batch(pairs, i0 + kAggBlock * kAggU, e1, nv);  // next batch in flight
+    load_batch<BLOCK>(pairs, e0, e1, v);
+    for (uint32_t i0 = e0; i0 < e1; i0 += BLOCK * kAggU) {
+      if (i0 + BLOCK * kAggU < e1) load_batch<BLOCK>(pairs, i0 + BLOCK * kAggU, e1, nv);  // next batch in flight
       bool act[kAggU];
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * kAggBlock + threadIdx.x;
+        const uint32_t i = i0 + u * BLOCK + threadIdx.x;
         const uint32_t lb = fm.mod(v[u].x) - lo - b0;
         act[u] = i < e1 && lb >= c0 && lb < c1;
-        k0[u] = tkey[act[u] ? slot_of(v[u].x) : 0u];
+        k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
@@ -278,14 +293,14 @@ __global__ __launch_bounds__(kAggBlock) void k_nagg(const uint2* __restrict__ pa
           const uint64_t same = __ballot(mine);
           if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive sub slots
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl)], uint32_t(__popcll(same)));
+            if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl, cap)], uint32_t(__popcll(same)));
             base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
             if (mine) sub[base + uint32_t(__popcll(same & lt))] = v[u].y;
             act[u] = act[u] && !mine;
           }
         }
         if (act[u]) {
-          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x) : tab_find(tkey, v[u].x);
+          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find(tkey, v[u].x, cap);
           sub[atomicAdd(&tcnt[s], 1u)] = v[u].y;
         }
       }
@@ -414,9 +429,40 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
   uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
   hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
-  hipLaunchKernelGGL(k_nagg, dim3(P), dim3(kAggBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
-                     uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
-                     reinterpret_cast<unsigned long long*>(counts + 2), fail, order);
+  // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
+  // insert slack; a partition with more keys retries its range in halves. Two 512-thread
+  // workgroups per CU when the LDS fits twice (config E), else one 1024-thread one.
+  auto prime_at_least = [](uint32_t x) {
+    for (;; ++x) {
+      bool pr = x > 1;
+      for (uint32_t d = 2; d * d <= x && pr; ++d) pr = x % d != 0;
+      if (pr) return x;
+    }
+  };
+  static bool lds_attr = false;  // dynamic LDS above 64 KB
+  if (!lds_attr) {
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nagg<512, 12>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
+      return e;
+    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nagg<1024, 10>),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
+      return e;
+    lds_attr = true;
+  }
+  const uint32_t want = uint32_t(1.5 * W) + 512 + 64;  // the 512-thread form's insert slack
+  const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
+  if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, 512) * 4 <= 81920) {
+    const size_t lds = agg_lds_words(cap512, W, 512) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_nagg<512, 12>), dim3(P), dim3(512), lds, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
+                       uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
+                       reinterpret_cast<unsigned long long*>(counts + 2), fail, order, cap512);
+  } else {
+    const uint32_t cap = kAggCapMax;
+    const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_nagg<1024, 10>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo),
+                       nbl, uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
+                       reinterpret_cast<unsigned long long*>(counts + 2), fail, order, cap);
+  }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // and the caller, which reads the counts once after the build, runs the sort build instead
   if ((e = exclusive_scan_u32(ctx, dcount, dcount, P, s)) != hipSuccess) return e;
