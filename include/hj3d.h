@@ -218,7 +218,12 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
  * (chaining) or main records (nested), *n_sub = build rows of a nested table (0 for chaining).
  * Then off[nb_local + 1] receives the CSR offsets of the local buckets into the payload, payload
  * the chaining entries {u32 hash, u32 row} or the nested main records {u32 hash, first_row,
- * sub_off, sub_len}, and sub (nested) the build rows grouped per key, sub[sub_off .. + sub_len). */
+ * sub_off, sub_len}, and sub (nested) the build rows grouped per key, sub[sub_off .. + sub_len).
+ * Entry order: chaining buckets of <= 32 entries come sorted by row (the reference's chain order is
+ * then [first, newest, ..., second], arithmetic in that order); longer buckets are in no defined
+ * order (the builds claim their runs with atomics) -- a consumer that needs the reference's chain
+ * order there sorts by row, as the drop-in host view does. Nested: mains and sub rows in no defined
+ * order (the reference's order follows from first_row and the rows). */
 hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
                               uint64_t* n_payload, uint64_t* n_sub);
 /* Synchronous statistics (makeStatistics). */
