@@ -38,6 +38,12 @@ constexpr int kPkBlock = 1024;
 #ifndef HJ3D_PK_FLAT
 #define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (1; measured slower at config B) or only short ones
 #endif
+#ifndef HJ3D_PK_NTREG
+#define HJ3D_PK_NTREG 1   // partition: region segments stored non-temporal (0: plain; nt 0.452 -> 0.447 ms, and the probe reading them 0.493 -> 0.489)
+#endif
+#ifndef HJ3D_PK_NTLOAD
+#define HJ3D_PK_NTLOAD 1  // partition: probe keys loaded non-temporal (0: plain; nt 0.447 -> 0.436 ms, probe phase -2 %)
+#endif
 #ifndef HJ3D_PK_DIAG
 #define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups
 #endif
@@ -128,7 +134,10 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       for (int j = 0; j < kPkRounds; ++j) {
         const uint32_t i = base + uint32_t(j) * kPkBlock + me;
         const char* t = r.base + uint64_t(i) * r.stride;
-        h[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + r.key_off) : 0u;
+        if (HJ3D_PK_NTLOAD)
+          h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
+        else
+          h[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + r.key_off) : 0u;
         if constexpr (SEL) pw[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + sel.word_off) : 0u;
       }
     } else {
@@ -259,7 +268,12 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       const uint32_t j = kk % kPkSeg;
       const uint2 e = stage[si.y + j];
       const bool spill = si.x & kOvfFlag;
-      if (!spill && HJ3D_PK_DIAG != 1) region[si.x + j] = e;
+      if (!spill && HJ3D_PK_DIAG != 1) {
+        if (HJ3D_PK_NTREG)
+          __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(region + si.x + j));
+        else
+          region[si.x + j] = e;
+      }
       to_ovf(e, si.x & ~kOvfFlag, spill);
     }
     // the run's tail (< one segment) becomes the slice's carry

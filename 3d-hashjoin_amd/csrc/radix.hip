@@ -33,6 +33,33 @@ constexpr int kPRoundsR = 8;                     // k_rp_part1r: 8192-tuple tile
 #define HJ3D_PROBE_WFRAC 0.8
 #endif
 constexpr int kPSeg = HJ3D_PSEG;                 // k_rp_part1r: 128-B region segments
+#ifndef HJ3D_NT_BUILD
+#define HJ3D_NT_BUILD 0  // build kernels: loads / stores non-temporal (A/B; measured worse: R is read twice, the
+                         // pairs re-read by the build, the table by the probe, all from the Infinity Cache)
+#endif
+template <typename T>
+__device__ __forceinline__ T nt_ld(const T* p) {
+  if constexpr (HJ3D_NT_BUILD) {
+    if constexpr (sizeof(T) == 8) {
+      const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+      T t;
+      __builtin_memcpy(&t, &v, 8);
+      return t;
+    } else {
+      return __builtin_nontemporal_load(p);
+    }
+  }
+  return *p;
+}
+__device__ __forceinline__ void nt_st(uint2* p, uint2 e) {
+  if constexpr (HJ3D_NT_BUILD) __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(p));
+  else *p = e;
+}
+__device__ __forceinline__ void nt_st(uint32_t* p, uint32_t v) {
+  if constexpr (HJ3D_NT_BUILD) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+__device__ __forceinline__ uint32_t key_ld(const RelView& r, uint64_t i) { return HJ3D_NT_BUILD ? r.key_nt(i) : r.key(i); }
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
@@ -70,7 +97,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    key[j] = i < r.n ? r.key(i) : 0u;
+    key[j] = i < r.n ? key_ld(r, i) : 0u;
   }
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t bl[kPRounds];
@@ -83,7 +110,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j) {
       const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      key[j] = i < r.n ? r.key(i) : 0u;
+      key[j] = i < r.n ? key_ld(r, i) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j)
@@ -120,7 +147,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    h[j] = i < r.n ? r.key(i) : 0u;
+    h[j] = i < r.n ? key_ld(r, i) : 0u;
   }
   // this workgroup's write cursor per partition: partition start + its run's offset (k_rp_hist)
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = cur[p];
@@ -164,12 +191,12 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j) {
       const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      h[j] = i < r.n ? r.key(i) : 0u;
+      h[j] = i < r.n ? key_ld(r, i) : 0u;
     }
     for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
       const uint2 e = stage[k];
       const uint32_t p = fw.div(fm.mod(e.x) - lo);
-      out[gb[p] + (k - loc[p])] = e;
+      nt_st(out + gb[p] + (k - loc[p]), e);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < P; p += kPBlock)  // advance the cursors by the tile's runs
@@ -266,7 +293,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
       const uint32_t i = s0 + u * kJBlock + threadIdx.x;
-      e[u] = i < s1 ? pairs[i] : make_uint2(0, 0);
+      e[u] = i < s1 ? nt_ld(pairs + i) : make_uint2(0, 0);
     }
   };
   auto build = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
@@ -314,7 +341,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
     __syncthreads();
     lds_excl_scan(cnt, nbs, wsum);
     if (threadIdx.x == 0) cnt[nbs] = m;
-    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) nt_st(off + b0 + k, s0 + cnt[k]);
     if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
     __syncthreads();
 #pragma unroll
@@ -331,7 +358,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
         for (uint32_t k = bs; k < bs + n; ++k) r += stage[k].y < x.y;
         pos = bs + r;
       }
-      ent[s0 + pos] = x;
+      nt_st(ent + s0 + pos, x);
     }
     __syncthreads();
   };
