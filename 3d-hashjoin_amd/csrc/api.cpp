@@ -556,6 +556,18 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
   return from_hip(ctx, partition(ctx, *rel, nb, parts, out_pairs, counts, ctx->stream, &a), "hj3d_partition_sel");
 }
 
+hj3d_status hj3d_partition_strided(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
+                                   uint64_t nb, uint32_t parts, void* out_pairs, uint64_t stride, void* counts) {
+  if (!ctx || !rel_ok(rel) || !counts || (rel->n && !out_pairs)) return HJ3D_EINVAL;
+  if (stride < rel->n) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: stride below rel->n");
+  if (parts == 0 || parts > 256) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: nparts outside [1, 256]");
+  if (npred && !sel_ok(rel, preds, npred)) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: invalid predicate");
+  PhaseTimer tm(ctx, HJ3D_T_PARTITION);
+  const SelArgs a = npred ? sel_args(preds, npred) : SelArgs{};
+  return from_hip(ctx, partition_strided(ctx, *rel, nb, parts, out_pairs, stride, counts, ctx->stream, &a),
+                  "hj3d_partition_strided");
+}
+
 hj3d_status hj3d_key_bitmap(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t domain, void* bitmap, void* outside) {
   if (!ctx || !rel_ok(rel) || domain == 0 || domain > (1ull << 32) || !bitmap) return HJ3D_EINVAL;
   return from_hip(ctx, key_bitmap(ctx, *rel, domain, bitmap, outside, ctx->stream), "hj3d_key_bitmap");

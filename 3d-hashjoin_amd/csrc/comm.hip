@@ -193,8 +193,9 @@ hj3d_comm_state* st(hj3d_ctx* ctx) { return ctx ? ctx->comm : nullptr; }
 // of elem bytes, displacements = prefix sums of the counts. Blocks move as 8- or 4-byte words
 // when their size allows, in pieces of at most 2^27 words (matched in order per peer), so no
 // RCCL count approaches 2^31 (a 2.5e8-pair chunk is 2e9 bytes).
+// send_stride (elements): peer p's elements start at send + p * send_stride (0: back to back)
 ncclResult_t alltoallv(hj3d_comm_state* c, const char* send, const int64_t* sc, char* recv, const int64_t* rc,
-                       size_t elem, hipStream_t s) {
+                       size_t elem, hipStream_t s, uint64_t send_stride = 0) {
   Rccl* r = rccl();
   const size_t word = elem % 8 == 0 ? 8 : elem % 4 == 0 ? 4 : 1;
   const ncclDataType_t dt = word == 8 ? ncclUint64 : word == 4 ? ncclUint32 : ncclUint8;
@@ -204,6 +205,7 @@ ncclResult_t alltoallv(hj3d_comm_state* c, const char* send, const int64_t* sc, 
   size_t so = 0, ro = 0;
   for (int p = 0; p < c->world && e == ncclSuccess; ++p) {
     const size_t ns = size_t(sc[p]) * elem / word, nr = size_t(rc[p]) * elem / word;
+    if (send_stride) so = size_t(p) * send_stride * elem;
     for (size_t k = 0; k < ns && e == ncclSuccess; k += kPiece)
       e = r->send(send + so + k * word, ns - k < kPiece ? ns - k : kPiece, dt, p, c->comm, s);
     for (size_t k = 0; k < nr && e == ncclSuccess; k += kPiece)
@@ -346,11 +348,20 @@ hj3d_status hj3d_comm_counts_cap(hj3d_ctx* ctx, const void* counts_dev, uint32_t
 hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_t* send_counts, void* recv_dev,
                                const int64_t* recv_counts, uint64_t recv_cap, uint32_t elem_bytes,
                                uint32_t* ticket) {
+  return hj3d_comm_exchange_strided(ctx, send_dev, 0, send_counts, recv_dev, recv_counts, recv_cap, elem_bytes, ticket);
+}
+
+hj3d_status hj3d_comm_exchange_strided(hj3d_ctx* ctx, const void* send_dev, uint64_t send_stride,
+                                       const int64_t* send_counts, void* recv_dev, const int64_t* recv_counts,
+                                       uint64_t recv_cap, uint32_t elem_bytes, uint32_t* ticket) {
   hj3d_comm_state* c = st(ctx);
   if (!c || !send_counts || !recv_counts || !elem_bytes) return HJ3D_EINVAL;
   uint64_t ns = 0, nr = 0;
   for (int p = 0; p < c->world; ++p) {
-    if (send_counts[p] < 0 || recv_counts[p] < 0) return HJ3D_EINVAL;
+    // a count above the stride is an argument error every rank can see coming only for its own
+    // sends: hj3d_partition_strided never writes one (stride >= its relation's size)
+    if (send_counts[p] < 0 || recv_counts[p] < 0 || (send_stride && uint64_t(send_counts[p]) > send_stride))
+      return HJ3D_EINVAL;
     ns += uint64_t(send_counts[p]);
     nr += uint64_t(recv_counts[p]);
   }
@@ -368,7 +379,7 @@ hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_
   }
   r = nccl_ok(ctx,
               alltoallv(c, static_cast<const char*>(send_dev), send_counts, static_cast<char*>(recv_dev), recv_counts,
-                        elem_bytes, s),
+                        elem_bytes, s, send_stride),
               "pair exchange");
   if (r != HJ3D_OK || !ticket) return r;
   const uint32_t t = c->next_ticket++;

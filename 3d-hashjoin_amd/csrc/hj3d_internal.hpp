@@ -305,6 +305,10 @@ hipError_t table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out, hipS
 // part.hip
 hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t nparts, void* out_pairs,
                      void* counts, hipStream_t s, const SelArgs* sel = nullptr);
+// single pass, no order kept inside a destination: destination p's pairs at out_pairs + p * stride
+// (stride >= r.n), counts (u64) zeroed here and then filled by the run claims
+hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t parts, void* out_pairs,
+                             uint64_t stride, void* counts, hipStream_t s, const SelArgs* sel = nullptr);
 hipError_t select_pairs(hj3d_ctx* ctx, const hj3d_rel& rel, const hj3d_sel_pred* preds, uint32_t npred, void* out,
                         void* count, hipStream_t s);
 hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s);

@@ -84,6 +84,154 @@ __global__ void k_part_counts(const uint32_t* __restrict__ offs, uint32_t ntiles
   if (p < parts) counts[p] = uint64_t(offs[uint64_t(p + 1) * ntiles]) - offs[uint64_t(p) * ntiles];
 }
 
+// ---- single-pass exchange partitioner (the probe side: order inside a destination not kept) ----
+// The probe's counters are per tuple, so its pairs need no stable order, and the two passes above
+// (histogram, then scatter: the relation read twice) become one. Destination p's pairs go to
+// out[p * stride ...]: a persistent workgroup (one per CU) takes 8192-tuple tiles; per tile it ranks
+// the tuples by destination (wave multi-split: one ballot per destination bit, one LDS atomic per
+// destination and wave), claims each destination's run with one device atomic on counts[p] (the
+// run's place in p's area), stages the tile destination-major in LDS and writes the runs out with
+// consecutive lanes on consecutive pairs. The next tile's keys load while this one is written.
+// Per tuple: the tuple read once (12 B at the headline layout) + one 8-B pair written.
+#ifndef HJ3D_XP_ROUNDS
+#define HJ3D_XP_ROUNDS 8  // tuples per thread and tile (8: 8192-tuple tiles)
+#endif
+#ifndef HJ3D_XP_NT
+#define HJ3D_XP_NT 1  // pairs stored non-temporal (0: plain; A/B)
+#endif
+constexpr int kXpBlock = 1024;
+constexpr int kXpRounds = HJ3D_XP_ROUNDS;
+constexpr int kXpTile = kXpBlock * kXpRounds;  // rank inside the tile: < 2^16
+constexpr int kXpMaxParts = 256;
+
+template <bool SEL, bool IMPLICIT>
+__global__ __launch_bounds__(kXpBlock) void k_xpart(RelView r, FastMod fm, uint64_t nb, uint32_t parts, uint32_t pbits,
+                                                    uint32_t magic, uint64_t ntiles, uint64_t stride,
+                                                    uint2* __restrict__ out, unsigned long long* __restrict__ counts,
+                                                    uint2* __restrict__ sink, SelArgs sel) {
+  __shared__ uint2 stage[kXpTile];
+  __shared__ uint8_t sown[kXpTile];
+  __shared__ uint32_t loc[kXpMaxParts], sbase[kXpMaxParts], bnd[kXpMaxParts + 1];
+  __shared__ unsigned long long gbase[kXpMaxParts];
+  __shared__ uint32_t ntot;
+  const uint32_t me = threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  // bnd[p] = first bucket of destination p (hj3d_part_range): owner(b) = max p with bnd[p] <= b
+  for (uint32_t p = me; p <= parts; p += kXpBlock)
+    bnd[p] = p == parts ? uint32_t(nb) : uint32_t((uint64_t(p) * nb + parts - 1) / parts);
+  for (uint32_t p = me; p < kXpMaxParts; p += kXpBlock) loc[p] = 0;
+  __syncthreads();
+  // Memory ordering: vmcnt counts loads and stores together, in issue order. The per-tile memory
+  // instruction counts are therefore fixed (clamped loads; kXpRounds stores, a lane without a pair
+  // storing to its own sink slot), so the wait for the next tile's keys leaves this tile's stores in
+  // flight (a store behind a branch would make the compiler wait for every older store).
+  uint32_t h[kXpRounds], rw[IMPLICIT ? 1 : kXpRounds];
+  const auto tile_len = [&](uint64_t tile) __attribute__((always_inline)) {
+    const uint64_t base = tile * kXpTile;
+    return base >= r.n ? 0u : uint32_t(r.n - base < kXpTile ? r.n - base : kXpTile);
+  };
+  // a wave-uniform 64-bit tile pointer + 32-bit lane offsets; past the end: the tile's (or the
+  // relation's) last tuple again, unconditionally
+  auto load = [&](uint64_t tile) __attribute__((always_inline)) {
+    const uint64_t t = tile < ntiles ? tile : ntiles - 1;
+    const uint32_t lim = tile_len(t) - 1;
+    const char* tp = r.base + t * kXpTile * r.stride;
+#pragma unroll
+    for (int j = 0; j < kXpRounds; ++j) {
+      const uint32_t o = min(uint32_t(j) * kXpBlock + me, lim) * r.stride;
+      h[j] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(tp + o + r.key_off));
+      if constexpr (!IMPLICIT) rw[j] = __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(tp + o + r.row_off));
+    }
+  };
+  // the loop starts one (empty) tile early, so the first tile's keys are loaded by the same code
+  // as every later tile's: the waits at the loop head then see one issue order only
+  for (int64_t tile = int64_t(blockIdx.x) - int64_t(gridDim.x); tile < int64_t(ntiles); tile += gridDim.x) {
+    const uint64_t base = tile < 0 ? 0 : uint64_t(tile) * kXpTile;
+    const uint32_t len = tile < 0 ? 0u : tile_len(uint64_t(tile));
+    uint32_t rk[kXpRounds];  // destination << 16 | rank inside the tile's run, or kInvalid
+#pragma unroll
+    for (int j = 0; j < kXpRounds; ++j) {
+      const uint32_t li = uint32_t(j) * kXpBlock + me;
+      bool valid = li < len;
+      if constexpr (SEL) valid = valid && sel_eval(r, sel, base + li);
+      uint32_t d = 0;
+      if (valid) {
+        const uint32_t b = fm.mod(murmur32(h[j]));
+        d = __umulhi(b, magic);  // <= owner(b), at most one or two below it
+        while (d + 1 < parts && b >= bnd[d + 1]) ++d;
+      }
+      uint64_t peer = __ballot(valid);
+      for (uint32_t bit = 0; bit < pbits; ++bit) {
+        const bool set = (d >> bit) & 1u;
+        const uint64_t bb = __ballot(set);
+        peer &= set ? bb : ~bb;
+      }
+      const uint32_t wr = uint32_t(__popcll(peer & lt));
+      uint32_t bs = 0;
+      if (valid && wr == 0) bs = atomicAdd(&loc[d], uint32_t(__popcll(peer)));
+      bs = uint32_t(__shfl(int(bs), valid ? __ffsll((unsigned long long)peer) - 1 : lane, kWave));
+      rk[j] = valid ? (d << 16) | (bs + wr) : kInvalid;
+    }
+    __syncthreads();
+    constexpr int kPer = kXpMaxParts / kWave;  // wave 0: destinations lane, lane + 64, ...
+    unsigned long long g[kPer];
+    if (wid == 0) {  // run starts in the stage, and each run's place in its destination's area
+      uint32_t c[kPer];
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t p = uint32_t(lane) + k * kWave;
+        c[k] = p < parts ? loc[p] : 0u;
+        if (p < parts) loc[p] = 0;
+      }
+#pragma unroll
+      for (int k = 0; k < kPer; ++k)  // the claims issued together; their values are needed last
+        g[k] = c[k] ? atomicAdd(counts + lane + k * kWave, (unsigned long long)c[k]) : 0ull;
+      // stage order: destination-major, p = lane + k * 64 -> (k, lane) scan order is p order
+      uint32_t run = 0;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        uint32_t wt;
+        const uint32_t pre = wave_excl_scan(c[k], &wt);
+        const uint32_t p = uint32_t(lane) + k * kWave;
+        if (p < parts) sbase[p] = run + pre;
+        run += wt;
+      }
+      if (lane == 0) ntot = run;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kXpRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint32_t d = rk[j] >> 16, s = sbase[d] + (rk[j] & 0xFFFFu);
+      stage[s] = make_uint2(h[j], IMPLICIT ? uint32_t(r.row_base + base) + uint32_t(j) * kXpBlock + me : rw[j]);
+      sown[s] = uint8_t(d);
+    }
+    load(uint64_t(tile + gridDim.x));  // the next tile's keys in flight while this one is written
+    if (wid == 0) {
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) {
+        const uint32_t p = uint32_t(lane) + k * kWave;
+        if (p < parts) gbase[p] = g[k];
+      }
+    }
+    __syncthreads();
+    const uint32_t nt = ntot;
+#pragma unroll
+    for (int it = 0; it < kXpRounds; ++it) {
+      const uint32_t kk = uint32_t(it) * kXpBlock + me;
+      const uint32_t d = sown[kk];
+      const uint64_t pos = gbase[d] + (kk - sbase[d]);
+      const uint2 e = stage[kk];
+      uint2* dst = kk < nt && pos < stride ? out + d * stride + pos : sink + me;
+      if (HJ3D_XP_NT)
+        __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(dst));
+      else
+        *dst = e;
+    }
+  }
+}
+
 // Bijective permutation of [0, n): 4-round Feistel network on the smallest even-bit domain
 // >= n, with cycle walking back into [0, n).
 struct Feistel {
@@ -310,6 +458,36 @@ hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t par
                      hist, static_cast<uint2*>(out_pairs), sa);
   hipLaunchKernelGGL(k_part_counts, dim3(1), dim3(kMaxParts), 0, s, hist, uint32_t(ntiles), parts,
                      static_cast<uint64_t*>(counts));
+  return hipGetLastError();
+}
+
+hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t parts, void* out_pairs,
+                             uint64_t stride, void* counts, hipStream_t s, const SelArgs* sel) {
+  if (parts == 0 || parts > kXpMaxParts || nb == 0 || nb >= (1ull << 32) || stride < r.n) return hipErrorInvalidValue;
+  hipError_t e;
+  if ((e = hipMemsetAsync(counts, 0, parts * sizeof(uint64_t), s)) != hipSuccess) return e;
+  if (r.n == 0) return hipSuccess;
+  const uint64_t ntiles = (r.n + kXpTile - 1) / kXpTile;
+  const uint64_t want = uint64_t(ctx->num_cus);  // one 1024-thread workgroup per CU
+  const unsigned grid = unsigned(ntiles < want ? ntiles : want);
+  uint32_t pbits = 0;
+  while ((1u << pbits) < parts) ++pbits;
+  const uint64_t m = (uint64_t(parts) << 32) / nb;  // owner(b) >= mulhi(b, m) >= owner(b) - 2
+  const uint32_t magic = m > 0xFFFFFFFFull ? 0xFFFFFFFFu : uint32_t(m);
+  const FastMod fm = FastMod::make(uint32_t(nb));
+  const RelView v = view_of(r);
+  auto* cnt = static_cast<unsigned long long*>(counts);
+  auto* out = static_cast<uint2*>(out_pairs);
+  const bool implicit = v.row_off == 0xFFFFFFFFu;
+  if ((e = ctx->scratch[kScrD].ensure(kXpBlock * sizeof(uint2))) != hipSuccess) return e;
+  uint2* sink = ctx->scratch[kScrD].as<uint2>();  // garbage stores of lanes without a pair
+  const SelArgs sa = sel ? *sel : SelArgs{};
+  if (sa.npred)
+    hipLaunchKernelGGL((implicit ? k_xpart<true, true> : k_xpart<true, false>), dim3(grid), dim3(kXpBlock), 0, s, v, fm,
+                       nb, parts, pbits, magic, ntiles, stride, out, cnt, sink, sa);
+  else
+    hipLaunchKernelGGL((implicit ? k_xpart<false, true> : k_xpart<false, false>), dim3(grid), dim3(kXpBlock), 0, s, v,
+                       fm, nb, parts, pbits, magic, ntiles, stride, out, cnt, sink, sa);
   return hipGetLastError();
 }
 

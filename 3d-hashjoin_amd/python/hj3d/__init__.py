@@ -122,6 +122,7 @@ def lib():
         "hj3d_probe2_result": (st, [p, C.POINTER(_Probe2Res)]),
         "hj3d_partition": (st, [p, R, u64, u32, p, p]),
         "hj3d_partition_sel": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, p]),
+        "hj3d_partition_strided": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, u64, p]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe_geometry": (C.c_int, [C.c_void_p, u64, u64, C.POINTER(u32)]),
         "hj3d_comm_counts_cap": (st, [p, p, u32, u64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -144,6 +145,8 @@ def lib():
         "hj3d_comm_counts": (st, [p, p, u32, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "hj3d_comm_exchange": (st, [p, p, C.POINTER(C.c_int64), p, C.POINTER(C.c_int64), u64, u32,
                                     C.POINTER(u32)]),
+        "hj3d_comm_exchange_strided": (st, [p, p, u64, C.POINTER(C.c_int64), p, C.POINTER(C.c_int64), u64, u32,
+                                            C.POINTER(u32)]),
         "hj3d_comm_wait": (st, [p, u32]),
         "hj3d_comm_allreduce_u64": (st, [p, p, u64, i32]),
         "hj3d_comm_allgather": (st, [p, p, p, u64]),
@@ -384,9 +387,20 @@ class Context:
         self.set_option(OPT_SEL_UNFUSED, int(on))
 
     # ---- exchange / synthetic data ----
-    def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts, preds=None):
+    def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts, preds=None, stride=None):
         """Bucket-range partition of rel into (key, row) pairs per destination (stable); with
-        preds, only the tuples passing the selection are partitioned (hj3d_partition_sel)."""
+        preds, only the tuples passing the selection are partitioned (hj3d_partition_sel).
+        stride (>= rel's tuple count): the single-pass form for the probe side, order inside a
+        destination not kept, destination p's pairs at rows [p * stride, p * stride + counts[p]) of
+        out_pairs (hj3d_partition_strided)."""
+        if stride is not None:
+            if out_pairs.shape[0] < parts * stride:
+                raise ValueError("out_pairs holds fewer than parts * stride pairs")
+            self._check(lib().hj3d_partition_strided(self.h, C.byref(rel.c), _sel_preds(preds) if preds else None,
+                                                     len(preds) if preds else 0, num_buckets, parts,
+                                                     out_pairs.data_ptr(), stride, counts.data_ptr()),
+                        "hj3d_partition_strided")
+            return
         if preds:
             self._check(lib().hj3d_partition_sel(self.h, C.byref(rel.c), _sel_preds(preds), len(preds), num_buckets,
                                                  parts, out_pairs.data_ptr(), counts.data_ptr()), "hj3d_partition_sel")
@@ -553,9 +567,10 @@ class Comm:
                         "hj3d_comm_counts_cap")
         return ([list(snd[c * P:(c + 1) * P]) for c in range(Cn)], [list(rcv[c * P:(c + 1) * P]) for c in range(Cn)])
 
-    def exchange(self, send, sc, rc, recv_buf, asynchronous: bool = True):
+    def exchange(self, send, sc, rc, recv_buf, asynchronous: bool = True, send_stride: Optional[int] = None):
         """Grouped send / recv of one chunk of (key, row) pairs (rows of `send` grouped by
-        destination, sc[p] rows for peer p) into recv_buf (rc[p] rows from peer p, in rank order).
+        destination, sc[p] rows for peer p; with send_stride, peer p's rows start at p * send_stride)
+        into recv_buf (rc[p] rows from peer p, in rank order).
         Returns (received view, ticket or None); wait(ticket) orders the context stream after it."""
         P = self.world
         total = int(sum(rc))
@@ -564,10 +579,11 @@ class Comm:
             raise ValueError("send and receive rows differ in size")
         sca, rca = (C.c_int64 * P)(*sc), (C.c_int64 * P)(*rc)
         t = C.c_uint32()
-        self.ctx._check(lib().hj3d_comm_exchange(self.ctx.h, send.data_ptr() if send.numel() else None, sca,
-                                                 recv_buf.data_ptr() if recv_buf.numel() else None, rca,
-                                                 recv_buf.shape[0], elem, C.byref(t) if asynchronous else None),
-                        "hj3d_comm_exchange")
+        self.ctx._check(lib().hj3d_comm_exchange_strided(self.ctx.h, send.data_ptr() if send.numel() else None,
+                                                         send_stride or 0, sca,
+                                                         recv_buf.data_ptr() if recv_buf.numel() else None, rca,
+                                                         recv_buf.shape[0], elem, C.byref(t) if asynchronous else None),
+                        "hj3d_comm_exchange_strided")
         return recv_buf[:total], (t.value if asynchronous else None)
 
     def wait(self, ticket: int):

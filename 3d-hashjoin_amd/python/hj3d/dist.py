@@ -139,18 +139,22 @@ def exchange_counts(send_counts: torch.Tensor, group=None, recv_cap: int | None 
 
 
 def exchange_pairs_async(send_pairs: torch.Tensor, sc: list[int], rc: list[int], recv_buf: torch.Tensor,
-                         group=None):
+                         group=None, send_stride: int | None = None):
     """The pair all-to-all of one chunk whose counts were exchanged (exchange_counts), left in flight:
     returns (received view, work handle or None for the host-staged gloo rehearsal). recv_buf must
     hold sum(rc) pairs: every rank knows its own receive total before any pair collective starts,
-    so a short buffer is the caller's sizing error, reported before the collective (never a hang)."""
+    so a short buffer is the caller's sizing error, reported before the collective (never a hang).
+    send_stride: peer p's pairs start at row p * send_stride of send_pairs (the single-pass
+    partitioner's layout, Context.partition(..., stride=)); None: back to back."""
     total = int(sum(rc))
     if recv_buf.shape[0] < total:
         raise RuntimeError(f"exchange: receive buffer holds {recv_buf.shape[0]} pairs, {total} arrive")
     if _comm is not None:
-        out, t = _comm.exchange(send_pairs, sc, rc, recv_buf, asynchronous=True)
+        out, t = _comm.exchange(send_pairs, sc, rc, recv_buf, asynchronous=True, send_stride=send_stride)
         return out, _Ticket(_comm, t)
     out = recv_buf[:total]
+    if send_stride is not None:  # torch's all-to-all takes the blocks back to back
+        send_pairs = torch.cat([send_pairs[p * send_stride:p * send_stride + int(c)] for p, c in enumerate(sc)])
     src = send_pairs[: int(sum(sc))]
     if _host_staged(group) and send_pairs.is_cuda:
         got = torch.empty((total, 2), dtype=send_pairs.dtype)

@@ -76,7 +76,7 @@ def merge_shard_stats(parts: list) -> dict:
 
 
 def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=None, stats: bool = True,
-                      checksum: bool = True, timing: list | None = None) -> dict:
+                      checksum: bool = True, timing: list | None = None, single_pass: bool = False) -> dict:
     """The multi-GPU split of SURVEY §8(e) emulated on ONE device, owner after owner: both
     relations are partitioned into `parts` bucket ranges by the exchange partitioner
     (hj3d_partition, as every rank does before the all-to-all), then for each owner p a table over
@@ -84,7 +84,9 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
     row ids, as received). This is each rank's compute at its real geometry (bucket_lo != 0,
     |R| / parts buckets), without the exchange; the counters add up to the single-table run's and
     are returned in exp1_plan's form. timing (a list): one dict of per-owner phase times (ms, the
-    library's HIP-event timers) is appended per owner, plus {"owner": "partition", ...} first."""
+    library's HIP-event timers) is appended per owner, plus {"owner": "partition", ...} first.
+    single_pass: the probe side through the single-pass partitioner (hj3d_partition_strided, no
+    order inside an owner; parts x |probe| pairs of send buffer), as bench.py's strand does."""
     import torch
     from . import (T_BUILD, T_HIST, T_PARTITION, T_PROBE, T_PROBE_KERNEL, T_SCATTER, MASK64, part_range)
     kind, bside, bkey, pkey, unique, unnest = EXP1_PLANS[plan]
@@ -92,7 +94,8 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
     probe = Rel(S if bside == "R" else R, key_word=pkey)
     dev = R.device
     bp = torch.empty((max(build.n, 1), 2), dtype=torch.int32, device=dev)
-    pp = torch.empty((max(probe.n, 1), 2), dtype=torch.int32, device=dev)
+    stride = probe.n if single_pass else None
+    pp = torch.empty((max(probe.n * (parts if single_pass else 1), 1), 2), dtype=torch.int32, device=dev)
     bc = torch.zeros(parts, dtype=torch.int64, device=dev)
     pc = torch.zeros(parts, dtype=torch.int64, device=dev)
     phases = {"build": T_BUILD, "probe": T_PROBE, "part_kernel": T_SCATTER, "split_kernel": T_HIST,
@@ -111,11 +114,15 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
         ctx.timing(True)
         ctx.timer_reset()
     ctx.partition(build, nb, parts, bp, bc)
-    ctx.partition(probe, nb, parts, pp, pc)
+    tb = timers() if timing is not None else {}
+    ctx.partition(probe, nb, parts, pp, pc, stride=stride)
     if timing is not None:
-        timing.append(dict(owner="partition", **timers()))
+        tp = timers()
+        timing.append(dict(owner="partition", partition=tb.get("partition", 0.0) + tp.get("partition", 0.0),
+                           partition_build=tb.get("partition"), partition_probe=tp.get("partition")))
     bcs = [0] + torch.cumsum(bc, 0).tolist()
     pcs = [0] + torch.cumsum(pc, 0).tolist()
+    pstart = [p * stride for p in range(parts)] if single_pass else pcs[:-1]
     tot = {"c_probe": 0, "c_cmp": 0, "c_unnest": 0, "c_top": 0, "n": 0, "sum_a": 0, "sum_b": 0, "sum_c": 0,
            "sum_h": 0, "xor_h": 0, "overflow": False}
     shard_stats = []
@@ -127,7 +134,7 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
         t.reserve(max(nbp, 1))
         t.build(Rel(bp[bcs[p]:bcs[p + 1]], key_word=0, row_word=1, n=nbp))
         o = out[ooff:] if out is not None else None
-        r = ctx.probe(t, Rel(pp[pcs[p]:pcs[p + 1]], key_word=0, row_word=1, n=npp), unique=unique, unnest=unnest,
+        r = ctx.probe(t, Rel(pp[pstart[p]:pstart[p] + npp], key_word=0, row_word=1, n=npp), unique=unique, unnest=unnest,
                       out=o, checksum=checksum)
         if kind == HJ3D_CHAIN:
             c_probe, c_unnest, c_top = r.n_out, 0, r.n_out

@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--rehearse", action="store_true",
                    help="N>1 on ONE GPU: every rank on cuda:0, gloo exchange staged through host memory "
                         "(checks the multi-GPU code path; the numbers are not a scaling measurement)")
+    p.add_argument("--xpart", default="single", choices=["single", "stable"],
+                   help="N>1 probe side: single-pass exchange partitioner (hj3d_partition_strided) or the "
+                        "stable two-pass one (hj3d_partition; A/B)")
     p.add_argument("--plan", default="Csr", choices=["Csr", "Nsr", "Nrs"],
                    help="workload B/D plan: Csr chaining build R / probe S (the headline); Nsr 3D table on R.k, "
                         "probe S + unnest; Nrs 3D table on S.a (NB = #dv(S.a) from the distributed pre-pass), "
@@ -384,16 +387,29 @@ def main():
         lo, hi = hj3d.part_range(nb, world, rank)
         table = hj3d.Table(ctx, kind, nb, lo, hi)
         sendB = torch.empty((nB, 2), dtype=torch.int32, device=dev)
-        sendP = torch.empty((nP, 2), dtype=torch.int32, device=dev)
         cntB = torch.zeros((1, world), dtype=torch.int64, device=dev)
         sb = [nP * c // C for c in range(C + 1)]
         pRel_c = [hj3d.Rel(pT[sb[c]:sb[c + 1]], key_word=pkw, row_base=prow0 + sb[c]) for c in range(C)]
         cntP = torch.zeros((C, world), dtype=torch.int64, device=dev)
+        # probe side: the single-pass partitioner writes destination p of chunk c at rows
+        # [p * stride_c, ...) of that chunk's send buffer (stride_c = the chunk's tuple count); the
+        # build side keeps the stable two-pass partitioner (its order fixes long chains' order)
+        single = args.xpart == "single"
+        if single:
+            xstride = [sb[c + 1] - sb[c] for c in range(C)]
+            sendP_c = [torch.empty((max(world * xstride[c], 1), 2), dtype=torch.int32, device=dev) for c in range(C)]
+        else:
+            xstride = [None] * C
+            sendP = torch.empty((nP, 2), dtype=torch.int32, device=dev)
+            sendP_c = [sendP[sb[c]:sb[c + 1]] for c in range(C)]
+
+        def part_probe(c):
+            ctx.partition(pRel_c[c], nb, world, sendP_c[c], cntP[c], stride=xstride[c])
         # receive buffers sized from the exchanged counts of a sizing pass (partition + counts
         # all-to-all): the inputs do not change between steps, so neither do the receive totals
         ctx.partition(bRel, nb, world, sendB, cntB[0])
         for c in range(C):
-            ctx.partition(pRel_c[c], nb, world, sendP[sb[c]:sb[c + 1]], cntP[c])
+            part_probe(c)
         _, rcB = hdist.exchange_counts(cntB)
         _, rcP = hdist.exchange_counts(cntP)
         n_recvB, n_recvP = int(sum(rcB[0])), int(sum(sum(r) for r in rcP))
@@ -429,11 +445,11 @@ def main():
             # chunk c as soon as its pairs have arrived (chunk c+1 in flight meanwhile); the chunks
             # accumulate into one probe strand
             for c in range(C):
-                ctx.partition(pRel_c[c], nb, world, sendP[sb[c]:sb[c + 1]], cntP[c])
+                part_probe(c)
             scP, rcP = hdist.exchange_counts(cntP, recv_cap=recvP.shape[0])
             pend, roff = [], 0
             for c in range(C):
-                rS, work = hdist.exchange_pairs_async(sendP[sb[c]:sb[c + 1]], scP[c], rcP[c], recvP[roff:])
+                rS, work = hdist.exchange_pairs_async(sendP_c[c], scP[c], rcP[c], recvP[roff:], send_stride=xstride[c])
                 roff += rS.shape[0]
                 pend.append((rS, work))
             ooff = 0
@@ -638,6 +654,9 @@ def main():
             "S_per_gpu": nS_tot // world, "num_buckets": nb, "num_dv_Sa": dv,
             "emit_pairs": emit, "parallelism": f"bucket-range partition x{world}" if sharded else "single GPU",
             "exchange_chunks": (C if sharded else None),
+            "exchange_partitioner": ((("single-pass hj3d_partition_strided" if args.xpart == "single" else
+                                       "stable two-pass hj3d_partition") + " (probe side); stable (build side)")
+                                     if sharded else None),
             "exchange": ("libhj3d hj3d_comm_* over RCCL" if sharded and not args.rehearse else
                          "torch.distributed gloo, host-staged (rehearsal)" if sharded else None),
             "rehearsal_one_gpu": bool(args.rehearse),

@@ -259,6 +259,17 @@ hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t num_buck
 typedef struct hj3d_sel_pred hj3d_sel_pred;
 hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                                uint64_t num_buckets, uint32_t nparts, void* out_pairs_dev, void* counts_dev);
+/* Single-pass form for the probe side of the exchange (no order kept inside a destination: the
+ * probe's counters are per tuple; the build side keeps hj3d_partition's stable order, which fixes
+ * the chain order of buckets longer than the sorted build handles). The relation is read once
+ * (hj3d_partition reads it twice); destination p's pairs go to out_pairs_dev + p * stride pairs
+ * (stride >= rel->n, nparts <= 256), counts_dev[p] (device u64) = their number. preds / npred: an
+ * optional selection as in hj3d_partition_sel (npred = 0: none). Send it with
+ * hj3d_comm_exchange_strided (same stride). Replaces the same seam as hj3d_partition
+ * (the reference itself runs on one node, main_experiment1.cc:623-848). */
+hj3d_status hj3d_partition_strided(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
+                                   uint64_t num_buckets, uint32_t nparts, void* out_pairs_dev, uint64_t stride,
+                                   void* counts_dev);
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
 /* Slice geometry the packed unique probe takes for a chaining table of nb_local buckets holding
@@ -312,6 +323,11 @@ hj3d_status hj3d_comm_counts_cap(hj3d_ctx* ctx, const void* counts_dev, uint32_t
 hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_t* send_counts, void* recv_dev,
                                const int64_t* recv_counts, uint64_t recv_cap, uint32_t elem_bytes,
                                uint32_t* ticket);
+/* The same with peer p's elements at send_dev + p * send_stride elements (hj3d_partition_strided's
+ * layout; send_stride = 0: back to back); a send count above send_stride is HJ3D_EINVAL. */
+hj3d_status hj3d_comm_exchange_strided(hj3d_ctx* ctx, const void* send_dev, uint64_t send_stride,
+                                       const int64_t* send_counts, void* recv_dev, const int64_t* recv_counts,
+                                       uint64_t recv_cap, uint32_t elem_bytes, uint32_t* ticket);
 hj3d_status hj3d_comm_wait(hj3d_ctx* ctx, uint32_t ticket);
 hj3d_status hj3d_comm_allreduce_u64(hj3d_ctx* ctx, void* buf_dev, uint64_t n, int op);
 hj3d_status hj3d_comm_allgather(hj3d_ctx* ctx, const void* send_dev, void* recv_dev, uint64_t bytes);

@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--nR", type=float, default=1e8)
     ap.add_argument("--nS", type=float, default=1e9)
+    ap.add_argument("--xpart", default="single", choices=["single", "stable"],
+                    help="probe side: single-pass (hj3d_partition_strided) or stable two-pass exchange partitioner")
     a = ap.parse_args()
     import torch
     import hj3d
@@ -41,13 +43,16 @@ def main():
     ctx = hj3d.Context(0)
     nb = hj3d.num_buckets_exp1(a.plan, nR, 0, 1)
     out = torch.empty((nS, 2), dtype=torch.int32, device="cuda") if a.plan == "Csr" else None
-    hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False)  # warm-up
+    sp = a.xpart == "single"
+    hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False,
+                           single_pass=sp)  # warm-up
     runs = []
     for _ in range(a.reps):
         tm = []
-        hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False, timing=tm)
+        hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False, timing=tm,
+                               single_pass=sp)
         runs.append(tm)
-    got = hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out)  # verification run
+    got = hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, single_pass=sp)  # verification run
     fx_path = os.path.join(ROOT, "tests", "golden", f"exp1_R{nR}_S{nS}_uni.json")
     verify = None
     if os.path.exists(fx_path):
@@ -78,6 +83,7 @@ def main():
             d["probe_phase_frac"] = (npp * (16 + 8)) / (d["probe_ms"] * 1e-3) / 1e9 / PEAK
         owners.append(d)
     part_ms = avg("partition", "partition")
+    pb_ms, pp_ms = avg("partition", "partition_build"), avg("partition", "partition_probe")
     line = {
         "what": f"config D {a.parts}-owner split emulated on one GPU, plan {a.plan}: per-rank compute at the "
                 f"{a.parts}-GPU geometry, owners run one after another; exchange (xGMI) NOT included; not a "
@@ -85,6 +91,11 @@ def main():
         "nR": nR, "nS": nS, "num_buckets": nb, "reps": a.reps, "input_generation_s": gen_s,
         "exchange_partition_ms_both_relations": part_ms,
         "exchange_partition_frac": ((nR + nS) * 20) / (part_ms * 1e-3) / 1e9 / PEAK if part_ms else None,
+        "exchange_partitioner_probe_side": ("single-pass hj3d_partition_strided" if sp else
+                                            "stable two-pass hj3d_partition"),
+        "exchange_partition_build_ms": pb_ms,
+        "exchange_partition_probe_ms": pp_ms,
+        "exchange_partition_probe_frac": (nS * 20) / (pp_ms * 1e-3) / 1e9 / PEAK if pp_ms else None,
         "owners": owners,
         "max_owner_probe_ms": max(o["probe_ms"] for o in owners),
         "max_owner_build_ms": max(o["build_ms"] for o in owners),

@@ -1,7 +1,8 @@
 """Multi-GPU path rehearsed on CPU: world size 2, gloo backend.
 
 Each rank holds a contiguous slice of R and S (global row ids), partitions it by bucket range
-exactly as hj3d_partition does (owner = bucket * P / NB, stable; restated here in numpy),
+exactly as hj3d_partition does (owner = bucket * P / NB, stable; restated here in numpy; the probe
+side as hj3d_partition_strided lays it out: strided, no order inside an owner),
 exchanges (key, row) pairs with hj3d.dist.exchange (all_to_all; the probe side in chunks through
 exchange_counts + exchange_pairs_async as bench.py does), and joins its received pairs
 with the oracle over the full bucket space (only its own buckets are populated). The per-rank
@@ -40,6 +41,21 @@ def partition(keys, rows, nb, parts):
     pairs = np.stack([keys[order], rows[order]], axis=1).astype(np.uint32)
     counts = np.bincount(owner, minlength=parts).astype(np.int64)
     return pairs, counts
+
+
+def partition_strided(keys, rows, nb, parts, seed):
+    """hj3d_partition_strided's layout: owner p's pairs at rows [p * n, p * n + counts[p]) of a
+    (parts * n, 2) buffer, in NO particular order inside an owner (shuffled here; the device's
+    order depends on run claims), the rest of each area garbage."""
+    n = len(keys)
+    pairs, counts = partition(keys, rows, nb, parts)
+    out = np.full((max(parts * n, 1), 2), 0xDEADBEEF, dtype=np.uint32)
+    rng = np.random.default_rng(seed)
+    starts = np.concatenate([[0], np.cumsum(counts)])
+    for p in range(parts):
+        blk = pairs[starts[p]:starts[p + 1]]
+        out[p * n:p * n + counts[p]] = blk[rng.permutation(len(blk))]
+    return out, counts
 
 
 def bitmap_np(keys, words):
@@ -97,18 +113,20 @@ def _worker(rank, port, case, q):
             pairs, counts = partition(k, r, nb, WORLD)
             got = hdist.exchange(torch.from_numpy(pairs.view(np.int32)), torch.from_numpy(counts))
             recv.append(got.numpy().view(np.uint32))
-            # the probe side as bench.py ships it: 3 chunks partitioned separately, all chunks'
-            # counts in one collective, then one pair all-to-all per chunk into one receive buffer
+            # the probe side as bench.py ships it: 3 chunks partitioned separately (the single-pass
+            # partitioner's strided, unordered layout), all chunks' counts in one collective, then one
+            # pair all-to-all per chunk into one receive buffer
             k, r = local(pkeys)
             cb = [len(k) * c // 3 for c in range(4)]
-            parts = [partition(k[cb[c]:cb[c + 1]], r[cb[c]:cb[c + 1]], nb, WORLD) for c in range(3)]
+            parts = [partition_strided(k[cb[c]:cb[c + 1]], r[cb[c]:cb[c + 1]], nb, WORLD, seed=rank * 3 + c)
+                     for c in range(3)]
             sc, rc = hdist.exchange_counts(torch.from_numpy(np.stack([pc for _, pc in parts])))
             assert sc == [pc.tolist() for _, pc in parts]
             rbuf = torch.empty((sum(map(sum, rc)), 2), dtype=torch.int32)
             off = 0
             for c in range(3):
                 got, work = hdist.exchange_pairs_async(torch.from_numpy(parts[c][0].view(np.int32)), sc[c], rc[c],
-                                                       rbuf[off:])
+                                                       rbuf[off:], send_stride=cb[c + 1] - cb[c])
                 assert work is None or work.wait()
                 off += got.shape[0]
             recv.append(rbuf.numpy().view(np.uint32))

@@ -274,9 +274,11 @@ def test_skewed_hot_key_heavy_unnest(ctx):
     _compare(ctx, R, S, nR, O.num_distinct(Sa))
 
 
-def test_bucket_shards_sum_to_single_table(ctx):
+@pytest.mark.parametrize("single", [False, True], ids=["stable", "single_pass"])
+def test_bucket_shards_sum_to_single_table(ctx, single):
     """Multi-GPU building block: tables that own disjoint bucket ranges, probed by the tuples of
-    their range (hj3d_partition), add up to the single-table reference counters exactly."""
+    their range (hj3d_partition; single_pass: the probe side from hj3d_partition_strided, no order
+    inside a range), add up to the single-table reference counters exactly."""
     import torch
     import hj3d
     g = dict(load_golden("exp1_R1024_S4096_zipf.json"))["exp1_R1024_S4096_zipf"]
@@ -289,18 +291,23 @@ def test_bucket_shards_sum_to_single_table(ctx):
         probe = hj3d.Rel(dS if bside == "R" else dR, key_word=pkey)
         parts = 3
         bp = torch.zeros((build.n, 2), dtype=torch.int32, device="cuda")
-        pp = torch.zeros((probe.n, 2), dtype=torch.int32, device="cuda")
+        stride = probe.n if single else None
+        pp = torch.zeros((probe.n * (parts if single else 1), 2), dtype=torch.int32, device="cuda")
         bc = torch.zeros(parts, dtype=torch.int64, device="cuda")
         pc = torch.zeros(parts, dtype=torch.int64, device="cuda")
         ctx.partition(build, nb, parts, bp, bc)
-        ctx.partition(probe, nb, parts, pp, pc)
+        ctx.partition(probe, nb, parts, pp, pc, stride=stride)
         bcs, pcs = [0] + np.cumsum(bc.cpu().numpy()).tolist(), [0] + np.cumsum(pc.cpu().numpy()).tolist()
+        if single:  # range p's probe pairs at [p * stride, p * stride + pc[p])
+            pcs = [[p * stride, p * stride + int(pc[p])] for p in range(parts)]
+        else:
+            pcs = [[pcs[p], pcs[p + 1]] for p in range(parts)]
         tot = {"c_cmp": 0, "n_out": 0, "n_matched": 0, "sum_h": 0, "xor_h": 0, "empty": 0, "cc0_max": 0}
         for p in range(parts):
             lo, hi = hj3d.part_range(nb, parts, p)
             t = hj3d.Table(ctx, kind, nb, lo, hi)
             t.build(hj3d.Rel(bp[bcs[p]:bcs[p + 1]], key_word=0, row_word=1))
-            r = ctx.probe(t, hj3d.Rel(pp[pcs[p]:pcs[p + 1]], key_word=0, row_word=1), unique=unique, unnest=unnest)
+            r = ctx.probe(t, hj3d.Rel(pp[pcs[p][0]:pcs[p][1]], key_word=0, row_word=1), unique=unique, unnest=unnest)
             st = t.stats()
             tot["c_cmp"] += r.n_cmps
             tot["n_out"] += r.n_out
