@@ -62,7 +62,7 @@ struct hj3d_ctx {
   int num_cus = 256;
   std::string last_error;
   // scratch arena slots (see api for their use)
-  hj3d::DevBuf scratch[14];
+  hj3d::DevBuf scratch[15];
   hj3d::DevBuf res;       // device result slot (u64 fields) for probe / probe2
   hj3d::DevBuf misc;      // small device reductions (statistics)
   uint32_t res_flags = 0;     // flags of the last probe (overflow check in hj3d_probe_result)
@@ -334,7 +334,8 @@ enum ScratchSlot {
   kScrPStart = 11,  // partition starts of the probe side
   kScrPk2 = 12,     // packed probe, second partition level: fine regions
   kScrPk2Cnt = 13,  // and their pair counts
-  kScrSlots = 14
+  kScrSink = 14,    // 1024 pairs: target of the stores of lanes without a pair (fixed store counts)
+  kScrSlots = 15
 };
 
 // Per-block result partials: kernels store their block totals (block_store) to
@@ -417,6 +418,13 @@ inline RelView view_of(const hj3d_rel& r) {
 
 // Grid for grid-stride streaming kernels: enough blocks to fill the chip (>= 8 per CU),
 // bounded so that per-block result flushes stay cheap.
+// the sink of fixed-count store loops (garbage, shared by every workgroup)
+inline hipError_t store_sink(hj3d_ctx* ctx, uint2** sink) {
+  const hipError_t e = ctx->scratch[kScrSink].ensure(1024 * sizeof(uint2));
+  *sink = ctx->scratch[kScrSink].as<uint2>();
+  return e;
+}
+
 inline unsigned grid_for(const hj3d_ctx* ctx, uint64_t items, unsigned items_per_block) {
   const uint64_t want = (items + items_per_block - 1) / items_per_block;
   const uint64_t cap = uint64_t(ctx->num_cus) * 8;

@@ -479,8 +479,8 @@ hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint
   auto* cnt = static_cast<unsigned long long*>(counts);
   auto* out = static_cast<uint2*>(out_pairs);
   const bool implicit = v.row_off == 0xFFFFFFFFu;
-  if ((e = ctx->scratch[kScrD].ensure(kXpBlock * sizeof(uint2))) != hipSuccess) return e;
-  uint2* sink = ctx->scratch[kScrD].as<uint2>();  // garbage stores of lanes without a pair
+  uint2* sink;  // garbage stores of lanes without a pair
+  if ((e = store_sink(ctx, &sink)) != hipSuccess) return e;
   const SelArgs sa = sel ? *sel : SelArgs{};
   if (sa.npred)
     hipLaunchKernelGGL((implicit ? k_xpart<true, true> : k_xpart<true, false>), dim3(grid), dim3(kXpBlock), 0, s, v, fm,
