@@ -417,6 +417,166 @@ __global__ __launch_bounds__(kBlock) void k_key_bitmap(RelView r, uint64_t domai
   if (outside && (threadIdx.x & 63) == 0 && t) atomicAdd(outside, (unsigned long long)t);
 }
 
+// The same bitmap without a device atomic per key (large inputs): the key domain is cut into NS =
+// 2^lg slices of whole 32-bit words, word w in slice w & (NS - 1) at slice word w >> lg, each slice
+// small enough for an LDS bitmap (<= kDvSliceWords words; interleaved by word, so a key range that
+// is dense in one part of the domain still spreads over every slice).
+//  pass 1 k_dv_part: one 1024-thread workgroup per 8192-tuple tile reads the keys (12-B tuples as
+//    three 16-B loads per 4 tuples), ranks them by slice with LDS atomics (no order kept) and writes
+//    the tile back slice-major as bit positions inside the slice (u32), with its NS + 1 run bounds
+//    (u16) per tile; keys >= domain are counted in *outside.
+//  pass 2 k_dv_bits: workgroup (s, g) sets the bits of slice s's runs in tiles [g·T/G2, (g+1)·T/G2)
+//    in an LDS bitmap (an LDS read first: a bit already set costs no atomic) and stores it as partial
+//    row g of slice s.
+//  pass 3 k_dv_merge: bm[w] |= OR over the G2 partial rows of slice w & (NS-1), word w >> lg.
+// Per key: the tuple read once + 4 B written and read back; the partial rows are G2 × the bitmap.
+constexpr int kDvBlock = 1024;
+constexpr int kDvPer = 8;
+constexpr int kDvTile = kDvBlock * kDvPer;  // run bounds fit u16
+constexpr uint32_t kDvMaxSlices = 1024;
+constexpr uint32_t kDvSliceWords = 20480;  // 80 KB: two pass-2 workgroups per CU
+constexpr uint32_t kDvSkip = 0xFFFFFFFFu;  // a tuple past the end or a key outside the domain
+
+// KO = key word inside a 12-B tuple (0..2) for the vector load form; -1: any layout (RelView::key)
+template <int KO>
+__global__ __launch_bounds__(kDvBlock) void k_dv_part(RelView r, uint64_t domain, uint32_t lg,
+                                                      uint32_t* __restrict__ pos_out, uint16_t* __restrict__ bounds,
+                                                      unsigned long long* __restrict__ outside) {
+  __shared__ uint32_t stage[kDvTile];
+  __shared__ uint32_t cnt[kDvMaxSlices];
+  __shared__ uint32_t wtot[kDvBlock / kWave];
+  const uint32_t me = threadIdx.x, ns = 1u << lg;
+  const int lane = me & 63, wid = me >> 6;
+  const uint64_t base = uint64_t(blockIdx.x) * kDvTile;
+  for (uint32_t s = me; s < ns; s += kDvBlock) cnt[s] = 0;
+  uint32_t k[kDvPer];
+  if constexpr (KO >= 0) {
+    // thread me: tuples base + h·4096 + 4·me .. +3 for h = 0, 1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint64_t i0 = base + uint64_t(h) * (kDvTile / 2) + 4ull * me;
+      if (i0 + 4 <= r.n) {
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        const u32x4* p = reinterpret_cast<const u32x4*>(r.base + i0 * 12);
+        const u32x4 a = __builtin_nontemporal_load(p), b = __builtin_nontemporal_load(p + 1),
+                    c = __builtin_nontemporal_load(p + 2);
+        const uint32_t w[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k[h * 4 + q] = w[3 * q + KO];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) k[h * 4 + q] = i0 + q < r.n ? r.key(i0 + q) : kDvSkip;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kDvPer; ++q) {
+      const uint64_t i = base + uint64_t(q) * kDvBlock + me;
+      k[q] = i < r.n ? r.key(i) : kDvSkip;
+    }
+  }
+  // tuples past the end drop out; keys outside the domain are counted
+  uint32_t nout = 0, valid = 0;
+#pragma unroll
+  for (int q = 0; q < kDvPer; ++q) {
+    const uint64_t i = KO >= 0 ? base + uint64_t(q >> 2) * (kDvTile / 2) + 4ull * me + (q & 3)
+                               : base + uint64_t(q) * kDvBlock + me;
+    if (i < r.n) {
+      if (uint64_t(k[q]) < domain) valid |= 1u << q;
+      else ++nout;
+    }
+  }
+  __syncthreads();  // cnt cleared
+  uint32_t slot[kDvPer];
+#pragma unroll
+  for (int q = 0; q < kDvPer; ++q)
+    if (valid >> q & 1u) slot[q] = atomicAdd(&cnt[(k[q] >> 5) & (ns - 1)], 1u);
+  __syncthreads();
+  // exclusive scan of the slice counts (ns <= 1024 = one per thread)
+  const uint32_t c = me < ns ? cnt[me] : 0u;
+  uint32_t wt;
+  const uint32_t ex = wave_excl_scan(c, &wt);
+  if (lane == 0) wtot[wid] = wt;
+  __syncthreads();
+  uint32_t before = 0, total = 0;
+#pragma unroll
+  for (int w = 0; w < kDvBlock / kWave; ++w) {
+    const uint32_t x = wtot[w];
+    before += w < wid ? x : 0u;
+    total += x;
+  }
+  __syncthreads();  // every thread has read its slice count
+  uint16_t* bd = bounds + uint64_t(blockIdx.x) * (ns + 1);
+  if (me < ns) {
+    cnt[me] = before + ex;
+    bd[me] = uint16_t(before + ex);
+  }
+  if (me == 0) bd[ns] = uint16_t(total);
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kDvPer; ++q)
+    if (valid >> q & 1u) {
+      const uint32_t w = k[q] >> 5;
+      stage[cnt[w & (ns - 1)] + slot[q]] = ((w >> lg) << 5) | (k[q] & 31u);
+    }
+  __syncthreads();
+  for (uint32_t x = me; x < total; x += kDvBlock) __builtin_nontemporal_store(stage[x], pos_out + base + x);
+  const uint64_t t = wave_sum(uint64_t(nout));
+  if (outside && lane == 0 && t) atomicAdd(outside, (unsigned long long)t);
+}
+
+// workgroup (s, g) = blockIdx.x = s * g2 + g; tiles [g·ntiles/g2, (g+1)·ntiles/g2), wave w takes
+// every 16th of them
+__global__ __launch_bounds__(kDvBlock) void k_dv_bits(const uint32_t* __restrict__ pos, const uint16_t* __restrict__ bounds,
+                                                      uint32_t lg, uint64_t ntiles, uint32_t g2, uint32_t wps,
+                                                      uint32_t* __restrict__ part) {
+  extern __shared__ uint32_t bm[];
+  const uint32_t me = threadIdx.x, ns = 1u << lg;
+  const uint32_t s = blockIdx.x / g2, g = blockIdx.x % g2;
+  const int lane = me & 63, wid = me >> 6;
+  for (uint32_t j = me; j < wps; j += kDvBlock) bm[j] = 0;
+  __syncthreads();
+  const uint64_t t0 = ntiles * g / g2, t1 = ntiles * (g + 1) / g2;
+  for (uint64_t t = t0 + wid; t < t1; t += kDvBlock / kWave) {
+    const uint16_t* bd = bounds + t * (ns + 1) + s;
+    const uint32_t lo = bd[0], hi = bd[1];
+    const uint32_t* p = pos + t * kDvTile;
+    uint32_t x = lo + lane;
+    for (; x + 3 * kWave < hi; x += 4 * kWave) {
+      uint32_t v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(p + x + u * kWave);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t bit = 1u << (v[u] & 31u);
+        if (!(bm[v[u] >> 5] & bit)) atomicOr(&bm[v[u] >> 5], bit);
+      }
+    }
+    for (; x < hi; x += kWave) {
+      const uint32_t v = __builtin_nontemporal_load(p + x), bit = 1u << (v & 31u);
+      if (!(bm[v >> 5] & bit)) atomicOr(&bm[v >> 5], bit);
+    }
+  }
+  __syncthreads();
+  uint32_t* row = part + (uint64_t(s) * g2 + g) * wps;
+  for (uint32_t j = me; j < wps; j += kDvBlock) row[j] = bm[j];
+}
+
+// thread (s, j), j fastest: bm[j·NS + s] |= OR over g of part[(s·g2 + g)·wps + j]
+__global__ __launch_bounds__(kBlock) void k_dv_merge(const uint32_t* __restrict__ part, uint32_t lg, uint32_t g2,
+                                                     uint32_t wps, uint64_t words, uint32_t* __restrict__ bm) {
+  const uint64_t n = uint64_t(wps) << lg;
+  for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock) {
+    const uint32_t s = uint32_t(i / wps), j = uint32_t(i % wps);
+    const uint64_t w = (uint64_t(j) << lg) | s;
+    if (w >= words) continue;
+    const uint32_t* src = part + uint64_t(s) * g2 * wps + j;
+    uint32_t x = 0;
+    for (uint32_t g = 0; g < g2; ++g) x |= src[uint64_t(g) * wps];
+    if (x) bm[w] |= x;
+  }
+}
+
 // *count += popcount(OR over rows of bm[row * words + w]) over w < words.
 __global__ __launch_bounds__(kBlock) void k_or_popcount(const uint32_t* __restrict__ bm, uint32_t rows, uint64_t words,
                                                         unsigned long long* __restrict__ count) {
@@ -537,6 +697,42 @@ hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel
 
 hipError_t key_bitmap(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t domain, void* bitmap, void* outside, hipStream_t s) {
   if (r.n == 0) return hipSuccess;
+  const uint64_t words = (domain + 31) / 32;
+  uint32_t lg = 0;
+  while ((words >> lg) > kDvSliceWords) ++lg;
+  if ((words + (1ull << lg) - 1) >> lg > kDvSliceWords) ++lg;  // ceil(words / NS) <= kDvSliceWords
+  static const bool direct = [] {
+    const char* e = getenv("HJ3D_OPT_DV_DIRECT");
+    return e && *e && *e != '0';
+  }();
+  if (!direct && r.n >= (1u << 20) && domain > 0 && (1u << lg) <= kDvMaxSlices && r.stride >= 4) {
+    const uint32_t ns = 1u << lg, wps = uint32_t((words + ns - 1) >> lg);
+    const uint64_t ntiles = (r.n + kDvTile - 1) / kDvTile;
+    uint32_t g2 = uint32_t(2 * ctx->num_cus) / ns;  // two 80-KB workgroups per CU
+    if (g2 < 1) g2 = 1;
+    if (g2 > ntiles) g2 = uint32_t(ntiles);
+    hipError_t e;
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_dv_bits),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (attr != hipSuccess) return attr;
+    if ((e = ctx->scratch[kScrSortK].ensure(ntiles * kDvTile * sizeof(uint32_t))) != hipSuccess ||
+        (e = ctx->scratch[kScrPHist].ensure(ntiles * (ns + 1) * sizeof(uint16_t))) != hipSuccess ||
+        (e = ctx->scratch[kScrSortV].ensure(uint64_t(ns) * g2 * wps * sizeof(uint32_t))) != hipSuccess)
+      return e;
+    uint32_t* pos = ctx->scratch[kScrSortK].as<uint32_t>();
+    uint16_t* bounds = ctx->scratch[kScrPHist].as<uint16_t>();
+    uint32_t* part = ctx->scratch[kScrSortV].as<uint32_t>();
+    const RelView v = view_of(r);
+    auto* outs = static_cast<unsigned long long*>(outside);
+    const bool v12 = r.stride == 12 && (reinterpret_cast<uintptr_t>(r.base) & 15) == 0 && r.key_off % 4 == 0;
+    auto pk = v12 ? (r.key_off == 0 ? k_dv_part<0> : r.key_off == 4 ? k_dv_part<1> : k_dv_part<2>) : k_dv_part<-1>;
+    hipLaunchKernelGGL(pk, dim3(unsigned(ntiles)), dim3(kDvBlock), 0, s, v, domain, lg, pos, bounds, outs);
+    hipLaunchKernelGGL(k_dv_bits, dim3(ns * g2), dim3(kDvBlock), wps * sizeof(uint32_t), s, pos, bounds, lg, ntiles,
+                       g2, wps, part);
+    hipLaunchKernelGGL(k_dv_merge, dim3(grid_for(ctx, uint64_t(wps) << lg, kBlock * 4)), dim3(kBlock), 0, s, part, lg,
+                       g2, wps, words, static_cast<uint32_t*>(bitmap));
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_key_bitmap, dim3(grid_for(ctx, r.n, kBlock * 4)), dim3(kBlock), 0, s, view_of(r), domain,
                      static_cast<uint32_t*>(bitmap), static_cast<unsigned long long*>(outside));
   return hipGetLastError();
