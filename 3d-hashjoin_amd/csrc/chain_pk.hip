@@ -45,7 +45,7 @@ constexpr int kPkBlock = 1024;
 #define HJ3D_PK_NTLOAD 1  // partition: probe keys loaded non-temporal (0: plain; nt 0.447 -> 0.436 ms, probe phase -2 %)
 #endif
 #ifndef HJ3D_PK_DIAG
-#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups
+#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups, 3 probe without staging the slice
 #endif
 #ifndef HJ3D_PK_SINK
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
@@ -793,7 +793,13 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     }
   };
   if (fits) {
-    walk([&]() __attribute__((always_inline)) { pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent); },
+    walk([&]() __attribute__((always_inline)) {
+           if (HJ3D_PK_DIAG == 3) {  // no staging: an empty directory (every probe misses)
+             for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) ldir[k] = 0;
+           } else {
+             pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent);
+           }
+         },
          [&](const uint64_t (&v)[K], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
            pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
          });

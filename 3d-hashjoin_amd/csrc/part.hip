@@ -536,25 +536,61 @@ __global__ __launch_bounds__(kDvBlock) void k_dv_bits(const uint32_t* __restrict
   const int lane = me & 63, wid = me >> 6;
   for (uint32_t j = me; j < wps; j += kDvBlock) bm[j] = 0;
   __syncthreads();
+  constexpr int kU = 8;  // keys per lane and run loaded in one batch (the next run's batch in flight)
+  constexpr uint32_t kWaves = kDvBlock / kWave;
   const uint64_t t0 = ntiles * g / g2, t1 = ntiles * (g + 1) / g2;
-  for (uint64_t t = t0 + wid; t < t1; t += kDvBlock / kWave) {
-    const uint16_t* bd = bounds + t * (ns + 1) + s;
-    const uint32_t lo = bd[0], hi = bd[1];
-    const uint32_t* p = pos + t * kDvTile;
-    uint32_t x = lo + lane;
-    for (; x + 3 * kWave < hi; x += 4 * kWave) {
-      uint32_t v[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = __builtin_nontemporal_load(p + x + u * kWave);
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t bit = 1u << (v[u] & 31u);
-        if (!(bm[v[u] >> 5] & bit)) atomicOr(&bm[v[u] >> 5], bit);
-      }
+  const uint64_t ntw = t0 + wid < t1 ? (t1 - t0 - wid + kWaves - 1) / kWaves : 0;  // this wave's tiles
+  const auto set_bit = [&](uint32_t v) __attribute__((always_inline)) {
+    const uint32_t bit = 1u << (v & 31u);
+    if (!(bm[v >> 5] & bit)) atomicOr(&bm[v >> 5], bit);
+  };
+  for (uint64_t c0 = 0; c0 < ntw; c0 += kWave) {
+    // lane k: run bounds of the wave's tile c0 + k (tile t0 + wid + 16 (c0 + k))
+    uint32_t blo = 0, bhi = 0;
+    if (c0 + lane < ntw) {
+      const uint16_t* bd = bounds + (t0 + wid + kWaves * (c0 + lane)) * (ns + 1) + s;
+      blo = bd[0];
+      bhi = bd[1];
     }
-    for (; x < hi; x += kWave) {
-      const uint32_t v = __builtin_nontemporal_load(p + x), bit = 1u << (v & 31u);
-      if (!(bm[v >> 5] & bit)) atomicOr(&bm[v >> 5], bit);
+    const uint32_t m = uint32_t(ntw - c0 < kWave ? ntw - c0 : kWave);
+    // runs taken kD at a time, the next kD runs' batches in flight
+    constexpr int kD = 2;
+    uint32_t v[kD][kU], nv[kD][kU];
+    const auto load = [&](uint32_t (&dst)[kD][kU], uint32_t i0) __attribute__((always_inline)) {
+#pragma unroll
+      for (int d = 0; d < kD; ++d) {
+        const uint32_t i = i0 + d < m ? i0 + d : m - 1;
+        const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(blo), int(i)));
+        const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(bhi), int(i)));
+        const uint32_t* p = pos + (t0 + wid + kWaves * (c0 + i)) * kDvTile;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const uint32_t x = lo + lane + u * kWave;
+          dst[d][u] = __builtin_nontemporal_load(p + (x < hi ? x : 0u));  // unconditional (slot 0 past the run)
+        }
+      }
+    };
+    load(v, 0);
+    for (uint32_t i0 = 0; i0 < m; i0 += kD) {
+      load(nv, i0 + kD < m ? i0 + kD : i0);
+#pragma unroll
+      for (int d = 0; d < kD; ++d) {
+        const uint32_t i = i0 + d;
+        if (i >= m) break;
+        const uint32_t lo = uint32_t(__builtin_amdgcn_readlane(int(blo), int(i)));
+        const uint32_t hi = uint32_t(__builtin_amdgcn_readlane(int(bhi), int(i)));
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+          if (lo + lane + u * kWave < hi) set_bit(v[d][u]);
+        if (lo + kU * kWave < hi) {  // a run longer than one batch
+          const uint32_t* p = pos + (t0 + wid + kWaves * (c0 + i)) * kDvTile;
+          for (uint32_t x = lo + kU * kWave + lane; x < hi; x += kWave) set_bit(__builtin_nontemporal_load(p + x));
+        }
+      }
+#pragma unroll
+      for (int d = 0; d < kD; ++d)
+#pragma unroll
+        for (int u = 0; u < kU; ++u) v[d][u] = nv[d][u];
     }
   }
   __syncthreads();
@@ -572,7 +608,15 @@ __global__ __launch_bounds__(kBlock) void k_dv_merge(const uint32_t* __restrict_
     if (w >= words) continue;
     const uint32_t* src = part + uint64_t(s) * g2 * wps + j;
     uint32_t x = 0;
-    for (uint32_t g = 0; g < g2; ++g) x |= src[uint64_t(g) * wps];
+    uint32_t g = 0;
+    for (; g + 8 <= g2; g += 8) {  // eight independent loads in flight
+      uint32_t y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) y[u] = src[uint64_t(g + u) * wps];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x |= y[u];
+    }
+    for (; g < g2; ++g) x |= src[uint64_t(g) * wps];
     if (x) bm[w] |= x;
   }
 }
