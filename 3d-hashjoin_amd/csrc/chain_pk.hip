@@ -836,7 +836,13 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     }
   }
   // this block's counters -> partials row (write-through stores), then the ticket; the last block
-  // folds every row into the result slot (loads that bypass the CU's L1) and resets the control words
+  // folds every row into the result slot (loads that bypass the CU's L1) and resets the control words.
+  // Ordering: the hand-off is the gfx950 form "8-B agent atomics both sides" of MI355X_MICROARCH.md
+  // (inter-workgroup visibility): every partial is an 8-B relaxed agent-scope store made by wave 0,
+  // which waits for them (vmcnt(0)) before its lane 0 takes the ticket with an agent-scope atomic;
+  // the block whose ticket came last reads the partials with 8-B relaxed agent-scope loads after a
+  // barrier. A release on the ticket (an L2 write-back per block) is not needed for that form; a
+  // target that counts stores apart from loads (vscnt) would need one here.
   __syncthreads();
 #pragma unroll
   for (int f = 1; f < kProbeFields; ++f) {
