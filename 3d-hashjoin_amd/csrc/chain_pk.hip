@@ -45,7 +45,7 @@ constexpr int kPkBlock = 1024;
 #define HJ3D_PK_NTLOAD 1  // partition: probe keys loaded non-temporal (0: plain; nt 0.447 -> 0.436 ms, probe phase -2 %)
 #endif
 #ifndef HJ3D_PK_DIAG
-#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups, 3 probe without staging the slice
+#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups, 3 probe without staging the slice, 4 probe without the first walk position's entry read
 #endif
 #ifndef HJ3D_PK_SINK
 #define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
@@ -493,7 +493,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t 
       live[j] = cmps[j] != 0 && cmps[j] <= kSortedMaxPk;
     }
 #pragma unroll
-    for (uint32_t c = 0; c < 3; ++c) {
+    for (uint32_t c = HJ3D_PK_DIAG == 4 ? 1 : 0; c < 3; ++c) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const uint32_t nn = d[j] & 0xFFFFu;
