@@ -197,9 +197,19 @@ hj3d_comm_state* st(hj3d_ctx* ctx) { return ctx ? ctx->comm : nullptr; }
 ncclResult_t alltoallv(hj3d_comm_state* c, const char* send, const int64_t* sc, char* recv, const int64_t* rc,
                        size_t elem, hipStream_t s, uint64_t send_stride = 0) {
   Rccl* r = rccl();
-  const size_t word = elem % 8 == 0 ? 8 : elem % 4 == 0 ? 4 : 1;
+  // diagnostics only (scripts/rccl_limits.py): HJ3D_COMM_WORD=1 forces byte words, HJ3D_COMM_PIECE_LOG2
+  // sets the piece size (default 27)
+  static const size_t force_word = [] {
+    const char* e = getenv("HJ3D_COMM_WORD");
+    return size_t(e && *e ? atoi(e) : 0);
+  }();
+  static const size_t kPiece = [] {
+    const char* e = getenv("HJ3D_COMM_PIECE_LOG2");
+    const int l = e && *e ? atoi(e) : 27;
+    return size_t(1) << (l < 0 ? 0 : l > 40 ? 40 : l);
+  }();
+  const size_t word = force_word == 1 ? 1 : elem % 8 == 0 ? 8 : elem % 4 == 0 ? 4 : 1;
   const ncclDataType_t dt = word == 8 ? ncclUint64 : word == 4 ? ncclUint32 : ncclUint8;
-  constexpr size_t kPiece = size_t(1) << 27;  // words per send / recv
   ncclResult_t e = r->groupStart();
   if (e != ncclSuccess) return e;
   size_t so = 0, ro = 0;
