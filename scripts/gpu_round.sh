@@ -1,12 +1,13 @@
-# A round record (split in two calls so that each fits gpurun's limit): PART=a the GPU tier
+# A round record (split in three calls so that each fits gpurun's limit): PART=a the GPU tier
 # (pytest -m gpu, smoke), the default bench line (as the driver runs it) + its rocprofv3 kernel stats,
-# PMC passes on the same code; PART=b configs C, E, D lines with kernel stats, the 8-owner split of
-# config D (scripts/d_shards.py) with its kernel stats. PART unset: both. Output under gpurun_out/
+# PMC passes on the same code; PART=b configs C, E, D lines with kernel stats; PART=c the 8-owner
+# split of config D (scripts/d_shards.py) with its kernel stats and its HBM bytes per probe tuple
+# (FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_bytes.py). PART unset: all. Output under gpurun_out/
 # (copied to profiles/ by hand).
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 TAG=${TAG:-r03}
-PART=${PART:-ab}
+PART=${PART:-abc}
 mkdir -p gpurun_out/prof
 step() { echo "[$(date +%T)] $*"; }
 if [[ $PART == *a* ]]; then
@@ -30,8 +31,17 @@ if [[ $PART == *b* ]]; then
     tail -1 gpurun_out/${TAG}_$w.log | cut -c1-300
     timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/${TAG}_$w -o run --output-format csv -- python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-mintime > gpurun_out/${TAG}_${w}_prof.log 2>&1 || exit 1
   done
+fi
+if [[ $PART == *c* ]]; then
   step d_shards
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/${TAG}_Dshards -o run --output-format csv -- python3 scripts/d_shards.py > gpurun_out/${TAG}_D_shards.json 2> gpurun_out/${TAG}_D_shards.err || { tail -5 gpurun_out/${TAG}_D_shards.err; exit 1; }
   tail -c 600 gpurun_out/${TAG}_D_shards.json
+  step pmc d_shards
+  i=0
+  for c in FETCH_SIZE WRITE_SIZE; do
+    i=$((i+1))
+    timeout -k 10 300 rocprofv3 --pmc $c --kernel-trace --output-format csv -d gpurun_out/pmc_${TAG}_Dsh/p$i -o run -- python3 scripts/d_shards.py --reps 1 > gpurun_out/pmc_${TAG}_Dsh_p$i.log 2>&1 || exit 1
+  done
+  python scripts/pmc_bytes.py ${TAG}_Dsh --runs 3 --out gpurun_out/${TAG}_D_shards_pmc.json
 fi
 step done
