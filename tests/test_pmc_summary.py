@@ -25,3 +25,36 @@ def test_kernel_name_mapping():
         "k_pk_probe<1, false>"
     assert m.short("void " + ns + "k_rp_part1r<1024, 8, 16, true, false>(hj3d::RelView)").startswith("k_rp_part1")
     assert m.short(ns + "k_scan_lb(unsigned int const*)") is None
+
+
+def test_pmc_bytes_per_probe_tuple(tmp_path, monkeypatch):
+    """scripts/pmc_bytes.py: every dispatch's FETCH_SIZE (x2, KiB) and WRITE_SIZE (KiB) summed per
+    kernel, divided by runs x |S|; the probe strand is the sum over its kernels."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    tag = "unit_Dsh"
+    root = tmp_path / "repo"
+    for i, (c, vals) in enumerate((("FETCH_SIZE", {"k_xpart": 6.0, "k_pk_part": 4.0, "k_pk_probe": 4.0,
+                                                    "k_rp_hist": 1.0}),
+                                   ("WRITE_SIZE", {"k_xpart": 8.0, "k_pk_part": 8.0, "k_pk_probe": 8.0}))):
+        d = root / "gpurun_out" / f"pmc_{tag}" / f"p{i + 1}"
+        d.mkdir(parents=True)
+        with open(d / "run_counter_collection.csv", "w", newline="") as fh:
+            w = csv.writer(fh)
+            w.writerow(["Kernel_Name", "Counter_Name", "Counter_Value", "Grid_Size"])
+            for k, v in vals.items():
+                for _ in range(2):  # two dispatches of each kernel: bytes add up
+                    w.writerow([f"void hj3d::(anonymous namespace)::{k}<true>(int)", c, v / 2 / 1024, 1024])
+    (root / "scripts").mkdir()
+    src = open(os.path.join(ROOT, "scripts", "pmc_bytes.py")).read()
+    (root / "scripts" / "pmc_bytes.py").write_text(src)
+    out = tmp_path / "o.json"
+    subprocess.run([sys.executable, str(root / "scripts" / "pmc_bytes.py"), tag, "--runs", "1", "--nS", "1",
+                    "--out", str(out)], check=True, capture_output=True)
+    r = json.load(open(out))
+    assert r["kernels"]["k_xpart"]["bytes_per_probe_tuple"] == 2 * 6.0 + 8.0
+    assert r["kernels"]["k_rp_hist"]["bytes_per_probe_tuple"] == 2 * 1.0
+    assert r["probe_strand_bytes_per_probe_tuple"] == (12 + 8) + (8 + 8) + (8 + 8)
+    assert "k_rp_hist" not in r["probe_strand_kernels"]
