@@ -3,6 +3,7 @@
 // Argument checking, context / table lifetime, device result slots and HIP-event phase
 // timers live here; the kernels are in the .hip translation units. Every entry point
 // returns an hj3d_status and never throws.
+#include <cmath>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -540,6 +541,15 @@ void hj3d_part_range(uint64_t nb, uint32_t parts, uint32_t part, uint64_t* lo, u
   if (hi) *hi = parts ? first(uint64_t(part) + 1) : nb;
 }
 
+uint64_t hj3d_partition_stride(uint64_t n, uint32_t parts) {
+  // Each tuple's destination is a bucket range of equal width: its count is ~ Binomial(n, 1/parts)
+  // for distinct keys. Area = mean + 8 sigma + 2 tiles of slack (the tile claims), capped at n.
+  if (parts <= 1) return n;
+  const double m = double(n) / parts, sd = std::sqrt(m * (1.0 - 1.0 / parts));
+  const uint64_t s = uint64_t(std::ceil(m + 8.0 * sd)) + 16384;
+  return s < n ? s : n;
+}
+
 hj3d_status hj3d_partition(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t nb, uint32_t parts, void* out_pairs,
                            void* counts) {
   if (!ctx || !rel_ok(rel) || !counts || (rel->n && !out_pairs)) return HJ3D_EINVAL;
@@ -559,7 +569,7 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
 hj3d_status hj3d_partition_strided(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                                    uint64_t nb, uint32_t parts, void* out_pairs, uint64_t stride, void* counts) {
   if (!ctx || !rel_ok(rel) || !counts || (rel->n && !out_pairs)) return HJ3D_EINVAL;
-  if (stride < rel->n) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: stride below rel->n");
+  if (stride == 0 && rel->n) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: stride 0");
   if (parts == 0 || parts > 256) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: nparts outside [1, 256]");
   if (npred && !sel_ok(rel, preds, npred)) return fail(ctx, HJ3D_EINVAL, "hj3d_partition_strided: invalid predicate");
   PhaseTimer tm(ctx, HJ3D_T_PARTITION);

@@ -126,18 +126,35 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
 #pragma unroll
   for (int j = 0; j < int(kPkSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
   uint32_t ha[kPkRounds], hb[kPkRounds], pa[SEL ? kPkRounds : 1], pb[SEL ? kPkRounds : 1];
+  // explicit rows: loaded with the key at tile prefetch and kept in registers (the row word shares
+  // the key's line; loading it again after the ranking phase fetched that line twice: 15.4 B per
+  // 8-B received pair, round 3). {key, row} pairs (stride 8, 8-B aligned) take one 8-B load.
+  uint32_t wa[IMPLICIT ? 1 : kPkRounds], wb[IMPLICIT ? 1 : kPkRounds];
+  const bool pair8 = !IMPLICIT && r.stride == 8 && r.key_off == 0 && r.row_off == 4 &&
+                     (reinterpret_cast<uintptr_t>(r.base) & 7u) == 0;
   // a wave-uniform 64-bit tile pointer + 32-bit lane offsets (the loads take the scalar-base form)
-  auto load = [&](uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1], uint32_t tile) __attribute__((always_inline)) {
+  auto load = [&](uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
+                  uint32_t (&rw)[IMPLICIT ? 1 : kPkRounds], uint32_t tile) __attribute__((always_inline)) {
     if constexpr (HJ3D_PK_GUARD) {
       const uint32_t base = tile * kPkTile;
 #pragma unroll
       for (int j = 0; j < kPkRounds; ++j) {
         const uint32_t i = base + uint32_t(j) * kPkBlock + me;
         const char* t = r.base + uint64_t(i) * r.stride;
-        if (HJ3D_PK_NTLOAD)
+        if constexpr (!IMPLICIT) {
+          if (pair8) {
+            const uint64_t kv = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(t)) : 0ull;
+            h[j] = uint32_t(kv);
+            rw[j] = uint32_t(kv >> 32);
+          } else {
+            h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
+            rw[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.row_off)) : 0u;
+          }
+        } else if (HJ3D_PK_NTLOAD) {
           h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
-        else
+        } else {
           h[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + r.key_off) : 0u;
+        }
         if constexpr (SEL) pw[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + sel.word_off) : 0u;
       }
     } else {
@@ -147,6 +164,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       for (int j = 0; j < kPkRounds; ++j) {
         const uint32_t o = min(uint32_t(j) * kPkBlock + me, lim) * r.stride;  // unconditional: clamped
         h[j] = *reinterpret_cast<const uint32_t*>(tp + o + r.key_off);
+        if constexpr (!IMPLICIT) rw[j] = *reinterpret_cast<const uint32_t*>(tp + o + r.row_off);
         if constexpr (SEL) pw[j] = *reinterpret_cast<const uint32_t*>(tp + o + sel.word_off);
       }
     }
@@ -187,7 +205,8 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     return pre + x - v;
   };
   uint32_t npassed = 0;
-  auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1]) __attribute__((always_inline)) {
+  auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
+                     uint32_t (&rw)[IMPLICIT ? 1 : kPkRounds]) __attribute__((always_inline)) {
     // HJ3D_PK_FEWBAR: loc[me] is cleared right after its count is read (nothing touches it again
     // in the tile) and no barrier ends the tile: the next tile's first LDS writes (stage, seginfo,
     // sbase) come after its ranking barrier, which every thread reaches only when done reading
@@ -257,10 +276,12 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     for (int j = 0; j < kPkRounds; ++j) {
       if (rk[j] == kInvalid) continue;
       const uint32_t li = uint32_t(j) * kPkBlock + me;
-      const uint32_t row = IMPLICIT ? rb + li : r.row(uint64_t(base) + li);
+      uint32_t row;
+      if constexpr (IMPLICIT) row = rb + li;
+      else row = rw[j];
       stage[sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1))] = make_uint2(h[j], row);
     }
-    load(h, pw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
+    load(h, pw, rw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
     __syncthreads();
     // whole segments: kPkSeg consecutive lanes store one 128-B segment
     for (uint32_t kk = me; kk < nfull * kPkSeg; kk += kPkBlock) {
@@ -291,15 +312,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     loc[me] = 0;
     __syncthreads();
   }
-  load(ha, pa, blockIdx.x);
+  load(ha, pa, wa, blockIdx.x);
   if constexpr (HJ3D_PK_AHEAD == 2) {
-    load(hb, pb, blockIdx.x + gridDim.x);
+    load(hb, pb, wb, blockIdx.x + gridDim.x);
     for (uint32_t tile = blockIdx.x; tile < ntiles; tile += 2 * gridDim.x) {
-      process(tile, ha, pa);
-      if (tile + gridDim.x < ntiles) process(tile + gridDim.x, hb, pb);
+      process(tile, ha, pa, wa);
+      if (tile + gridDim.x < ntiles) process(tile + gridDim.x, hb, pb, wb);
     }
   } else {
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa);
+    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa, wa);
   }
   flush_carry();
   if (me < P) counts[blockIdx.x * P + me] = min(my_cur, my_end);

@@ -191,24 +191,32 @@ hj3d_comm_state* st(hj3d_ctx* ctx) { return ctx ? ctx->comm : nullptr; }
 
 // grouped send / recv of per-peer blocks (an all-to-all with per-peer sizes); counts in elements
 // of elem bytes, displacements = prefix sums of the counts. Blocks move as 8- or 4-byte words
-// when their size allows, in pieces of at most 2^27 words (matched in order per peer), so no
-// RCCL count approaches 2^31 (a 2.5e8-pair chunk is 2e9 bytes).
+// when their size allows, in pieces of at most kPieceBytes = 2^28 bytes (matched in order per
+// peer). A single RCCL message of ~1 GiB and more arrived with its second half corrupted
+// (profiles/r03d_rccl_limits.jsonl, r04 sweep), so pieces stay a factor 4 below that, whatever the
+// word size.
 // send_stride (elements): peer p's elements start at send + p * send_stride (0: back to back)
+constexpr size_t kPieceBytes = size_t(1) << 28;
 ncclResult_t alltoallv(hj3d_comm_state* c, const char* send, const int64_t* sc, char* recv, const int64_t* rc,
                        size_t elem, hipStream_t s, uint64_t send_stride = 0) {
   Rccl* r = rccl();
-  // diagnostics only (scripts/rccl_limits.py): HJ3D_COMM_WORD=1 forces byte words, HJ3D_COMM_PIECE_LOG2
-  // sets the piece size (default 27)
+#ifdef HJ3D_COMM_DIAG
+  // diagnostic builds only (scripts/rccl_limits.sh builds a variant library with -DHJ3D_COMM_DIAG):
+  // HJ3D_COMM_WORD=1 forces byte words, HJ3D_COMM_PIECE_LOG2 sets the piece size in BYTES
   static const size_t force_word = [] {
     const char* e = getenv("HJ3D_COMM_WORD");
     return size_t(e && *e ? atoi(e) : 0);
   }();
-  static const size_t kPiece = [] {
+  static const size_t piece_bytes = [] {
     const char* e = getenv("HJ3D_COMM_PIECE_LOG2");
-    const int l = e && *e ? atoi(e) : 27;
-    return size_t(1) << (l < 0 ? 0 : l > 40 ? 40 : l);
+    const int l = e && *e ? atoi(e) : 28;
+    return size_t(1) << (l < 3 ? 3 : l > 40 ? 40 : l);
   }();
+#else
+  constexpr size_t force_word = 0, piece_bytes = kPieceBytes;
+#endif
   const size_t word = force_word == 1 ? 1 : elem % 8 == 0 ? 8 : elem % 4 == 0 ? 4 : 1;
+  const size_t kPiece = piece_bytes / word;  // words per piece
   const ncclDataType_t dt = word == 8 ? ncclUint64 : word == 4 ? ncclUint32 : ncclUint8;
   ncclResult_t e = r->groupStart();
   if (e != ncclSuccess) return e;

@@ -667,7 +667,7 @@ hipError_t partition(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t par
 
 hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint32_t parts, void* out_pairs,
                              uint64_t stride, void* counts, hipStream_t s, const SelArgs* sel) {
-  if (parts == 0 || parts > kXpMaxParts || nb == 0 || nb >= (1ull << 32) || stride < r.n) return hipErrorInvalidValue;
+  if (parts == 0 || parts > kXpMaxParts || nb == 0 || nb >= (1ull << 32) || (stride == 0 && r.n)) return hipErrorInvalidValue;
   hipError_t e;
   if ((e = hipMemsetAsync(counts, 0, parts * sizeof(uint64_t), s)) != hipSuccess) return e;
   if (r.n == 0) return hipSuccess;

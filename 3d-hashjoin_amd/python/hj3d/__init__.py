@@ -123,6 +123,7 @@ def lib():
         "hj3d_partition": (st, [p, R, u64, u32, p, p]),
         "hj3d_partition_sel": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, p]),
         "hj3d_partition_strided": (st, [p, R, C.POINTER(_SelPred), u32, u64, u32, p, u64, p]),
+        "hj3d_partition_stride": (u64, [u64, u32]),
         "hj3d_part_range": (None, [u64, u32, u32, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe_geometry": (C.c_int, [C.c_void_p, u64, u64, C.POINTER(u32)]),
         "hj3d_comm_counts_cap": (st, [p, p, u32, u64, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -138,6 +139,7 @@ def lib():
         "hj3d_gen_exp1_ref": (st, [u64, u64, i32, C.c_double, u32, p, p, i32]),
         "hj3d_gen_exp4_ref": (st, [u32, u32, u32, u32, u32, p, p, C.POINTER(u64)]),
         "hj3d_runtime_info": (st, [C.c_char_p, u64]),
+        "hj3d_stream_copy": (st, [p, p, p, u64, u32, C.POINTER(C.c_double)]),
         "hj3d_comm_unique_id": (st, [p, C.c_char_p]),
         "hj3d_comm_init": (st, [p, C.c_char_p, i32, i32]),
         "hj3d_comm_destroy": (st, [p]),
@@ -390,9 +392,11 @@ class Context:
     def partition(self, rel: Rel, num_buckets: int, parts: int, out_pairs, counts, preds=None, stride=None):
         """Bucket-range partition of rel into (key, row) pairs per destination (stable); with
         preds, only the tuples passing the selection are partitioned (hj3d_partition_sel).
-        stride (>= rel's tuple count): the single-pass form for the probe side, order inside a
-        destination not kept, destination p's pairs at rows [p * stride, p * stride + counts[p]) of
-        out_pairs (hj3d_partition_strided)."""
+        stride: the single-pass form for the probe side, order inside a destination not kept,
+        destination p's pairs at rows [p * stride, p * stride + counts[p]) of out_pairs
+        (hj3d_partition_strided). counts[p] > stride means destination p spilled (its pairs past
+        the stride were not written): re-partition without stride (partition_stride(n, parts) is
+        the library's bounded stride; stride = rel's tuple count never spills)."""
         if stride is not None:
             if out_pairs.shape[0] < parts * stride:
                 raise ValueError("out_pairs holds fewer than parts * stride pairs")
@@ -436,6 +440,18 @@ class Context:
         if out:
             raise ValueError(f"{out} keys outside [0, {domain})")
         return c
+
+    def stream_copy_peak(self, dst, src, reps: int = 5) -> dict:
+        """The box's streaming-copy rate (hj3d_stream_copy: read + write bytes / launch time, the
+        best of six copy variants): SURVEY §8(d)'s same-run copy peak. dst, src: device tensors."""
+        nbytes = min(dst.numel() * dst.element_size(), src.numel() * src.element_size()) & ~15
+        out = (C.c_double * 3)()
+        self._check(lib().hj3d_stream_copy(self.h, C.c_void_p(dst.data_ptr()), C.c_void_p(src.data_ptr()),
+                                             nbytes, reps, out), "stream_copy")
+        v = int(out[2])
+        return {"copy_peak_GBs": out[0], "copy_median_GBs": out[1], "bytes_copied": nbytes,
+                "variant": f"{v % 100} workgroups/CU of 256 threads, 16-B {'non-temporal ' if v >= 100 else ''}"
+                           f"loads+stores, best of {reps} launches"}
 
     def gen_keys(self, tensor, key_word: int, row_base: int, n_keys: int, seed: int):
         """n_keys == 0: identity (k = global row id); else a seeded permutation of [0, n_keys)."""
@@ -514,6 +530,12 @@ def gen_exp4_ref(log2R: int, alpha: int, mult_a: int, beta: int, mult_b: int):
     if st != HJ3D_OK:
         raise Hj3dError(st, "hj3d_gen_exp4_ref: invalid arguments")
     return Sa[:card.value], Ta[:card.value]
+
+
+def partition_stride(n: int, parts: int) -> int:
+    """Bounded per-destination area of the single-pass exchange partitioner (hj3d_partition_stride):
+    mean + 8 sigma of the binomial destination count + 2 tiles, at most n."""
+    return int(lib().hj3d_partition_stride(n, parts))
 
 
 def part_range(num_buckets: int, parts: int, part: int):

@@ -86,16 +86,19 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
     are returned in exp1_plan's form. timing (a list): one dict of per-owner phase times (ms, the
     library's HIP-event timers) is appended per owner, plus {"owner": "partition", ...} first.
     single_pass: the probe side through the single-pass partitioner (hj3d_partition_strided, no
-    order inside an owner; parts x |probe| pairs of send buffer), as bench.py's strand does."""
+    order inside an owner) with the library's bounded stride (hj3d_partition_stride: ~|probe| pairs
+    of send buffer in all), as bench.py's strand does; a spill (an owner above its stride) falls back
+    to the stable partitioner."""
     import torch
-    from . import (T_BUILD, T_HIST, T_PARTITION, T_PROBE, T_PROBE_KERNEL, T_SCATTER, MASK64, part_range)
+    from . import (T_BUILD, T_HIST, T_PARTITION, T_PROBE, T_PROBE_KERNEL, T_SCATTER, MASK64, part_range,
+                   partition_stride)
     kind, bside, bkey, pkey, unique, unnest = EXP1_PLANS[plan]
     build = Rel(R if bside == "R" else S, key_word=bkey)
     probe = Rel(S if bside == "R" else R, key_word=pkey)
     dev = R.device
     bp = torch.empty((max(build.n, 1), 2), dtype=torch.int32, device=dev)
-    stride = probe.n if single_pass else None
-    pp = torch.empty((max(probe.n * (parts if single_pass else 1), 1), 2), dtype=torch.int32, device=dev)
+    stride = partition_stride(probe.n, parts) if single_pass else None
+    pp = torch.empty((max(stride * parts if single_pass else probe.n, 1), 2), dtype=torch.int32, device=dev)
     bc = torch.zeros(parts, dtype=torch.int64, device=dev)
     pc = torch.zeros(parts, dtype=torch.int64, device=dev)
     phases = {"build": T_BUILD, "probe": T_PROBE, "part_kernel": T_SCATTER, "split_kernel": T_HIST,
@@ -116,6 +119,10 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
     ctx.partition(build, nb, parts, bp, bc)
     tb = timers() if timing is not None else {}
     ctx.partition(probe, nb, parts, pp, pc, stride=stride)
+    if single_pass and max(pc.tolist()) > stride:  # spilled: the stable partitioner instead
+        single_pass, stride = False, None
+        pp = torch.empty((max(probe.n, 1), 2), dtype=torch.int32, device=dev)
+        ctx.partition(probe, nb, parts, pp, pc)
     if timing is not None:
         tp = timers()
         timing.append(dict(owner="partition", partition=tb.get("partition", 0.0) + tp.get("partition", 0.0),

@@ -260,6 +260,33 @@ def cpu_baseline_port(R_host, S_host, nb, reps):
     }
 
 
+def copy_peak(torch, ctx, dev, nbytes=1 << 30):
+    """the streaming-copy peak measured in this run (hj3d_stream_copy on the engine's
+    stream: 1 GiB read + 1 GiB written per launch, best of six variants x 5 launches), so the
+    roofline fractions against 8 TB/s can be read against what this box actually streams."""
+    try:
+        src = torch.empty(nbytes // 4, dtype=torch.int32, device=dev).fill_(1)
+        dst = torch.empty_like(src)
+        r = ctx.stream_copy_peak(dst, src, 5)
+        del src, dst
+        return r
+    except Exception as e:  # measurement only: the line still carries the 8 TB/s fractions
+        log(f"copy peak not measured: {e}")
+        return None
+
+
+def _with_copy_peak(roof, cp, keys=("achieved",)):
+    """Adds the same-run copy peak and the fractions of it to a roofline dict."""
+    if not cp:
+        roof["copy_peak_GBs"] = None
+        return
+    roof["copy_peak_GBs"] = cp["copy_peak_GBs"]
+    roof["copy_peak"] = cp
+    for k in keys:
+        if roof.get(k):
+            roof[f"{k}_frac_of_copy_peak" if k != "achieved" else "frac_of_copy_peak"] = roof[k] / cp["copy_peak_GBs"]
+
+
 def _events(torch, n):
     return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
@@ -395,16 +422,30 @@ def main():
         # [p * stride_c, ...) of that chunk's send buffer (stride_c = the chunk's tuple count); the
         # build side keeps the stable two-pass partitioner (its order fixes long chains' order)
         single = args.xpart == "single"
+        # stride_c = hj3d_partition_stride (mean + 8 sigma + 2 tiles per destination), so the send
+        # buffer is ~ the chunk's pairs, not world x chunk; a chunk whose counts show a spill (a
+        # destination above its stride: skewed keys) is re-partitioned by the stable partitioner
+        # into `spill` and sent back to back (the counts are the same, so no rank notices)
         if single:
-            xstride = [sb[c + 1] - sb[c] for c in range(C)]
+            xstride = [hj3d.partition_stride(sb[c + 1] - sb[c], world) for c in range(C)]
             sendP_c = [torch.empty((max(world * xstride[c], 1), 2), dtype=torch.int32, device=dev) for c in range(C)]
         else:
             xstride = [None] * C
             sendP = torch.empty((nP, 2), dtype=torch.int32, device=dev)
             sendP_c = [sendP[sb[c]:sb[c + 1]] for c in range(C)]
+        spill = {}
 
         def part_probe(c):
             ctx.partition(pRel_c[c], nb, world, sendP_c[c], cntP[c], stride=xstride[c])
+
+        def send_of(c, sc_c):
+            """(send buffer, stride) of chunk c once its counts are known on the host."""
+            if xstride[c] is None or max(sc_c) <= xstride[c]:
+                return sendP_c[c], xstride[c]
+            if c not in spill:
+                spill[c] = torch.empty((max(sb[c + 1] - sb[c], 1), 2), dtype=torch.int32, device=dev)
+            ctx.partition(pRel_c[c], nb, world, spill[c], cntP[c])
+            return spill[c], None
         # receive buffers sized from the exchanged counts of a sizing pass (partition + counts
         # all-to-all): the inputs do not change between steps, so neither do the receive totals
         ctx.partition(bRel, nb, world, sendB, cntB[0])
@@ -449,7 +490,8 @@ def main():
             scP, rcP = hdist.exchange_counts(cntP, recv_cap=recvP.shape[0])
             pend, roff = [], 0
             for c in range(C):
-                rS, work = hdist.exchange_pairs_async(sendP_c[c], scP[c], rcP[c], recvP[roff:], send_stride=xstride[c])
+                sbuf, sstride = send_of(c, scP[c])
+                rS, work = hdist.exchange_pairs_async(sbuf, scP[c], rcP[c], recvP[roff:], send_stride=sstride)
                 roff += rS.shape[0]
                 pend.append((rS, work))
             ooff = 0
@@ -684,8 +726,15 @@ def main():
         "verification": verify,
         "verified_bit_exact": verified,
     }
+    _with_copy_peak(line["roofline"], copy_peak(torch, ctx, dev))
+    pp = line["roofline"]["probe_phase"]
+    if line["roofline"].get("copy_peak_GBs"):
+        pp["frac_of_copy_peak"] = pp["achieved_GBs"] / line["roofline"]["copy_peak_GBs"]
     if world > 1:
         line["per_gpu"] = per_gpu
+    if sharded:
+        line["config"]["probe_send_pairs"] = sum(int(t.shape[0]) for t in sendP_c) if single else nP
+        line["config"]["probe_spilled_chunks"] = sorted(spill)
     line["cpu_baseline"] = None
     if world == 1 and not args.no_cpu_baseline and plan == "Csr":
         m = min(args.cpu_sample, nS)
@@ -914,6 +963,7 @@ def main_single_config(args):
             k: {"traffic": v, "fetch": pm["kernels"][k].get("fetch_bytes"), "write": pm["kernels"][k].get("write_bytes")}
             for k, v in tr.items() if k in ph_build + ph_probe}
         line["roofline"]["pmc_source"] = pm.get("_path")
+    _with_copy_peak(line["roofline"], copy_peak(torch, ctx, dev), keys=("achieved", "build_achieved"))
     if args.workload == "C" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_reference_nrs(max(nR // 10, 1), max(nS // 10, 1), args.theta,
                                                           args.cpu_reps)

@@ -263,13 +263,19 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
  * probe's counters are per tuple; the build side keeps hj3d_partition's stable order, which fixes
  * the chain order of buckets longer than the sorted build handles). The relation is read once
  * (hj3d_partition reads it twice); destination p's pairs go to out_pairs_dev + p * stride pairs
- * (stride >= rel->n, nparts <= 256), counts_dev[p] (device u64) = their number. preds / npred: an
- * optional selection as in hj3d_partition_sel (npred = 0: none). Send it with
+ * (stride >= 1, nparts <= 256; out_pairs_dev holds nparts * stride pairs), counts_dev[p] (device
+ * u64) = the number of tuples destined to p. Pairs past a destination's stride are NOT written
+ * (a spill): when any counts_dev[p] > stride the caller re-partitions with hj3d_partition (the
+ * counts are the same). hj3d_partition_stride gives a bounded stride that distinct keys spill with
+ * negligible probability (mean + 8 sigma of the binomial destination count + 2 tiles), so the send
+ * buffer is ~|rel| pairs instead of nparts x |rel| (stride = rel->n never spills). preds / npred:
+ * an optional selection as in hj3d_partition_sel (npred = 0: none). Send it with
  * hj3d_comm_exchange_strided (same stride). Replaces the same seam as hj3d_partition
  * (the reference itself runs on one node, main_experiment1.cc:623-848). */
 hj3d_status hj3d_partition_strided(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_sel_pred* preds, uint32_t npred,
                                    uint64_t num_buckets, uint32_t nparts, void* out_pairs_dev, uint64_t stride,
                                    void* counts_dev);
+uint64_t hj3d_partition_stride(uint64_t n, uint32_t nparts);
 /* Owned bucket range of part p: [lo, hi) with lo = ceil(p*NB/nparts). */
 void hj3d_part_range(uint64_t num_buckets, uint32_t nparts, uint32_t part, uint64_t* lo, uint64_t* hi);
 /* Slice geometry the packed unique probe takes for a chaining table of nb_local buckets holding
@@ -349,6 +355,15 @@ hj3d_status hj3d_key_bitmap(hj3d_ctx* ctx, const hj3d_rel* rel, uint64_t domain,
  * back to back at bitmaps_dev. */
 hj3d_status hj3d_bitmap_or_popcount(hj3d_ctx* ctx, const void* bitmaps_dev, uint32_t rows, uint64_t words,
                                     void* count_dev);
+
+/* ---- measurement: the box's streaming-copy peak, measured in the same run as the
+ * kernels whose roofline fractions are quoted. Replaces nothing of the reference. ----
+ * Synchronous: copies `bytes` (a multiple of 16) from src_dev to dst_dev `reps` times for each of
+ * six variants (plain / non-temporal 16-B vectors, 4 / 8 / 16 workgroups per CU), each launch timed
+ * by HIP events on the context stream; out[0] = the best rate in GB/s (read + write bytes), out[1] =
+ * the median launch of that variant, out[2] = its id (workgroups per CU, + 100 when non-temporal). */
+hj3d_status hj3d_stream_copy(hj3d_ctx* ctx, void* dst_dev, const void* src_dev, uint64_t bytes, uint32_t reps,
+                             double out[3]);
 
 /* ---- selection pushdown: AlgSelection / AlgDynSelection (algebra.hh:278-358) on the device ----
  * The predicate is a conjunction of `npred` (<= HJ3D_SEL_MAX) comparisons of one u32 tuple word

@@ -10,6 +10,9 @@ KiB; on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, s
 WRITE_SIZE is taken as reported (exact for 16-B/lane streaming stores; our 8-B/lane stores are
 uncalibrated, noted in the output). For each kernel only the launches of the largest grid are
 kept (the probe side S, not the build side R) and the median over those launches is reported.
+Of several template instantiations of one kernel the one LAUNCHED MOST OFTEN is reported under the
+plain name: that is the one the timed steps run (a checksum-folding verification launch runs
+once); the others stay under `instantiations`.
 
 usage: python scripts/pmc_summary.py TAG [--nR 10000000 --nS 100000000 --emit 1]
 """
@@ -63,14 +66,20 @@ def main():
     per = {}
     for (k, c), lst in vals.items():
         gmax = max(g for g, _ in lst)
-        v = statistics.median([x for g, x in lst if g == gmax])
-        per.setdefault(k, {"grid_size": gmax})[c] = v
-    # one entry per kernel name: the instantiation that moved the most bytes
-    kern = {}
+        sel = [x for g, x in lst if g == gmax]
+        d = per.setdefault(k, {"grid_size": gmax, "launches": 0})
+        d[c] = statistics.median(sel)
+        d["launches"] = max(d["launches"], len(sel))
+    # one entry per kernel name: the instantiation launched most often (the timed one)
+    kern, inst = {}, collections.defaultdict(dict)
     for k, d in per.items():
         base = k.split("<")[0]
-        if base not in kern or d.get("FETCH_SIZE", 0) > kern[base].get("FETCH_SIZE", 0):
+        inst[base][k] = {"launches": d["launches"], "grid_size": d["grid_size"]}
+        if base not in kern or d["launches"] > kern[base]["launches"]:
             kern[base] = dict(d, instantiation=k)
+    for base, d in kern.items():
+        if len(inst[base]) > 1:
+            d["instantiations"] = inst[base]
     for k, d in kern.items():
         if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
             d["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * 2

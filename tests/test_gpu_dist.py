@@ -224,7 +224,8 @@ def test_bench_dist_path_on_rccl_equals_reference(plan, tmp_path):
 
 def test_rccl_exchange_large_message(ctx, comm):
     """One chunk of more than 2^31 bytes (2^28 + 12345 pairs) arrives intact: the exchange moves
-    8-byte words in pieces (a 2e9-byte chunk of config D once came out corrupted as one message)."""
+    8-byte words in pieces of at most 2^28 bytes, the library default (a 2e9-byte chunk of config D
+    once came out corrupted as one message)."""
     import torch
     n = (1 << 28) + 12345
     send = torch.randint(-2**31, 2**31 - 1, (n, 2), dtype=torch.int32, device="cuda")

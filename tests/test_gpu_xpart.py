@@ -33,12 +33,12 @@ def _sorted_rows(a):
     return a[np.lexsort((a[:, 1], a[:, 0]))]
 
 
-def _compare(ctx, rel, n, nb, parts, preds=None):
+def _compare(ctx, rel, n, nb, parts, preds=None, stride=None):
     import torch
     stable = torch.empty((max(n, 1), 2), dtype=torch.int32, device="cuda")
     cs = torch.zeros(parts, dtype=torch.int64, device="cuda")
     ctx.partition(rel, nb, parts, stable, cs, preds=preds)
-    stride = n
+    stride = max(n, 1) if stride is None else stride
     single = torch.full((max(parts * stride, 1), 2), -1, dtype=torch.int32, device="cuda")
     cx = torch.full((parts,), 12345, dtype=torch.int64, device="cuda")  # the call zeroes its counts
     ctx.partition(rel, nb, parts, single, cx, preds=preds, stride=stride)
@@ -49,8 +49,14 @@ def _compare(ctx, rel, n, nb, parts, preds=None):
     off = 0
     for p in range(parts):
         exp = st[off:off + a[p]]
-        got = sg[p * stride:p * stride + a[p]]
-        assert (_sorted_rows(got) == _sorted_rows(exp)).all(), p
+        w = min(a[p], stride)
+        got = sg[p * stride:p * stride + w]
+        if w == a[p]:
+            assert (_sorted_rows(got) == _sorted_rows(exp)).all(), p
+        else:  # spilled: the area holds `stride` of the destination's pairs, each exactly once
+            e = {tuple(x) for x in _sorted_rows(exp).tolist()}
+            g = [tuple(x) for x in _sorted_rows(got).tolist()]
+            assert len(set(g)) == len(g) == stride and set(g) <= e, p
         # nothing past the destination's count was written
         if a[p] < stride:
             assert (sg[p * stride + a[p]:(p + 1) * stride] == 0xFFFFFFFF).all(), p
@@ -98,11 +104,36 @@ def test_single_pass_with_selection(ctx, parts):
     assert counts == [int((owner == d).sum()) for d in range(parts)]
 
 
-def test_single_pass_refuses_short_stride(ctx):
+@pytest.mark.parametrize("parts", [2, 8, 64])
+def test_single_pass_bounded_stride(ctx, parts):
+    """The library's bounded stride (hj3d_partition_stride: mean + 8 sigma + 2 tiles) holds every
+    destination of distinct keys: no spill, parts x stride pairs of send buffer instead of parts x n."""
+    import hj3d
+    n, nb = 4_000_037, 3_999_971
+    rng = np.random.default_rng(parts)
+    t = np.stack([rng.permutation(n).astype(np.uint32), np.arange(n, dtype=np.uint32)], axis=1)
+    stride = hj3d.partition_stride(n, parts)
+    assert stride < n and parts * stride < n + parts * 40_000
+    counts = _compare(ctx, hj3d.Rel(dev(t), key_word=0, row_word=1), n, nb, parts, stride=stride)
+    assert max(counts) <= stride and sum(counts) == n
+
+
+def test_single_pass_spill_reported_by_counts(ctx):
+    """A destination above its stride spills: its count still counts every tuple, exactly `stride`
+    of its pairs are written, nothing outside the areas (the caller then re-partitions)."""
+    import hj3d
+    _, Sa, _ = O.gen_exp1(1 << 16, 400_000, True, 1.0, 0)
+    t = np.stack([Sa, np.arange(len(Sa), dtype=np.uint32)], axis=1).astype(np.uint32)
+    stride = hj3d.partition_stride(len(t), 4)
+    counts = _compare(ctx, hj3d.Rel(dev(t), key_word=0, row_word=1), len(t), 1 << 16, 4, stride=stride)
+    assert max(counts) > stride and sum(counts) == len(t)
+
+
+def test_single_pass_refuses_zero_stride(ctx):
     import torch
     import hj3d
     t = np.zeros((100, 3), dtype=np.uint32)
     out = torch.empty((800, 2), dtype=torch.int32, device="cuda")
     cnt = torch.zeros(8, dtype=torch.int64, device="cuda")
     with pytest.raises(hj3d.Hj3dError):
-        ctx.partition(hj3d.Rel(dev(t), 1), 1000, 8, out, cnt, stride=99)
+        ctx.partition(hj3d.Rel(dev(t), 1), 1000, 8, out, cnt, stride=0)

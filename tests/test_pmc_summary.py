@@ -58,3 +58,33 @@ def test_pmc_bytes_per_probe_tuple(tmp_path, monkeypatch):
     assert r["kernels"]["k_rp_hist"]["bytes_per_probe_tuple"] == 2 * 1.0
     assert r["probe_strand_bytes_per_probe_tuple"] == (12 + 8) + (8 + 8) + (8 + 8)
     assert "k_rp_hist" not in r["probe_strand_kernels"]
+
+
+def test_pmc_summary_reports_the_timed_instantiation(tmp_path):
+    """Of two instantiations of k_pk_probe, the one launched most often (the timed <7, 1, false>)
+    is reported, not the once-run checksum launch that moves more bytes (round-3 verdict)."""
+    import csv
+    import json
+    import subprocess
+    import sys
+    tag = "unit_inst"
+    root = tmp_path / "repo"
+    d = root / "gpurun_out" / f"pmc_{tag}" / "p1"
+    d.mkdir(parents=True)
+    ns = "void hj3d::(anonymous namespace)::"
+    with open(d / "run_counter_collection.csv", "w", newline="") as fh:
+        w = csv.writer(fh)
+        w.writerow(["Kernel_Name", "Counter_Name", "Counter_Value", "Grid_Size"])
+        for _ in range(5):
+            w.writerow([ns + "k_pk_probe<7, 1, false>(int)", "FETCH_SIZE", 100.0, 1024])
+        w.writerow([ns + "k_pk_probe<7, 1, true>(int)", "FETCH_SIZE", 900.0, 1024])
+    (root / "scripts").mkdir()
+    (root / "profiles").mkdir()
+    (root / "scripts" / "pmc_summary.py").write_text(open(os.path.join(ROOT, "scripts", "pmc_summary.py")).read())
+    out = tmp_path / "o.json"
+    subprocess.run([sys.executable, str(root / "scripts" / "pmc_summary.py"), tag, "--out", str(out)],
+                   check=True, capture_output=True)
+    k = json.load(open(out))["kernels"]["k_pk_probe"]
+    assert k["instantiation"] == "k_pk_probe<7, 1, false>"
+    assert k["launches"] == 5 and k["FETCH_SIZE"] == 100.0
+    assert set(k["instantiations"]) == {"k_pk_probe<7, 1, false>", "k_pk_probe<7, 1, true>"}
