@@ -159,6 +159,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       ctx->pk_slice_max = uint32_t(value);
       return HJ3D_OK;
     case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_NESTED_PK: ctx->nested_pk = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);
@@ -294,25 +295,34 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   hipError_t e;
   if (t->desc.kind == HJ3D_CHAIN) {
     bool sorted = false;
+    t->path = "radix";
     e = (!ctx->force_direct && !ctx->pk_build && build->n >= (ctx->radix_min >> 4) && build->n > 0 &&
          t->nb_local >= 64)
             ? radix_build(ctx, t, *build, ctx->stream, &sorted)
             : hipErrorNotSupported;
     if (e == hipErrorNotSupported && build->n >= (ctx->radix_min >> 4)) {
+      t->path = "slices";
       e = pk_build(ctx, t, *build, ctx->stream);  // tables beyond the radix build's 2048 x 16384 buckets
       sorted = e == hipSuccess;
     }
-    if (e == hipErrorNotSupported) e = chain_build(ctx, t, *build, ctx->stream);
+    if (e == hipErrorNotSupported) {
+      t->path = "direct";
+      e = chain_build(ctx, t, *build, ctx->stream);
+    }
     if (e == hipSuccess && !sorted) e = sort_small_buckets(ctx, t, ctx->stream);
   } else {
+    t->path = "nested_radix";
     e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
                                                   : hipErrorNotSupported;
     bool agg = false;
     if (e == hipErrorNotSupported && !ctx->nested_sort) {
-      e = nested_build_agg(ctx, t, *build, ctx->stream);
+      e = nested_build_agg(ctx, t, *build, ctx->stream, &t->path);
       agg = e == hipSuccess;
     }
-    if (e == hipErrorNotSupported) e = nested_build(ctx, t, *build, ctx->stream);
+    if (e == hipErrorNotSupported) {
+      t->path = "nested_sort";
+      e = nested_build(ctx, t, *build, ctx->stream);
+    }
     // the partitioned probe sizes its LDS slices by the number of main records: counts read once
     // after the build (word 1 = main records; word 3 = the aggregation build's give-up flag)
     uint64_t hc[4] = {0, 0, 0, 0};
@@ -322,6 +332,7 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
     };
     if (e == hipSuccess) e = read_counts();
     if (e == hipSuccess && agg && uint32_t(hc[3]) != 0) {  // a key range too dense for the LDS table
+      t->path = "nested_sort";
       e = nested_build(ctx, t, *build, ctx->stream);
       if (e == hipSuccess) e = read_counts();
     }
@@ -330,6 +341,8 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");
 }
+
+const char* hj3d_table_build_path(const hj3d_table* t) { return t && t->built ? t->path : "none"; }
 
 hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
                               uint64_t* n_payload, uint64_t* n_sub) {

@@ -75,14 +75,6 @@ constexpr uint32_t kOvfFlag = 0x80000000u;
 // control words (u64) of one probe strand
 enum { kCtlNovf = 0, kCtlOut = 1, kCtlTicket = 2, kCtlOvfCursor = 3, kCtlNprobe = 4, kCtlWords = 8 };
 
-struct PkGeom {
-  FastDiv32 dnb, dw;  // / NB, / W
-  uint32_t nb, lo, nbl, W, P, qbits, qmask;
-  // hash of a packed pair in slice p
-  __device__ __forceinline__ uint32_t hash_of(uint32_t v, uint32_t p) const {
-    return (v & qmask) * nb + lo + p * W + (v >> qbits);
-  }
-};
 
 // Wave-aggregated append to the overflow list: pairs {h, row} (counted in ctl[kCtlNovf]).
 __device__ __forceinline__ void pk_ovf_append(bool me, uint2 e, uint2* __restrict__ ovf, uint64_t* ctl) {
@@ -1278,17 +1270,19 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
 }
 
 
-hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s) {
   hipError_t e;
   const uint32_t nbl = t->nb_local, nb = uint32_t(t->desc.num_buckets);
-  if (ctx->force_direct || nbl < 64 || r.n == 0 || r.n >= (1ull << 31)) return hipErrorNotSupported;
-  const uint32_t W = kPbW, P = (nbl + W - 1) / W;
+  if (nbl < 64 || r.n == 0 || r.n >= (1ull << 31) || W < 2) return hipErrorNotSupported;
+  const uint32_t P = (nbl + W - 1) / W;
   const uint32_t C = (P + kPkBlock - 1) / kPkBlock;
-  if ((C < 2 && !ctx->pk_build) || C > kSpMaxC) return hipErrorNotSupported;  // one level: the radix build's range
+  if (C > kSpMaxC) return hipErrorNotSupported;
   const uint32_t W1 = W * C, P1 = (nbl + W1 - 1) / W1;
   auto bits = [](uint64_t x) { uint32_t b = 0; while (x) { ++b; x >>= 1; } return b; };
   const uint32_t qbits = bits(0xFFFFFFFFull / nb);
-  if (qbits + bits(W1 - 1) > 32) return hipErrorNotSupported;
+  // the packed word holds the bucket inside the coarse range (and, after the split, inside the
+  // slice, whose width W must also fit, for the nested build's empty marker W << qbits)
+  if (qbits + bits(W1 - 1) > 32 || qbits + bits(W) > 32) return hipErrorNotSupported;
   const uint32_t ntiles = uint32_t((r.n + kPkTile - 1) / kPkTile);
   const uint32_t G = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
   auto capacity = [](double ex) {
@@ -1302,8 +1296,6 @@ hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t
   const uint64_t cap2 = capacity(double(r.n) / (double(S2) * P));
   const uint64_t nreg2 = uint64_t(S2) * P;
   if (nreg * cap >= (1ull << 31) || nreg2 * cap2 >= (1ull << 31)) return hipErrorNotSupported;
-  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
-  if ((e = t->ent.ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPHist].ensure(nreg * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
@@ -1340,24 +1332,51 @@ hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t
   else
     hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
                        counts, ovf, ctl, sr, kPkStage);
-  // (C = 1, forced: the split only regroups each slice's G regions into S2)
+  // (C = 1: the split only regroups each slice's G regions into S2)
   hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kSpBlock), 0, s, static_cast<const uint2*>(region),
                      static_cast<const uint32_t*>(counts), G, P1, uint32_t(cap), S2, pk, C, bits(C - 1), uint32_t(cap2),
                      fine, fcnt, ovf, ctl);
   hipLaunchKernelGGL(k_pk_slice_sums, dim3((P + 255) / 256), dim3(256), 0, s, static_cast<const uint32_t*>(fcnt), S2, P, ps);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = exclusive_scan_u32(ctx, ps, ps, P, s)) != hipSuccess) return e;
+  o->pk = pk;
+  o->P = P;
+  o->S2 = S2;
+  o->cap2 = uint32_t(cap2);
+  o->fine = fine;
+  o->fcnt = fcnt;
+  o->ps = ps;
+  return hipSuccess;
+}
+
+hipError_t pk_overflow_check(hj3d_ctx* ctx, hipStream_t s, uint64_t* novf) {
+  hipError_t e;
+  uint64_t* ctl = ctx->ctl.as<uint64_t>();
+  *novf = 0;
+  if ((e = hipMemcpyAsync(novf, ctl + kCtlNovf, sizeof(*novf), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(ctl, 0, kCtlWords * sizeof(uint64_t), s)) != hipSuccess) return e;
+  return hipStreamSynchronize(s);
+}
+
+hipError_t pk_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+  hipError_t e;
+  const uint32_t nbl = t->nb_local;
+  if (ctx->force_direct || nbl < 64 || r.n == 0 || r.n >= (1ull << 31)) return hipErrorNotSupported;
+  const uint32_t W = kPbW, P = (nbl + W - 1) / W;
+  const uint32_t C = (P + kPkBlock - 1) / kPkBlock;
+  if ((C < 2 && !ctx->pk_build) || C > kSpMaxC) return hipErrorNotSupported;  // one level: the radix build's range
+  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = t->ent.ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
+  PkSlices sl;
+  if ((e = pk_slices(ctx, t, r, W, &sl, s)) != hipSuccess) return e;
   const uint32_t g2 = P < uint32_t(ctx->num_cus) ? P : uint32_t(ctx->num_cus);
-  hipLaunchKernelGGL(k_pk_build, dim3(g2), dim3(kPkBlock), 0, s, static_cast<const uint2*>(fine),
-                     static_cast<const uint32_t*>(fcnt), S2, uint32_t(cap2), static_cast<const uint32_t*>(ps), pk,
+  hipLaunchKernelGGL(k_pk_build, dim3(g2), dim3(kPkBlock), 0, s, sl.fine, sl.fcnt, sl.S2, sl.cap2, sl.ps, sl.pk,
                      t->off.as<uint32_t>(), t->ent.as<uint2>());
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // pairs past a region's capacity (skewed keys) are not in the slices: then the direct build
   // runs instead. The control words go back to zero (the probes' invariant) either way.
   uint64_t novf = 0;
-  if ((e = hipMemcpyAsync(&novf, ctl + kCtlNovf, sizeof(novf), hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(ctl, 0, kCtlWords * sizeof(uint64_t), s)) != hipSuccess) return e;
-  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  if ((e = pk_overflow_check(ctx, s, &novf)) != hipSuccess) return e;
   if (novf) return hipErrorNotSupported;
   t->n_build = r.n;
   return hipSuccess;

@@ -84,6 +84,7 @@ struct hj3d_ctx {
   uint32_t pk_slice_max = 0;      // HJ3D_OPT_PK_SLICE: cap on the packed probe's slice width (0 = LDS-sized)
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
+  bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
@@ -113,6 +114,7 @@ struct hj3d_table {
   uint64_t n_build = 0;   // tuples in the last build (host-known)
   uint64_t n_mains = 0;   // nested: main records (distinct keys) of the last build (host-known)
   bool built = false;
+  const char* path = "none";  // which build made the table (hj3d_table_build_path)
   // chaining: off[nb_local+1] (u32 CSR offsets), ent[n] = {hash, row}
   // nested:   off[nb_local+1] over mains, main[d] = {hash, first_row, sub_off, sub_len},
   //           sub[n] = build rows grouped per key (first occurrence first, then row order)
@@ -273,6 +275,30 @@ struct PkPlan {
   uint32_t W = 0, P = 0, C = 1, W1 = 0, P1 = 0;
 };
 PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nb_local, uint64_t n_build);
+// Packed-pair geometry of P slices of W buckets: a pair of slice p carries v = (bucket in the slice)
+// << qbits | h / NB, from which the hash follows without a division (chain_pk.hip).
+struct PkGeom {
+  FastDiv32 dnb, dw;  // / NB, / W
+  uint32_t nb, lo, nbl, W, P, qbits, qmask;
+  // hash of a packed pair in slice p
+  __device__ __forceinline__ uint32_t hash_of(uint32_t v, uint32_t p) const {
+    return (v & qmask) * nb + lo + p * W + (v >> qbits);
+  }
+};
+// A relation partitioned into slices of W local buckets by the packed partitioner's two levels
+// (k_pk_part into coarse ranges, k_pk_split into slices): slice p's pairs {v, row} lie in S2 fine
+// regions fine[(s * P + p) * cap2 ...], fcnt[s * P + p] pairs each; ps[p] = exclusive scan of the
+// slices' totals (ps[P] = all pairs in the slices). Pairs that overflowed a region are not in any
+// slice: pk_overflow_check (synchronous) reports their number and restores the control words.
+struct PkSlices {
+  PkGeom pk{};
+  uint32_t P = 0, S2 = 0, cap2 = 0;
+  const uint2* fine = nullptr;
+  const uint32_t* fcnt = nullptr;
+  const uint32_t* ps = nullptr;
+};
+hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s);
+hipError_t pk_overflow_check(hj3d_ctx* ctx, hipStream_t s, uint64_t* novf);
 // The chaining build of tables beyond the radix build's range (> 2048 x 16384 buckets): R
 // partitioned by the packed partitioner's two levels into 8192-bucket slices, each built in LDS
 // (rows sorted inside buckets of <= 32). Synchronous (checks for region overflow);
@@ -286,7 +312,9 @@ hipError_t chain_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
 hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 // nested_agg.hip: the nested build by bucket-range partition + per-partition LDS aggregation.
 // hipErrorNotSupported when not applicable (small inputs / tables): use nested_build.
-hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
+// *path (optional): "nested_agg" or "nested_agg_slices" (the pk_slices form, > 2048 partitions).
+hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s,
+                            const char** path = nullptr);
 // nested_radix.hip: nested build from the radix-partitioned bucket CSR (large inputs);
 // hipErrorNotSupported when a bucket holds too many distinct keys (use nested_build).
 bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n);

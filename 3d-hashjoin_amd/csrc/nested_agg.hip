@@ -20,6 +20,12 @@
 //      the per-partition key counts).
 // Traffic: 12 B read (tuple) x 2 + 8 B write + 2 x 8 B read (pairs) + 4 B write (sub) per tuple,
 // + 16 B per distinct key (twice) + 4 B per bucket.
+// Tables of more than 2048 partitions (config D's 1e8-bucket Nrs table on one GPU, 2.5e7 and 5e7
+// buckets per rank at 4 and 2 GPUs) take step 1 from the packed partitioner's two levels instead
+// (pk_slices, chain_pk.hip: k_pk_part + k_pk_split, 12 + 8 + 8 + 8 B per tuple): each slice's pairs
+// lie in S2 = 16 fine regions, read as one stream, and the LDS table's key is the packed word
+// {bucket in the slice, h / NB} itself (unique per hash inside the slice: no modulo per pair). Pairs
+// that overflowed a region (skewed keys) set the give-up flag: the sort build then runs.
 #include "hj3d_internal.hpp"
 
 namespace hj3d {
@@ -74,16 +80,6 @@ __device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint3
   }
 }
 
-// kAggU pairs per thread of the partition's pairs from i0 (coalesced: pair i0 + u * BLOCK + tid)
-template <int BLOCK>
-__device__ __forceinline__ void load_batch(const uint2* __restrict__ pairs, uint32_t i0, uint32_t e1, uint2 (&v)[kAggU]) {
-#pragma unroll
-  for (int u = 0; u < kAggU; ++u) {
-    const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-    v[u] = i < e1 ? pairs[i] : make_uint2(0, 0);
-  }
-}
-
 __device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h, uint32_t cap) {
   uint32_t s = slot_of(h, cap);
   const uint32_t st = step_of(h, cap);
@@ -133,17 +129,25 @@ __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
 // main records in bucket order (i < its key count, with sub_off global); sub rows; dcount[p].
 // Dynamic LDS (agg_lds_bytes): tkey | tcnt | tmin [cap each] | bcnt [W] | wsum | nkeys, ovf.
 // SLOTS >= cap / BLOCK: table slots per thread in the per-slot loops.
+constexpr uint32_t kAggMaxS2 = 16;  // fine regions per slice (pk_slices)
 __host__ __device__ constexpr uint32_t agg_lds_words(uint32_t cap, uint32_t W, int block) {
-  return 3 * cap + W + uint32_t(block / 64) + 2;
+  return 3 * cap + W + uint32_t(block / 64) + 2 + kAggMaxS2 + 2;
 }
-template <int BLOCK, int SLOTS>
+// PK: the partition's pairs are slice p's fine regions (pk_slices), packed words as keys.
+struct NaggSrc {
+  const uint2* fine = nullptr;
+  const uint32_t* fcnt = nullptr;
+  uint32_t S2 = 0, cap2 = 0;
+  PkGeom pk{};
+};
+template <int BLOCK, int SLOTS, bool PK>
 __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                 FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                                 uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
                                                 uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
                                                 unsigned long long* __restrict__ maxlen,
                                                 uint32_t* __restrict__ fail, const uint32_t* __restrict__ order,
-                                                uint32_t cap) {
+                                                uint32_t cap, NaggSrc src) {
   extern __shared__ uint32_t agg_lds[];
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
@@ -152,18 +156,71 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
   uint32_t* wsum = bcnt + W;
   uint32_t& nkeys = wsum[BLOCK / kWave];
   uint32_t& ovf = wsum[BLOCK / kWave + 1];
+  uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
   const uint32_t limit = cap - BLOCK - 64;
-  const uint32_t p = order[blockIdx.x];
+  const uint32_t p = PK ? blockIdx.x : order[blockIdx.x];
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
-  const uint32_t e0 = ps[p], e1 = ps[p + 1];
+  const uint32_t e0 = ps[p], e1 = ps[p + 1], total = e1 - e0;
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  if constexpr (PK) {
+    if (threadIdx.x < 64) {
+      const uint32_t len = uint32_t(lane) < src.S2 ? src.fcnt[uint64_t(lane) * src.pk.P + p] : 0u;
+      uint32_t tot;
+      const uint32_t pre = wave_excl_scan(len, &tot);
+      if (uint32_t(lane) < src.S2) rstart[lane] = pre;
+      if (lane == 0) {
+        rstart[src.S2] = tot;
+        rstart[src.S2 + 1] = tot;
+      }
+    }
+    // (the first barrier below orders these writes before any read)
+  }
+  // bucket of a table key inside the partition, and the hash its main record carries
+  const auto lbk = [&](uint32_t x) __attribute__((always_inline)) {
+    if constexpr (PK) return x >> src.pk.qbits;
+    else return fm.mod(x) - lo - b0;
+  };
+  const auto hash_of = [&](uint32_t x) __attribute__((always_inline)) {
+    if constexpr (PK) return src.pk.hash_of(x, p);
+    else return x;
+  };
+  // PK: per-lane cursor over the S2 fine regions (a thread's item indices only grow inside a pass)
+  uint32_t cr = 0, nst = 0;
+  const uint2* rsrc = nullptr;
+  const auto restart = [&]() __attribute__((always_inline)) {
+    if constexpr (PK) {
+      cr = 0;
+      nst = rstart[1];
+      rsrc = src.fine + uint64_t(p) * src.cap2;
+    }
+  };
+  // kAggU pairs per thread of the partition's stream from f0 (coalesced: item f0 + u * BLOCK + tid)
+  const auto load = [&](uint32_t f0, uint2 (&v)[kAggU]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < kAggU; ++u) {
+      const uint32_t f = f0 + u * BLOCK + threadIdx.x;
+      if constexpr (PK) {
+        v[u] = make_uint2(0, 0);
+        if (f < total) {
+          while (f >= nst) {
+            ++cr;
+            nst = rstart[cr + 1];
+            rsrc = src.fine + (uint64_t(cr) * src.pk.P + p) * src.cap2;
+          }
+          v[u] = rsrc[f - rstart[cr]];
+        }
+      } else {
+        v[u] = f < total ? pairs[e0 + f] : make_uint2(0, 0);
+      }
+    }
+  };
   uint32_t mrun = 0, srun = 0, mxlen = 0;  // keys and rows of the finished rounds
   uint32_t c0 = 0, span = (nbs + kAggRounds - 1) / kAggRounds;
   while (c0 < nbs) {
     const uint32_t c1 = min(nbs, c0 + span);
-    // a hash that no key of this round has: its bucket lies outside [b0 + c0, b0 + c1)
-    const uint32_t empty = uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
+    // a key that no key of this round is: its bucket lies outside [b0 + c0, b0 + c1)
+    const uint32_t empty = PK ? (c1 << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
     for (uint32_t s = threadIdx.x; s < cap; s += BLOCK) {
       tkey[s] = empty;
       tcnt[s] = 0;
@@ -177,9 +234,10 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     __syncthreads();
     // ---- pass A: count and min row per key ----
     uint2 v[kAggU], nv[kAggU];
-    load_batch<BLOCK>(pairs, e0, e1, v);
-    for (uint32_t i0 = e0; i0 < e1; i0 += BLOCK * kAggU) {
-      if (i0 + BLOCK * kAggU < e1) load_batch<BLOCK>(pairs, i0 + BLOCK * kAggU, e1, nv);  // next batch in flight
+    restart();
+    load(0, v);
+    for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
+      if (i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
       // home slots of all items read together (one LDS latency for the batch); only items whose
       // key is not in its home slot walk the probe sequence
       bool act[kAggU];
@@ -187,8 +245,8 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-        const uint32_t lb = fm.mod(v[u].x) - lo - b0;
-        act[u] = i < e1 && lb >= c0 && lb < c1;
+        const uint32_t lb = lbk(v[u].x);
+        act[u] = i < total && lb >= c0 && lb < c1;
         k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
@@ -242,7 +300,7 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
       const uint32_t s = j * BLOCK + threadIdx.x;
-      rank[j] = s < cap && tcnt[s] ? atomicAdd(&bcnt[fm.mod(tkey[s]) - lo - b0 - c0], 1u) : 0u;
+      rank[j] = s < cap && tcnt[s] ? atomicAdd(&bcnt[lbk(tkey[s]) - c0], 1u) : 0u;
     }
     __syncthreads();
     const uint32_t nk = block_scan_lds<BLOCK>(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
@@ -261,9 +319,9 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
       const uint32_t s = j * BLOCK + threadIdx.x;
       if (cnt[j]) {
         const uint32_t h = tkey[s];
-        const uint32_t m = mrun + bcnt[fm.mod(h) - lo - b0 - c0] + rank[j];
+        const uint32_t m = mrun + bcnt[lbk(h) - c0] + rank[j];
         const uint32_t so = e0 + srun + tcnt[s];
-        mtmp[e0 + m] = make_uint4(h, tmin[s], so, cnt[j]);
+        mtmp[e0 + m] = make_uint4(hash_of(h), tmin[s], so, cnt[j]);
         tcnt[s] = so;  // sub cursor
         mxlen = max(mxlen, cnt[j]);
       }
@@ -271,16 +329,17 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     for (uint32_t k = threadIdx.x; k < c1 - c0; k += BLOCK) off[b0 + c0 + k] = mrun + bcnt[k];
     __syncthreads();
     // ---- pass B: rows into their keys' sub ranges ----
-    load_batch<BLOCK>(pairs, e0, e1, v);
-    for (uint32_t i0 = e0; i0 < e1; i0 += BLOCK * kAggU) {
-      if (i0 + BLOCK * kAggU < e1) load_batch<BLOCK>(pairs, i0 + BLOCK * kAggU, e1, nv);  // next batch in flight
+    restart();
+    load(0, v);
+    for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
+      if (i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
       bool act[kAggU];
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-        const uint32_t lb = fm.mod(v[u].x) - lo - b0;
-        act[u] = i < e1 && lb >= c0 && lb < c1;
+        const uint32_t lb = lbk(v[u].x);
+        act[u] = i < total && lb >= c0 && lb < c1;
         k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
@@ -375,6 +434,14 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
   for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[mbase[p] + i] = mtmp[ps[p] + i];
 }
 
+// pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
+// partitioner's control words back to zero, the invariant of the probes that share them
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail) {
+  if (threadIdx.x == 0 && ctl[0] != 0) *fail = 1u;  // ctl[0]: chain_pk.hip's overflow count
+  __syncthreads();
+  if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
+}
+
 __global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t P,
                               uint32_t nbl, uint32_t* __restrict__ off, uint64_t* __restrict__ counts) {
   if (reinterpret_cast<const uint32_t*>(counts + 3)[0]) return;  // fail flag
@@ -385,7 +452,7 @@ __global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* _
 
 }  // namespace
 
-hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s) {
+hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, const char** path) {
   const uint64_t n = r.n;
   const uint32_t nbl = t->nb_local;
   // small inputs and tables that one partition would cover (no free bucket for the LDS table's
@@ -406,29 +473,56 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   const uint32_t G = uint32_t(ctx->num_cus);
   uint32_t W = uint32_t((uint64_t(nbl) + 2 * G - 1) / (2 * G));
   W = W < 1024 ? 1024 : W > kAggW ? kAggW : W;
+  bool pk = false;  // more than 2048 partitions: the packed partitioner's slices (pk_slices)
   {
     const uint64_t P0 = (uint64_t(nbl) + W - 1) / W, P1 = (P0 + G - 1) / G * G;
     const uint64_t W1 = (uint64_t(nbl) + P1 - 1) / P1;
     if (HJ3D_NAGG_WAVES && P1 <= 2048 && W1 >= 1024) W = uint32_t(W1);
+    if (P0 > 2048 || ctx->nested_pk) {
+      pk = true;
+      W = uint32_t(W1 >= 1024 ? W1 : W);
+    }
   }
   const uint32_t P = (nbl + W - 1) / W;
-  // scratch: pairs (n uint2) | main records before compaction (n uint4) | starts, key counts
-  if ((e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
+  if (path) *path = pk ? "nested_agg_slices" : "nested_agg";
+  // scratch: pairs (n uint2; PK: the fine regions of pk_slices) | main records before compaction
+  // (n uint4) | starts, key counts, order
+  if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrPStart].ensure((3 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
-  uint2* pairs = ctx->scratch[kScrPairs].as<uint2>();
+  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
-  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
-  uint32_t* dcount = ps + P + 2;  // P + 1 (scanned in place into the main bases)
+  uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // P + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + P + 1;
-  uint32_t np = 0;
-  if ((e = radix_partition_pairs(ctx, t, r, W, pairs, ps, &np, s)) != hipSuccess) return e;
-  if (np != P) return hipErrorNotSupported;
   uint64_t* counts = t->counts.as<uint64_t>();
   uint32_t* off = t->off.as<uint32_t>();
-  if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
   uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
-  hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
+  if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+  const uint2* pairs = nullptr;
+  const uint32_t* ps = nullptr;
+  NaggSrc src;
+  if (pk) {
+    PkSlices sl;
+    if ((e = pk_slices(ctx, t, r, W, &sl, s)) != hipSuccess) return e;
+    if (sl.P != P) return hipErrorNotSupported;
+    src.fine = sl.fine;
+    src.fcnt = sl.fcnt;
+    src.S2 = sl.S2;
+    src.cap2 = sl.cap2;
+    src.pk = sl.pk;
+    ps = sl.ps;
+    // region overflows (skewed keys) -> the give-up flag; the control words back to zero
+    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), fail);
+  } else {
+    if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(P) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
+    uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
+    uint32_t np = 0;
+    if ((e = radix_partition_pairs(ctx, t, r, W, ctx->scratch[kScrPairs].as<uint2>(), pst, &np, s)) != hipSuccess)
+      return e;
+    if (np != P) return hipErrorNotSupported;
+    pairs = ctx->scratch[kScrPairs].as<uint2>();
+    ps = pst;
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
+  }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
   // workgroups per CU when the LDS fits twice (config E), else one 1024-thread one.
@@ -441,27 +535,29 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   };
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nagg<512, 12>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
-      return e;
-    if ((e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_nagg<1024, 10>),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess)
-      return e;
+    for (const void* k : {reinterpret_cast<const void*>(&k_nagg<512, 12, false>),
+                          reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
+                          reinterpret_cast<const void*>(&k_nagg<1024, 10, true>)})
+      if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
     lds_attr = true;
   }
   const uint32_t want = uint32_t(1.5 * W) + 512 + 64;  // the 512-thread form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
-  if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, 512) * 4 <= 81920) {
+  const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
+  auto* mx = reinterpret_cast<unsigned long long*>(counts + 2);
+  if (!pk && HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, 512) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, 512) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg<512, 12>), dim3(P), dim3(512), lds, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,
-                       uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
-                       reinterpret_cast<unsigned long long*>(counts + 2), fail, order, cap512);
+    hipLaunchKernelGGL((k_nagg<512, 12, false>), dim3(P), dim3(512), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
+                       mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap512, src);
   } else {
     const uint32_t cap = kAggCapMax;
     const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg<1024, 10>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo),
-                       nbl, uint32_t(t->desc.num_buckets), W, off, mtmp, t->sub.as<uint32_t>(), dcount,
-                       reinterpret_cast<unsigned long long*>(counts + 2), fail, order, cap);
+    if (pk)
+      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
+                         mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap, src);
+    else
+      hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
+                         mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap, src);
   }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // and the caller, which reads the counts once after the build, runs the sort build instead

@@ -27,7 +27,7 @@ PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
 OPT_PROBE_ITEMS = 7
-OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD = 8, 9, 10
+OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK = 8, 9, 10, 11
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -114,6 +114,7 @@ def lib():
         "hj3d_table_reserve": (st, [p, p, u64]),
         "hj3d_table_clear": (st, [p, p]),
         "hj3d_build": (st, [p, p, R]),
+        "hj3d_table_build_path": (C.c_char_p, [p]),
         "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
         "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe": (st, [p, p, R, u32, p, u64]),
@@ -383,6 +384,11 @@ class Context:
     def pk_build(self, on: bool = True):
         """Test hook: chaining builds take the two-level slice build (pk_build) whenever it applies."""
         self.set_option(OPT_PK_BUILD, int(on))
+
+    def nested_pk(self, on: bool = True):
+        """Nested aggregation builds always on the packed partitioner's slices (the form tables of
+        more than 2048 partitions take; tests)."""
+        self.set_option(OPT_NESTED_PK, int(on))
 
     def sel_unfused(self, on: bool = True):
         """A/B switch: hj3d_probe_sel selects first instead of fusing into the partitioner."""
@@ -658,6 +664,10 @@ class Table:
     def clear(self):
         self.ctx._check(lib().hj3d_table_clear(self.ctx.h, self.h), "hj3d_table_clear")
 
+    def build_path(self) -> str:
+        """Which build made the table (hj3d_table_build_path)."""
+        return lib().hj3d_table_build_path(self.h).decode()
+
     def stats(self) -> dict:
         s = _Stats()
         self.ctx._check(lib().hj3d_table_stats(self.ctx.h, self.h, C.byref(s)), "hj3d_table_stats")
@@ -676,4 +686,4 @@ class Table:
 
 
 from .plans import (EXP1_PLANS, exp1_plan, exp1_plan_sharded, exp1_relations_ref, exp4_plan,  # noqa: E402,F401
-                    exp4_relations_ref, merge_shard_stats, num_buckets_exp1)
+                    exp4_relations_ref, merge_shard_stats, num_buckets_exp1, num_distinct_sharded)

@@ -167,6 +167,32 @@ def exp1_plan_sharded(ctx: Context, plan: str, R, S, nb: int, parts: int, out=No
     return res
 
 
+def num_distinct_sharded(ctx: Context, rel: Rel, domain: int, parts: int) -> int:
+    """The distributed #dv pre-pass of SURVEY §8(e) step 1 (hj3d.dist.num_distinct) emulated on ONE
+    device: `parts` ranks each hold a contiguous 1/parts of rel and set the bits of their keys in a
+    bitmap over [0, domain) (hj3d_key_bitmap); rank r then receives slice r of every rank's bitmap
+    (the all-to-all), ORs the `parts` slices and popcounts them (hj3d_bitmap_or_popcount), and the
+    per-rank counts add up. Equals the single-device count; NB = #dv(S.a) of the Nrs / NrsNU plans
+    (main_experiment1.cc:453-454)."""
+    import torch
+    words = (domain + 31) // 32
+    words = (words + parts - 1) // parts * parts
+    dev = rel.tensor.device
+    bm = torch.zeros((parts, words), dtype=torch.int32, device=dev)
+    outside = torch.zeros(1, dtype=torch.int64, device=dev)
+    for r in range(parts):
+        lo, hi = rel.n * r // parts, rel.n * (r + 1) // parts
+        ctx.key_bitmap(Rel(rel.tensor[lo:hi], key_word=rel.c.key_off // 4), domain, bm[r], outside)
+    per = words // parts
+    cnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    for r in range(parts):
+        ctx.bitmap_or_popcount(bm[:, r * per:(r + 1) * per].contiguous(), cnt)
+    ctx.sync()
+    if int(outside.item()):
+        raise ValueError(f"{int(outside.item())} keys outside [0, {domain})")
+    return int(cnt.item())
+
+
 def exp1_relations_ref(nR: int, nS: int, skew: bool = False, theta: float = 1.0, t: int = 0, device="cuda"):
     """The reference's experiment-1 relations R {k,0,0}, S {i,a,0} (main_experiment1.cc:415-457,
     495-515) from the bit-exact generator (hj3d_gen_exp1_ref), as (n, 3) int32 device tensors:

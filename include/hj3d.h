@@ -177,7 +177,12 @@ enum {
    * radix build's range (R through the packed partitioner's two levels into 8192-bucket slices,
    * each built in LDS; synchronous, region overflow falls back to the direct build) whenever it
    * applies, not only above 2048 x 16384 buckets (tests). */
-  HJ3D_OPT_PK_BUILD = 10
+  HJ3D_OPT_PK_BUILD = 10,
+  /* HJ3D_OPT_NESTED_PK (0/1, default 0): the nested aggregation build partitions by the packed
+   * partitioner's slices (k_pk_part + k_pk_split, the form tables of more than 2048 partitions take,
+   * e.g. config D's 1e8-bucket Nrs table) whenever it applies, not only above 2048 partitions
+   * (tests). Region overflow (skewed keys) falls back to the sort build. */
+  HJ3D_OPT_NESTED_PK = 11
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
@@ -226,6 +231,11 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
  * order (the reference's order follows from first_row and the rows). */
 hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
                               uint64_t* n_payload, uint64_t* n_sub);
+/* Which build made the table's current content (diagnostic, static string): chaining "radix",
+ * "slices" (pk_slices, tables beyond the radix build's range) or "direct"; nested "nested_agg",
+ * "nested_agg_slices" (more than 2048 partitions), "nested_sort" or "nested_radix"; "none" before a
+ * build. Replaces nothing of the reference (which has one insert path). */
+const char* hj3d_table_build_path(const hj3d_table* t);
 /* Synchronous statistics (makeStatistics). */
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out);
 /* Number of tuples / distinct keys currently stored (synchronous). */

@@ -163,7 +163,8 @@ def test_nested_agg_build_vs_oracle(ctx, nb, zipf):
     distinct keys per bucket (at 50 it gives up and the sort build replaces the table after the
     fact; at 14 it splits every partition into several rounds), uniform and Zipf(1.0)
     duplicates (hot keys aggregated per wave): counters, output checksums and statistics equal
-    the oracle's, and equal the LSD key-sort build's."""
+    the oracle's, and equal the LSD key-sort build's and those of the aggregation build on the
+    packed partitioner's slices (HJ3D_OPT_NESTED_PK: the form of tables above 2048 partitions)."""
     import hj3d
     rng = np.random.default_rng(nb + zipf)
     nR, nS = 100_000, 400_000
@@ -174,16 +175,25 @@ def test_nested_agg_build_vs_oracle(ctx, nb, zipf):
     ctx.radix_min(0)
     try:
         for plan, e in (("Nsr", O.nested_plan(R, 0, S, 1, nb, True)), ("Nrs", O.nested_plan(S, 1, R, 0, nb, True))):
-            for sort in (False, True):
-                ctx.nested_sort(sort)
-                got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb)
+            for mode in ("agg", "slices", "sort"):
+                ctx.nested_sort(mode == "sort")
+                ctx.nested_pk(mode == "slices")
+                t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+                got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb, table=t)
+                path = t.build_path()
+                t.close()
                 assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
-                    (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), (plan, sort)
-                assert got["out"] == e.out, (plan, sort)
-                assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, (plan, sort)
+                    (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), (plan, mode, path)
+                assert got["out"] == e.out, (plan, mode, path)
+                assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, (plan, mode)
+                # the packed-slice form really ran where nothing sends it to the sort build (~50
+                # keys per bucket give up; Zipf S.a overflows the slices' regions)
+                if mode == "slices" and nb >= 20000 and not (zipf and plan == "Nrs"):
+                    assert path == "nested_agg_slices", (plan, path)
     finally:
         ctx.radix_min(1 << 20)
         ctx.nested_sort(False)
+        ctx.nested_pk(False)
 
 
 @pytest.mark.parametrize("path", ["default", "partitioned"])
