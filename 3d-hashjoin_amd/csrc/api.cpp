@@ -303,6 +303,10 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
     if (e == hipErrorNotSupported && build->n >= (ctx->radix_min >> 4)) {
       t->path = "slices";
       e = pk_build(ctx, t, *build, ctx->stream);  // tables beyond the radix build's 2048 x 16384 buckets
+      if (e == hipErrorOutOfMemory) {  // its region scratch did not fit: the direct build needs far less
+        (void)hipGetLastError();
+        e = hipErrorNotSupported;
+      }
       sorted = e == hipSuccess;
     }
     if (e == hipErrorNotSupported) {
@@ -317,6 +321,10 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
     bool agg = false;
     if (e == hipErrorNotSupported && !ctx->nested_sort) {
       e = nested_build_agg(ctx, t, *build, ctx->stream, &t->path);
+      if (e == hipErrorOutOfMemory) {  // partition / slice scratch did not fit: the sort build
+        (void)hipGetLastError();
+        e = hipErrorNotSupported;
+      }
       agg = e == hipSuccess;
     }
     if (e == hipErrorNotSupported) {

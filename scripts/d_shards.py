@@ -11,7 +11,7 @@ bytes as bench.py counts them for a received-pair probe side: k_pk_part 8 + 8 B 
 k_pk_probe 8 + 8 B per pair + the table slices once), and the exchange partitioner's time.
 Per-rank compute, exchange not included: NOT a scaling number.
 
-Usage: python scripts/d_shards.py [--parts 8] [--plan Csr] [--reps 3] [--nR 1e8 --nS 1e9]
+Usage: python scripts/d_shards.py [--parts 8] [--plan Csr|Nsr|Nrs|NrsNU] [--reps 3] [--nR 1e8 --nS 1e9]
 """
 import argparse
 import json
@@ -27,7 +27,7 @@ PEAK = 8000.0  # GB/s
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--parts", type=int, default=8)
-    ap.add_argument("--plan", default="Csr", choices=["Csr", "Nsr"])
+    ap.add_argument("--plan", default="Csr", choices=["Csr", "Nsr", "Nrs", "NrsNU"])
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--nR", type=float, default=1e8)
     ap.add_argument("--nS", type=float, default=1e9)
@@ -41,8 +41,10 @@ def main():
     R, S = hj3d.exp1_relations_ref(nR, nS)
     gen_s = time.perf_counter() - t0
     ctx = hj3d.Context(0)
-    nb = hj3d.num_buckets_exp1(a.plan, nR, 0, 1)
-    out = torch.empty((nS, 2), dtype=torch.int32, device="cuda") if a.plan == "Csr" else None
+    # NB of the plans built on S.a: #dv(S.a) by the distributed pre-pass (per-rank bitmaps, OR-merge)
+    dv = hj3d.num_distinct_sharded(ctx, hj3d.Rel(S, key_word=1), nR, a.parts) if a.plan.startswith("Nrs") else 0
+    nb = hj3d.num_buckets_exp1(a.plan, nR, dv, 1)
+    out = torch.empty((nS, 2), dtype=torch.int32, device="cuda") if a.plan in ("Csr", "Nrs") else None
     sp = a.xpart == "single"
     hj3d.exp1_plan_sharded(ctx, a.plan, R, S, nb, a.parts, out=out, stats=False, checksum=False,
                            single_pass=sp)  # warm-up
@@ -88,7 +90,7 @@ def main():
         "what": f"config D {a.parts}-owner split emulated on one GPU, plan {a.plan}: per-rank compute at the "
                 f"{a.parts}-GPU geometry, owners run one after another; exchange (xGMI) NOT included; not a "
                 "scaling number",
-        "nR": nR, "nS": nS, "num_buckets": nb, "reps": a.reps, "input_generation_s": gen_s,
+        "nR": nR, "nS": nS, "num_buckets": nb, "num_dv_Sa": dv or None, "reps": a.reps, "input_generation_s": gen_s,
         "exchange_partition_ms_both_relations": part_ms,
         "exchange_partition_frac": ((nR + nS) * 20) / (part_ms * 1e-3) / 1e9 / PEAK if part_ms else None,
         "exchange_partitioner_probe_side": ("single-pass hj3d_partition_strided" if sp else

@@ -4,8 +4,9 @@
 #   b  the default bench line (as the driver runs it), its rocprofv3 kernel stats, PMC passes on it
 #   c  configs C and E: bench line, rocprofv3 kernel stats, PMC passes (HBM traffic per phase)
 #   d  config D on one GPU (Csr and the non-unique 3D plan Nrs): bench line + kernel stats
-#   s  the 2-, 4- and 8-owner splits of config D (scripts/d_shards.py) with kernel stats and the HBM
-#      bytes per probe tuple of the 8-owner split (FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_bytes.py)
+#   s  the 8-, 4- and 2-owner splits of config D (scripts/d_shards.py, Csr) with kernel stats, the HBM
+#      bytes per probe tuple of the 8-owner split (FETCH_SIZE / WRITE_SIZE passes, scripts/pmc_bytes.py),
+#      and the 8-owner split of the non-unique 3D plan Nrs
 #   r  the RCCL message-size sweep (scripts/rccl_limits.sh; needs the commdiag variant library)
 # Output under gpurun_out/ (copied to profiles/ by hand). Every GPU step has its own time limit;
 # the first failing step ends the call.
@@ -65,9 +66,12 @@ fi
 if [[ $PART == *s* ]]; then
   for o in 8 4 2; do
     step d_shards $o owners
-    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/${TAG}_Dshards$o -o run --output-format csv -- python3 scripts/d_shards.py --owners $o > gpurun_out/${TAG}_D_shards$o.json 2> gpurun_out/${TAG}_D_shards$o.err || { tail -5 gpurun_out/${TAG}_D_shards$o.err; exit 1; }
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/${TAG}_Dshards$o -o run --output-format csv -- python3 scripts/d_shards.py --parts $o > gpurun_out/${TAG}_D_shards$o.json 2> gpurun_out/${TAG}_D_shards$o.err || { tail -5 gpurun_out/${TAG}_D_shards$o.err; exit 1; }
     tail -c 600 gpurun_out/${TAG}_D_shards$o.json
   done
+  step d_shards 8 owners Nrs
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/${TAG}_Dshards8_Nrs -o run --output-format csv -- python3 scripts/d_shards.py --parts 8 --plan Nrs --reps 2 > gpurun_out/${TAG}_D_shards8_Nrs.json 2> gpurun_out/${TAG}_D_shards8_Nrs.err || { tail -5 gpurun_out/${TAG}_D_shards8_Nrs.err; exit 1; }
+  tail -c 600 gpurun_out/${TAG}_D_shards8_Nrs.json
   step pmc d_shards
   i=0
   for c in FETCH_SIZE WRITE_SIZE; do
