@@ -60,3 +60,26 @@ def test_single_hip_runtime_mapped():
     info = hj3d.runtime_info()
     assert "hip mapped=1" in info, info
     assert "libamdhip64" in info, info
+
+
+@pytest.mark.parametrize("n,parts", [(0, 8), (1, 8), (1000, 8), (25_000_000, 8), (250_000_000, 8), (10**9, 2),
+                                     (10**8, 256), (12345, 1)])
+def test_partition_stride_bounds(n, parts):
+    """hj3d_partition_stride (host-only): at least the mean destination count plus 8 sigma (distinct
+    keys spill with negligible probability), at most n (stride n never spills), and for large
+    inputs about n / parts, so parts x stride pairs of send buffer stay near n."""
+    import math
+    s = hj3d.partition_stride(n, parts)
+    assert s <= n
+    if parts == 1:
+        assert s == n
+        return
+    m = n / parts
+    assert s >= min(n, m + 8 * math.sqrt(m * (1 - 1 / parts)))
+    if n >= 10**7:
+        assert parts * s < 1.01 * n + parts * 20_000
+
+
+def test_table_build_path_before_build():
+    """hj3d_table_build_path is "none" for a null or unbuilt table (no device needed)."""
+    assert hj3d.lib().hj3d_table_build_path(None) == b"none"
