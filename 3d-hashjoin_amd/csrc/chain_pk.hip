@@ -1169,7 +1169,10 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   if (nreg * cap >= (1ull << 31)) return hipErrorNotSupported;
   // second level: S2 workgroups per coarse range, each writing one fine region per slice
   const uint32_t S2 = two ? (G < 16u ? G : 16u) : 0u;
-  const uint64_t cap2 = two ? capacity(double(r.n) / (double(S2) * pl.P)) : 0;
+  // a fine region gathers the pass-1 regions of ceil(G / S2) workgroups at most (G need not be a
+  // multiple of S2): its expected pairs are that many workgroups' share of the slice
+  const double per_gp = double(per_g < r.n ? per_g : r.n) / pl.P;
+  const uint64_t cap2 = two ? capacity(per_gp * double((G + S2 - 1) / S2)) : 0;
   const uint64_t nreg2 = uint64_t(S2) * pl.P;
   if (two && nreg2 * cap2 >= (1ull << 31)) return hipErrorNotSupported;
   if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;
@@ -1293,7 +1296,10 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   const uint64_t cap = capacity(double(per_g < r.n ? per_g : r.n) / P1);
   const uint64_t nreg = uint64_t(G) * P1;
   const uint32_t S2 = G < 16u ? G : 16u;
-  const uint64_t cap2 = capacity(double(r.n) / (double(S2) * P));
+  // a fine region gathers the pass-1 regions of ceil(G / S2) workgroups at most (G need not be a
+  // multiple of S2): its expected pairs are that many workgroups' share of the slice
+  const double per_gp = double(per_g < r.n ? per_g : r.n) / P;
+  const uint64_t cap2 = capacity(per_gp * double((G + S2 - 1) / S2));
   const uint64_t nreg2 = uint64_t(S2) * P;
   if (nreg * cap >= (1ull << 31) || nreg2 * cap2 >= (1ull << 31)) return hipErrorNotSupported;
   if ((e = ctx->scratch[kScrPairs].ensure(nreg * cap * sizeof(uint2))) != hipSuccess) return e;

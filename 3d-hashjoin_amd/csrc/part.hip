@@ -99,7 +99,13 @@ __global__ void k_part_counts(const uint32_t* __restrict__ offs, uint32_t ntiles
 #ifndef HJ3D_XP_NT
 #define HJ3D_XP_NT 1  // pairs stored non-temporal (0: plain; A/B)
 #endif
-constexpr int kXpBlock = 1024;
+#ifndef HJ3D_XP_BLOCK
+#define HJ3D_XP_BLOCK 1024  // threads per workgroup (A/B: 512 with two workgroups per CU)
+#endif
+#ifndef HJ3D_XP_WGS
+#define HJ3D_XP_WGS 1  // persistent workgroups per CU
+#endif
+constexpr int kXpBlock = HJ3D_XP_BLOCK;
 constexpr int kXpRounds = HJ3D_XP_ROUNDS;
 constexpr int kXpTile = kXpBlock * kXpRounds;  // rank inside the tile: < 2^16
 constexpr int kXpMaxParts = 256;
@@ -672,7 +678,7 @@ hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint
   if ((e = hipMemsetAsync(counts, 0, parts * sizeof(uint64_t), s)) != hipSuccess) return e;
   if (r.n == 0) return hipSuccess;
   const uint64_t ntiles = (r.n + kXpTile - 1) / kXpTile;
-  const uint64_t want = uint64_t(ctx->num_cus);  // one 1024-thread workgroup per CU
+  const uint64_t want = uint64_t(ctx->num_cus) * HJ3D_XP_WGS;  // persistent: HJ3D_XP_WGS workgroups per CU
   const unsigned grid = unsigned(ntiles < want ? ntiles : want);
   uint32_t pbits = 0;
   while ((1u << pbits) < parts) ++pbits;
