@@ -41,9 +41,20 @@ constexpr uint32_t kAggCapMax = 10223;
 // race past the test, so the table never fills and every probe sequence ends
 constexpr uint32_t kAggRounds = 1;  // initial rounds per partition (2, 3: slower under Zipf, pairs re-read)
 constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
-constexpr int kAggU = 8;             // pairs per thread and step (the next step's in flight)
+#ifndef HJ3D_NAGG_U
+#define HJ3D_NAGG_U 8
+#endif
+constexpr int kAggU = HJ3D_NAGG_U;   // pairs per thread and step (the next step's in flight)
 #ifndef HJ3D_NAGG_SMALL
 #define HJ3D_NAGG_SMALL 1  // small partitions: two 512-thread workgroups per CU with a smaller table (0: A/B)
+#endif
+#ifndef HJ3D_NAGG_SB
+#define HJ3D_NAGG_SB 512  // threads of the small-partition form (A/B: 256, four workgroups per CU)
+#endif
+constexpr int kSmallBlock = HJ3D_NAGG_SB;
+constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap <= 6144)
+#ifndef HJ3D_NAGG_PER_CU
+#define HJ3D_NAGG_PER_CU 2  // target partitions per CU when the table is small (A/B: 4 with 256 threads)
 #endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
@@ -471,7 +482,7 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   // time, latency-bound, so a last wave of a few partitions costs as long as a full one): config C
   // 9.6M buckets -> 1792 partitions of 5357 (7 waves) instead of 1563 of 6144 (6.1 waves, run as 7).
   const uint32_t G = uint32_t(ctx->num_cus);
-  uint32_t W = uint32_t((uint64_t(nbl) + 2 * G - 1) / (2 * G));
+  uint32_t W = uint32_t((uint64_t(nbl) + HJ3D_NAGG_PER_CU * G - 1) / (HJ3D_NAGG_PER_CU * G));
   W = W < 1024 ? 1024 : W > kAggW ? kAggW : W;
   bool pk = false;  // more than 2048 partitions: the packed partitioner's slices (pk_slices)
   {
@@ -535,19 +546,19 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   };
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
-    for (const void* k : {reinterpret_cast<const void*>(&k_nagg<512, 12, false>),
+    for (const void* k : {reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, true>)})
       if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
     lds_attr = true;
   }
-  const uint32_t want = uint32_t(1.5 * W) + 512 + 64;  // the 512-thread form's insert slack
+  const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
   auto* mx = reinterpret_cast<unsigned long long*>(counts + 2);
-  if (!pk && HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, 512) * 4 <= 81920) {
-    const size_t lds = agg_lds_words(cap512, W, 512) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg<512, 12, false>), dim3(P), dim3(512), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
+  if (!pk && HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
+    const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(P), dim3(kSmallBlock), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
                        mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap512, src);
   } else {
     const uint32_t cap = kAggCapMax;
