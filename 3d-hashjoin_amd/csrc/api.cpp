@@ -254,6 +254,11 @@ hj3d_status hj3d_table_create(hj3d_ctx* ctx, const hj3d_table_desc* desc, hj3d_t
 
 void hj3d_table_destroy(hj3d_table* t) {
   if (!t) return;
+  if (t->hc_ev) {
+    (void)hipEventSynchronize(t->hc_ev);  // the counts copy into t->hc has landed
+    (void)hipEventDestroy(t->hc_ev);
+  }
+  if (t->hc) (void)hipHostFree(t->hc);
   t->off.release();
   t->ent.release();
   t->main.release();
@@ -280,6 +285,7 @@ hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build)
 
 hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
   if (!ctx || !t) return HJ3D_EINVAL;
+  t->pending = false;
   hipError_t e = hipMemsetAsync(t->off.p, 0, (uint64_t(t->nb_local) + 1) * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(t->counts.p, 0, 4 * sizeof(uint64_t), ctx->stream);
   t->n_build = 0;
@@ -293,6 +299,7 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
+  t->pending = false;  // a build in flight for the old content is replaced (its copy stays stream-ordered)
   if (t->desc.kind == HJ3D_CHAIN) {
     bool sorted = false;
     t->path = "radix";
@@ -331,33 +338,70 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
       t->path = "nested_sort";
       e = nested_build(ctx, t, *build, ctx->stream);
     }
-    // the partitioned probe sizes its LDS slices by the number of main records: counts read once
-    // after the build (word 1 = main records; word 3 = the aggregation build's give-up flag)
-    uint64_t hc[4] = {0, 0, 0, 0};
-    auto read_counts = [&]() {
-      hipError_t x = hipMemcpyAsync(hc, t->counts.p, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream);
-      return x == hipSuccess ? hipStreamSynchronize(ctx->stream) : x;
-    };
-    if (e == hipSuccess) e = read_counts();
-    if (e == hipSuccess && agg && uint32_t(hc[3]) != 0) {  // a key range too dense for the LDS table
-      t->path = "nested_sort";
-      e = nested_build(ctx, t, *build, ctx->stream);
-      if (e == hipSuccess) e = read_counts();
+    // the partitioned probe sizes its LDS slices by the number of main records: the counts (word 1
+    // = main records; word 3 = the aggregation build's give-up flag) travel to pinned host memory
+    // behind the build and are read at the table's next use (table_resolve), so consecutive builds
+    // (experiment 4's two tables) do not wait for each other
+    if (e == hipSuccess && !t->hc) {
+      e = hipHostMalloc(reinterpret_cast<void**>(&t->hc), 4 * sizeof(uint64_t), hipHostMallocDefault);
+      if (e == hipSuccess) e = hipEventCreateWithFlags(&t->hc_ev, hipEventDisableTiming);
     }
-    t->n_mains = e == hipSuccess ? hc[1] : 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(t->hc, t->counts.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipEventRecord(t->hc_ev, ctx->stream);
+    t->pending = e == hipSuccess;
+    t->pending_agg = agg;
+    t->pending_rel = *build;
+    t->pending_ctx = ctx;
+    t->n_mains = 0;
   }
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");
 }
 
-const char* hj3d_table_build_path(const hj3d_table* t) { return t && t->built ? t->path : "none"; }
+}  // extern "C"
+
+namespace hj3d {
+hipError_t table_resolve(hj3d_ctx* ctx, hj3d_table* t) {
+  if (!t->pending) return hipSuccess;
+  t->pending = false;
+  hipError_t e = hipEventSynchronize(t->hc_ev);
+  if (e != hipSuccess) {
+    t->built = false;
+    return e;
+  }
+  uint64_t hc[4];
+  std::memcpy(hc, t->hc, sizeof(hc));
+  if (t->pending_agg && uint32_t(hc[3]) != 0) {  // a key range too dense for the LDS table
+    t->path = "nested_sort";
+    e = nested_build(ctx, t, t->pending_rel, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(hc, t->counts.p, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  }
+  t->n_mains = e == hipSuccess ? hc[1] : 0;
+  t->built = e == hipSuccess;
+  return e;
+}
+}  // namespace hj3d
+
+static hipError_t resolve(hj3d_ctx* ctx, const hj3d_table* t) {
+  return table_resolve(ctx, const_cast<hj3d_table*>(t));
+}
+
+extern "C" {
+
+const char* hj3d_table_build_path(const hj3d_table* t) {
+  if (t && t->pending && t->pending_ctx) (void)resolve(t->pending_ctx, t);
+  return t && t->built ? t->path : "none";
+}
 
 hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,
                               uint64_t* n_payload, uint64_t* n_sub) {
   if (!ctx || !t || !n_payload || !n_sub) return HJ3D_EINVAL;
   const uint64_t nbl = t->nb_local;
   uint32_t last = 0;  // off[nb_local] = the payload count
-  hipError_t e = hipMemcpyAsync(&last, t->off.as<uint32_t>() + nbl, sizeof(last), hipMemcpyDeviceToHost, ctx->stream);
+  hipError_t e = resolve(ctx, t);
+  if (e != hipSuccess) return from_hip(ctx, e, "hj3d_table_export");
+  e = hipMemcpyAsync(&last, t->off.as<uint32_t>() + nbl, sizeof(last), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return from_hip(ctx, e, "hj3d_table_export");
   const bool nested = t->desc.kind == HJ3D_NESTED;
@@ -377,7 +421,9 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out) {
   if (!ctx || !t || !out) return HJ3D_EINVAL;
   std::memset(out, 0, sizeof(*out));
-  return from_hip(ctx, table_stats(ctx, t, out, ctx->stream), "hj3d_table_stats");
+  hipError_t e = resolve(ctx, t);
+  if (e == hipSuccess) e = table_stats(ctx, t, out, ctx->stream);
+  return from_hip(ctx, e, "hj3d_table_stats");
 }
 
 hj3d_status hj3d_table_size(hj3d_ctx* ctx, const hj3d_table* t, uint64_t* n_entries, uint64_t* n_distinct) {
@@ -417,6 +463,7 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
   if ((flags & HJ3D_PROBE_EMIT) && !out_dev && out_cap) return fail(ctx, HJ3D_EINVAL, "hj3d_probe: EMIT without buffer");
   if ((flags & HJ3D_PROBE_UNNEST) && t->desc.kind != HJ3D_NESTED)
     return fail(ctx, HJ3D_EINVAL, "hj3d_probe: UNNEST needs a nested table");
+  if (hipError_t re = resolve(ctx, t); re != hipSuccess) return from_hip(ctx, re, "hj3d_probe");
   PhaseTimer tm(ctx, HJ3D_T_PROBE);
   uint64_t* res = ctx->res.as<uint64_t>();
   const bool acc = flags & HJ3D_PROBE_ACCUMULATE;
@@ -455,6 +502,7 @@ hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* p
   if ((flags & HJ3D_PROBE_EMIT) && !out_dev && out_cap) return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: EMIT without buffer");
   if ((flags & HJ3D_PROBE_UNNEST) && t->desc.kind != HJ3D_NESTED)
     return fail(ctx, HJ3D_EINVAL, "hj3d_probe_sel: UNNEST needs a nested table");
+  if (hipError_t re = resolve(ctx, t); re != hipSuccess) return from_hip(ctx, re, "hj3d_probe_sel");
   const bool chain_radix = t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n);
   const bool nested_radix = t->desc.kind == HJ3D_NESTED && radix_nested_applicable(ctx, t, probe->n);
   if (!ctx->sel_unfused && pk_probe_applicable(ctx, t, probe->n, flags)) {
@@ -520,6 +568,8 @@ hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* t
   if (!rel_ok(probe)) return fail(ctx, HJ3D_EINVAL, "hj3d_probe2: invalid relation");
   if (ts->desc.kind != tt->desc.kind) return fail(ctx, HJ3D_EINVAL, "hj3d_probe2: both tables must be of one kind");
   if (flags & HJ3D_PROBE_EMIT) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_probe2: triple materialisation not implemented");
+  if (hipError_t re = resolve(ctx, ts); re != hipSuccess) return from_hip(ctx, re, "hj3d_probe2");
+  if (hipError_t re = resolve(ctx, tt); re != hipSuccess) return from_hip(ctx, re, "hj3d_probe2");
   PhaseTimer tm(ctx, HJ3D_T_PROBE);
   uint64_t* res = ctx->res.as<uint64_t>();
   hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);

@@ -115,6 +115,13 @@ struct hj3d_table {
   uint64_t n_mains = 0;   // nested: main records (distinct keys) of the last build (host-known)
   bool built = false;
   const char* path = "none";  // which build made the table (hj3d_table_build_path)
+  // nested builds: the counts (main records, give-up flag) are copied to pinned host memory behind
+  // the build and read at the table's next use (table_resolve), not waited for inside hj3d_build
+  bool pending = false, pending_agg = false;
+  hj3d_rel pending_rel{};
+  hj3d_ctx* pending_ctx = nullptr;
+  uint64_t* hc = nullptr;  // pinned host copy of counts[4]
+  hipEvent_t hc_ev = nullptr;
   // chaining: off[nb_local+1] (u32 CSR offsets), ent[n] = {hash, row}
   // nested:   off[nb_local+1] over mains, main[d] = {hash, first_row, sub_off, sub_len},
   //           sub[n] = build rows grouped per key (first occurrence first, then row order)
@@ -352,6 +359,10 @@ hipError_t expected_fk_join(hj3d_ctx* ctx, const hj3d_rel& build, const hj3d_rel
                             bool swap, void* res, hipStream_t s);
 hipError_t expected_fk_join_gen(hj3d_ctx* ctx, const hj3d_rel& probe, uint64_t n_keys, uint64_t seed, bool swap,
                                 void* res, hipStream_t s);
+
+// api.cpp: completes a nested build whose counts are still in flight (reads them; runs the sort
+// build when the aggregation build gave up). Every use of a table's content calls it first.
+hipError_t table_resolve(hj3d_ctx* ctx, hj3d_table* t);
 
 // Scratch slot ids in hj3d_ctx::scratch.
 enum ScratchSlot {

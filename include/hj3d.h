@@ -215,7 +215,10 @@ void        hj3d_table_destroy(hj3d_table* t);
 /* Pre-size device storage for builds of up to max_build tuples (allocation outside timed loops). */
 hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build);
 hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t);
-/* Build: replaces the table content with the tuples of `build` (asynchronous). */
+/* Build: replaces the table content with the tuples of `build` (asynchronous). A nested table's
+ * build finishes at the table's next use (probe, statistics, export): its counts are read then, and
+ * when the LDS aggregation build gave up on a key range too dense for it, the sort build runs then,
+ * from `build` again -- so the build relation's device memory must stay valid until that use. */
 hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
 /* Host copy of a table's device arrays (synchronous): what the drop-in layer's per-tuple probes
  * walk (HtChaining1::findDirEntryByOther ht_chaining.hh:236-248, HtNested1::findMainNodeByOther
