@@ -293,6 +293,62 @@ hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
   return from_hip(ctx, e, "hj3d_table_clear");
 }
 
+// The partitioned probe sizes its LDS slices by the number of main records: a nested build's counts
+// (word 1 = main records; word 3 = the aggregation build's give-up flag) travel to pinned host
+// memory behind the build and are read at the table's next use (table_resolve), so consecutive
+// builds (experiment 4's two tables) do not wait for each other.
+static hipError_t nested_pending(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& build, bool agg) {
+  hipError_t e = hipSuccess;
+  if (!t->hc) {
+    e = hipHostMalloc(reinterpret_cast<void**>(&t->hc), 4 * sizeof(uint64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&t->hc_ev, hipEventDisableTiming);
+  }
+  if (e == hipSuccess) e = hipMemcpyAsync(t->hc, t->counts.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipEventRecord(t->hc_ev, ctx->stream);
+  t->pending = e == hipSuccess;
+  t->pending_agg = agg;
+  t->pending_rel = build;
+  t->pending_ctx = ctx;
+  t->n_mains = 0;
+  return e;
+}
+
+hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d_rel* builds, uint32_t count) {
+  if (!ctx || (count && (!tables || !builds))) return HJ3D_EINVAL;
+  for (uint32_t k = 0; k < count; ++k) {
+    if (!tables[k]) return HJ3D_EINVAL;
+    if (!rel_ok(&builds[k])) return fail(ctx, HJ3D_EINVAL, "hj3d_build_many: invalid relation");
+    for (uint32_t j = 0; j < k; ++j)
+      if (tables[j] == tables[k]) return fail(ctx, HJ3D_EINVAL, "hj3d_build_many: a table given twice");
+  }
+  // two nested tables of one geometry: one launch sequence (the aggregation build over both)
+  if (count == 2 && tables[0]->desc.kind == HJ3D_NESTED && tables[1]->desc.kind == HJ3D_NESTED &&
+      !ctx->nested_sort && !ctx->nested_pk && !nested_radix_applicable(ctx, tables[0], builds[0].n) &&
+      !nested_radix_applicable(ctx, tables[1], builds[1].n)) {
+    PhaseTimer tm(ctx, HJ3D_T_BUILD);
+    const char* path = "nested_agg";
+    for (uint32_t k = 0; k < 2; ++k) tables[k]->pending = false;
+    hipError_t e = nested_build_agg_many(ctx, tables, builds, 2, ctx->stream, &path);
+    if (e == hipErrorOutOfMemory) {
+      (void)hipGetLastError();
+      e = hipErrorNotSupported;
+    }
+    if (e != hipErrorNotSupported) {
+      for (uint32_t k = 0; k < 2 && e == hipSuccess; ++k) {
+        tables[k]->path = path;
+        e = nested_pending(ctx, tables[k], builds[k], true);
+      }
+      for (uint32_t k = 0; k < 2; ++k) tables[k]->built = e == hipSuccess;
+      return from_hip(ctx, e, "hj3d_build_many");
+    }
+  }
+  for (uint32_t k = 0; k < count; ++k) {
+    const hj3d_status st = hj3d_build(ctx, tables[k], &builds[k]);
+    if (st != HJ3D_OK) return st;
+  }
+  return HJ3D_OK;
+}
+
 hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   if (!ctx || !t) return HJ3D_EINVAL;
   if (!rel_ok(build)) return fail(ctx, HJ3D_EINVAL, "hj3d_build: invalid relation");
@@ -338,21 +394,7 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
       t->path = "nested_sort";
       e = nested_build(ctx, t, *build, ctx->stream);
     }
-    // the partitioned probe sizes its LDS slices by the number of main records: the counts (word 1
-    // = main records; word 3 = the aggregation build's give-up flag) travel to pinned host memory
-    // behind the build and are read at the table's next use (table_resolve), so consecutive builds
-    // (experiment 4's two tables) do not wait for each other
-    if (e == hipSuccess && !t->hc) {
-      e = hipHostMalloc(reinterpret_cast<void**>(&t->hc), 4 * sizeof(uint64_t), hipHostMallocDefault);
-      if (e == hipSuccess) e = hipEventCreateWithFlags(&t->hc_ev, hipEventDisableTiming);
-    }
-    if (e == hipSuccess) e = hipMemcpyAsync(t->hc, t->counts.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
-    if (e == hipSuccess) e = hipEventRecord(t->hc_ev, ctx->stream);
-    t->pending = e == hipSuccess;
-    t->pending_agg = agg;
-    t->pending_rel = *build;
-    t->pending_ctx = ctx;
-    t->n_mains = 0;
+    if (e == hipSuccess) e = nested_pending(ctx, t, *build, agg);
   }
   t->built = e == hipSuccess;
   return from_hip(ctx, e, "hj3d_build");

@@ -322,6 +322,10 @@ hipError_t nested_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStre
 // *path (optional): "nested_agg" or "nested_agg_slices" (the pk_slices form, > 2048 partitions).
 hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s,
                             const char** path = nullptr);
+// The same for nt <= 2 tables of one geometry (equal NB and bucket range) in one launch sequence:
+// both relations partitioned, one k_nagg grid over both tables' partitions, one scan, one compaction.
+hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* t, const hj3d_rel* r, uint32_t nt, hipStream_t s,
+                                 const char** path = nullptr);
 // nested_radix.hip: nested build from the radix-partitioned bucket CSR (large inputs);
 // hipErrorNotSupported when a bucket holds too many distinct keys (use nested_build).
 bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n);

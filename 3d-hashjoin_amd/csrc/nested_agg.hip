@@ -151,14 +151,23 @@ struct NaggSrc {
   uint32_t S2 = 0, cap2 = 0;
   PkGeom pk{};
 };
+// The tables one launch builds: one, or two of one geometry (experiment 4's S and T share NB): the
+// partitions of table 1 follow table 0's (global partition index P.. 2P - 1), its pairs follow
+// table 0's at pbase[1]; per table its directory, main records, sub rows and counts words.
+struct NaggTabs {
+  uint32_t P = 0, nt = 1;
+  uint32_t pbase[2] = {0, 0};
+  uint32_t* off[2] = {nullptr, nullptr};
+  uint32_t* sub[2] = {nullptr, nullptr};
+  uint4* main[2] = {nullptr, nullptr};
+  uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
+};
 template <int BLOCK, int SLOTS, bool PK>
 __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                 FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
-                                                uint32_t* __restrict__ off, uint4* __restrict__ mtmp,
-                                                uint32_t* __restrict__ sub, uint32_t* __restrict__ dcount,
-                                                unsigned long long* __restrict__ maxlen,
-                                                uint32_t* __restrict__ fail, const uint32_t* __restrict__ order,
-                                                uint32_t cap, NaggSrc src) {
+                                                uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
+                                                const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
+                                                NaggTabs tabs) {
   extern __shared__ uint32_t agg_lds[];
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
@@ -169,9 +178,15 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
   uint32_t& ovf = wsum[BLOCK / kWave + 1];
   uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
   const uint32_t limit = cap - BLOCK - 64;
-  const uint32_t p = PK ? blockIdx.x : order[blockIdx.x];
+  const uint32_t gp = PK ? blockIdx.x : order[blockIdx.x];  // partition over all tables
+  const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
+  const uint32_t p = gp - ti * tabs.P;                      // partition inside table ti
+  uint32_t* __restrict__ off = tabs.off[ti];
+  uint32_t* __restrict__ sub = tabs.sub[ti];
+  auto* maxlen = reinterpret_cast<unsigned long long*>(tabs.counts[ti] + 2);
+  auto* fail = reinterpret_cast<uint32_t*>(tabs.counts[ti] + 3);
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
-  const uint32_t e0 = ps[p], e1 = ps[p + 1], total = e1 - e0;
+  const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = tabs.pbase[ti];
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   if constexpr (PK) {
@@ -331,7 +346,7 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
       if (cnt[j]) {
         const uint32_t h = tkey[s];
         const uint32_t m = mrun + bcnt[lbk(h) - c0] + rank[j];
-        const uint32_t so = e0 + srun + tcnt[s];
+        const uint32_t so = e0 - tb + srun + tcnt[s];  // table ti's sub rows
         mtmp[e0 + m] = make_uint4(hash_of(h), tmin[s], so, cnt[j]);
         tcnt[s] = so;  // sub cursor
         mxlen = max(mxlen, cnt[j]);
@@ -382,7 +397,7 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     c0 = c1;
     __syncthreads();
   }
-  if (threadIdx.x == 0) dcount[p] = mrun;
+  if (threadIdx.x == 0) dcount[gp] = mrun;
   const uint64_t wm = wave_max(uint64_t(mxlen));
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
 }
@@ -433,16 +448,17 @@ __global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ o
                                                         const uint32_t* __restrict__ mbase,
                                                         const uint32_t* __restrict__ fail) {
   if (*fail) return;
-  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[dw.div(b)];
+  const uint32_t m0 = mbase[0];  // the table's first main record in the scan over every table
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[dw.div(b)] - m0;
 }
 
 __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
-                                                       const uint32_t* __restrict__ mbase, uint4* __restrict__ mains,
-                                                       const uint32_t* __restrict__ fail) {
-  if (*fail) return;
-  const uint32_t p = blockIdx.x;
-  const uint32_t n = mbase[p + 1] - mbase[p];
-  for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[mbase[p] + i] = mtmp[ps[p] + i];
+                                                       const uint32_t* __restrict__ mbase, NaggTabs tabs) {
+  const uint32_t gp = blockIdx.x, ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
+  if (reinterpret_cast<const uint32_t*>(tabs.counts[ti] + 3)[0]) return;  // fail flag
+  uint4* __restrict__ mains = tabs.main[ti];
+  const uint32_t n = mbase[gp + 1] - mbase[gp], m0 = mbase[gp] - mbase[ti * tabs.P];
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[m0 + i] = mtmp[ps[gp] + i];
 }
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
@@ -453,29 +469,50 @@ __global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
 
-__global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t P,
-                              uint32_t nbl, uint32_t* __restrict__ off, uint64_t* __restrict__ counts) {
+__global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t nbl,
+                              NaggTabs tabs) {
+  const uint32_t ti = threadIdx.x;
+  if (ti >= tabs.nt) return;
+  uint64_t* counts = tabs.counts[ti];
   if (reinterpret_cast<const uint32_t*>(counts + 3)[0]) return;  // fail flag
-  counts[0] = ps[P];
-  counts[1] = mbase[P];
-  off[nbl] = mbase[P];
+  const uint32_t a = ti * tabs.P, b = (ti + 1) * tabs.P;
+  counts[0] = ps[b] - ps[a];
+  counts[1] = mbase[b] - mbase[a];
+  tabs.off[ti][nbl] = mbase[b] - mbase[a];
+}
+
+// table 1's partition starts (written 0-based by its partition pass) moved behind table 0's pairs
+__global__ void k_nagg_ps_shift(uint32_t* __restrict__ ps, uint32_t n, uint32_t by) {
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ps[i] += by;
 }
 
 }  // namespace
 
-hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, const char** path) {
-  const uint64_t n = r.n;
+hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3d_rel* rr, uint32_t nt, hipStream_t s,
+                                 const char** path) {
+  if (nt < 1 || nt > 2) return hipErrorNotSupported;
+  hj3d_table* t = tt[0];
   const uint32_t nbl = t->nb_local;
-  // small inputs and tables that one partition would cover (no free bucket for the LDS table's
-  // empty marker) take the sort-based build
-  if (ctx->force_direct || n < (ctx->radix_min >> 4) || n >= (1ull << 31) || nbl <= 1024 ||
-      t->desc.num_buckets >= (1ull << 32))
+  uint64_t n = 0;
+  for (uint32_t k = 0; k < nt; ++k) {
+    // every table of one launch has one geometry (the partitions of both follow one plan)
+    if (tt[k]->nb_local != nbl || tt[k]->desc.bucket_lo != t->desc.bucket_lo ||
+        tt[k]->desc.num_buckets != t->desc.num_buckets || tt[k]->desc.kind != HJ3D_NESTED)
+      return hipErrorNotSupported;
+    // small inputs and tables that one partition would cover (no free bucket for the LDS table's
+    // empty marker) take the sort-based build
+    if (rr[k].n < (ctx->radix_min >> 4) || rr[k].n == 0) return hipErrorNotSupported;
+    n += rr[k].n;
+  }
+  if (ctx->force_direct || n >= (1ull << 31) || nbl <= 1024 || t->desc.num_buckets >= (1ull << 32))
     return hipErrorNotSupported;
   hipError_t e;
-  if ((e = t->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
-  if ((e = t->main.ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = t->sub.ensure(n * sizeof(uint32_t))) != hipSuccess) return e;
-  if ((e = t->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
+  for (uint32_t k = 0; k < nt; ++k) {
+    if ((e = tt[k]->off.ensure((uint64_t(nbl) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = tt[k]->main.ensure(rr[k].n * sizeof(uint4))) != hipSuccess) return e;
+    if ((e = tt[k]->sub.ensure(rr[k].n * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = tt[k]->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
+  }
   // partition width: kAggW buckets, narrower when that would leave the chip with fewer than two
   // partitions per CU (config E: 2M buckets -> 512 partitions of 4K instead of 342 of 6K)
   // Then the count is rounded up to whole waves of workgroups (one k_nagg workgroup per CU at a
@@ -495,25 +532,35 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
     }
   }
   const uint32_t P = (nbl + W - 1) / W;
+  if (pk && nt > 1) return hipErrorNotSupported;  // one table at a time on the slices
+  if (!pk && uint64_t(P) * nt > 2048) return hipErrorNotSupported;  // k_nagg_order's limit
+  const uint32_t PT = P * nt;  // partitions over every table
   if (path) *path = pk ? "nested_agg_slices" : "nested_agg";
   // scratch: pairs (n uint2; PK: the fine regions of pk_slices) | main records before compaction
-  // (n uint4) | starts, key counts, order
+  // (n uint4) | starts | key counts, order
   if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(P) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(PT) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
-  uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // P + 1 (scanned in place into the main bases)
-  uint32_t* order = dcount + P + 1;
-  uint64_t* counts = t->counts.as<uint64_t>();
-  uint32_t* off = t->off.as<uint32_t>();
-  uint32_t* fail = reinterpret_cast<uint32_t*>(counts + 3);
-  if ((e = hipMemsetAsync(counts, 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+  uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
+  uint32_t* order = dcount + PT + 1;
+  NaggTabs tabs;
+  tabs.P = P;
+  tabs.nt = nt;
+  for (uint32_t k = 0; k < nt; ++k) {
+    tabs.pbase[k] = k ? uint32_t(rr[0].n) : 0u;
+    tabs.off[k] = tt[k]->off.as<uint32_t>();
+    tabs.sub[k] = tt[k]->sub.as<uint32_t>();
+    tabs.main[k] = tt[k]->main.as<uint4>();
+    tabs.counts[k] = tt[k]->counts.as<uint64_t>();
+    if ((e = hipMemsetAsync(tabs.counts[k], 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
+  }
   const uint2* pairs = nullptr;
   const uint32_t* ps = nullptr;
   NaggSrc src;
   if (pk) {
     PkSlices sl;
-    if ((e = pk_slices(ctx, t, r, W, &sl, s)) != hipSuccess) return e;
+    if ((e = pk_slices(ctx, t, rr[0], W, &sl, s)) != hipSuccess) return e;
     if (sl.P != P) return hipErrorNotSupported;
     src.fine = sl.fine;
     src.fcnt = sl.fcnt;
@@ -522,17 +569,23 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
     src.pk = sl.pk;
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
-    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), fail);
+    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(),
+                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3));
   } else {
-    if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(P) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
+    if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
-    uint32_t np = 0;
-    if ((e = radix_partition_pairs(ctx, t, r, W, ctx->scratch[kScrPairs].as<uint2>(), pst, &np, s)) != hipSuccess)
-      return e;
-    if (np != P) return hipErrorNotSupported;
-    pairs = ctx->scratch[kScrPairs].as<uint2>();
+    uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
+    for (uint32_t k = 0; k < nt; ++k) {
+      uint32_t np = 0;
+      if ((e = radix_partition_pairs(ctx, tt[k], rr[k], W, pw + tabs.pbase[k], pst + k * P, &np, s)) != hipSuccess)
+        return e;
+      if (np != P) return hipErrorNotSupported;
+    }
+    if (nt > 1)  // table 1's starts were written 0-based into pst[P .. 2P]
+      hipLaunchKernelGGL(k_nagg_ps_shift, dim3((P + 256) / 256), dim3(256), 0, s, pst + P, P + 1, tabs.pbase[1]);
+    pairs = pw;
     ps = pst;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, P, order);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order);
   }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
@@ -555,30 +608,35 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
   const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
-  auto* mx = reinterpret_cast<unsigned long long*>(counts + 2);
   if (!pk && HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(P), dim3(kSmallBlock), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
-                       mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap512, src);
+    hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps, t->fm,
+                       lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
   } else {
     const uint32_t cap = kAggCapMax;
     const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
     if (pk)
-      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
-                         mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap, src);
+      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap, src, tabs);
     else
-      hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(P), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, off,
-                         mtmp, t->sub.as<uint32_t>(), dcount, mx, fail, order, cap, src);
+      hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap, src, tabs);
   }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
-  // and the caller, which reads the counts once after the build, runs the sort build instead
-  if ((e = exclusive_scan_u32(ctx, dcount, dcount, P, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, off, nbl,
-                     FastDiv32::make(W), dcount, fail);
-  hipLaunchKernelGGL(k_nagg_mains, dim3(P), dim3(kBlock), 0, s, mtmp, ps, dcount, t->main.as<uint4>(), fail);
-  hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(1), 0, s, ps, dcount, P, nbl, off, counts);
-  t->n_build = n;
+  // for its table and the caller, which reads the counts at the table's next use, runs the sort
+  // build instead
+  if ((e = exclusive_scan_u32(ctx, dcount, dcount, PT, s)) != hipSuccess) return e;
+  for (uint32_t k = 0; k < nt; ++k)
+    hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, tabs.off[k], nbl,
+                       FastDiv32::make(W), dcount + k * P, reinterpret_cast<const uint32_t*>(tabs.counts[k] + 3));
+  hipLaunchKernelGGL(k_nagg_mains, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs);
+  hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(64), 0, s, ps, dcount, nbl, tabs);
+  for (uint32_t k = 0; k < nt; ++k) tt[k]->n_build = rr[k].n;
   return hipGetLastError();
+}
+
+hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, const char** path) {
+  return nested_build_agg_many(ctx, &t, &r, 1, s, path);
 }
 
 }  // namespace hj3d

@@ -114,6 +114,7 @@ def lib():
         "hj3d_table_reserve": (st, [p, p, u64]),
         "hj3d_table_clear": (st, [p, p]),
         "hj3d_build": (st, [p, p, R]),
+        "hj3d_build_many": (st, [p, C.POINTER(p), R, u32]),
         "hj3d_table_build_path": (C.c_char_p, [p]),
         "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
         "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
@@ -284,6 +285,14 @@ class Context:
 
     def timer_reset(self):
         self._check(lib().hj3d_ctx_timer_reset(self.h), "timer_reset")
+
+    def build_many(self, tables, rels):
+        """Build tables[k] from rels[k] (hj3d_build_many): two nested tables of one geometry take
+        one launch sequence (experiment 4's S and T)."""
+        n = len(tables)
+        th = (C.c_void_p * n)(*[t.h for t in tables])
+        rs = (_Rel * n)(*[r.c for r in rels])
+        self._check(lib().hj3d_build_many(self.h, th, rs, n), "hj3d_build_many")
 
     # ---- probes ----
     def probe(self, table: "Table", rel: Rel, unique: bool = False, unnest: bool = False, out=None,

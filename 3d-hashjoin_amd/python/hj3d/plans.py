@@ -226,11 +226,17 @@ def exp4_relations_ref(log2R: int, alpha: int, mult_a: int, beta: int, mult_b: i
     return R, S, T
 
 
-def exp4_plan(ctx: Context, plan: str, R, S, T, nb: int) -> dict:
-    """Experiment-4 Ndu (nested, deferred unnesting) or Chj (chaining) on {k,a} relations."""
+def exp4_plan(ctx: Context, plan: str, R, S, T, nb: int, fused: bool = True) -> dict:
+    """Experiment-4 Ndu (nested, deferred unnesting) or Chj (chaining) on {k,a} relations. fused:
+    both tables built by one hj3d_build_many call (one launch sequence for two nested tables),
+    else one hj3d_build each (main_experiment4.cc:879-881)."""
     kind = HJ3D_NESTED if plan == "Ndu" else HJ3D_CHAIN
     ts, tt = Table(ctx, kind, nb), Table(ctx, kind, nb)
-    ts.build(Rel(S, key_word=1))
-    tt.build(Rel(T, key_word=1))
+    rs, rt = Rel(S, key_word=1), Rel(T, key_word=1)
+    if fused:
+        ctx.build_many([ts, tt], [rs, rt])
+    else:
+        ts.build(rs)
+        tt.build(rt)
     r = ctx.probe2(ts, tt, Rel(R, key_word=0))
     return r

@@ -859,8 +859,7 @@ def main_single_config(args):
 
         def step(ev):
             ev[0].record()
-            ts.build(relS)
-            tt.build(relT)
+            ctx.build_many([ts, tt], [relS, relT])  # one launch sequence for both tables
             ev[1].record()
             ctx.probe2(ts, tt, relR, fetch=False)
             ev[2].record()

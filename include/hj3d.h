@@ -220,6 +220,13 @@ hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t);
  * when the LDS aggregation build gave up on a key range too dense for it, the sort build runs then,
  * from `build` again -- so the build relation's device memory must stay valid until that use. */
 hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
+/* Builds several tables, tables[k] from builds[k] (asynchronous; as hj3d_build for each). Two nested
+ * tables of one geometry (equal num_buckets and bucket range: experiment 4's S and T tables,
+ * main_experiment4.cc:832-859) take ONE launch sequence: both relations partitioned, one
+ * aggregation grid over both tables' partitions, one scan, one compaction. Otherwise the tables
+ * are built one after another. Replaces the reference's consecutive AlgScan -> AlgNestJoinBuild
+ * runs (main_experiment4.cc:856-859, 879-881). */
+hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d_rel* builds, uint32_t count);
 /* Host copy of a table's device arrays (synchronous): what the drop-in layer's per-tuple probes
  * walk (HtChaining1::findDirEntryByOther ht_chaining.hh:236-248, HtNested1::findMainNodeByOther
  * ht_nested.hh:354-382). Call with NULL arrays first to get the sizes: *n_payload = entries

@@ -217,9 +217,11 @@ def test_exp4_plans_bit_exact(ctx, name, g, path):
 
 
 def _exp4_check(ctx, g, R, S, T):
+    """Both plans, with the two builds as one hj3d_build_many call (one launch sequence for the two
+    nested tables) and as two hj3d_build calls."""
     import hj3d
-    for plan in ("Ndu", "Chj"):
-        got = hj3d.exp4_plan(ctx, plan, R, S, T, g["nb"])
+    for plan, fused in (("Ndu", True), ("Ndu", False), ("Chj", True)):
+        got = hj3d.exp4_plan(ctx, plan, R, S, T, g["nb"], fused=fused)
         ref = g["plans"][plan]
         for k in ("c_probe_RS", "c_probe_RS_cmp", "c_probe_RT", "c_probe_RT_cmp", "c_top"):
             assert got[k.lower()] == ref[k], (plan, k, got[k.lower()], ref[k])
