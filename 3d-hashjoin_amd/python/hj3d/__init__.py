@@ -17,7 +17,7 @@ from typing import Optional
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(os.path.dirname(HERE))  # 3d-hashjoin_amd/
-LIB_PATH = os.environ.get("HJ3D_LIB", os.path.join(PKG_ROOT, "lib", "libhj3d.so"))
+LIB_PATH = os.environ.get("HJ3D_LIB") or os.path.join(PKG_ROOT, "lib", "libhj3d.so")
 HEADER_PATH = os.path.join(os.path.dirname(PKG_ROOT), "include", "hj3d.h")
 
 HJ3D_OK, HJ3D_EINVAL, HJ3D_ENOMEM, HJ3D_EDEVICE, HJ3D_EUNSUPPORTED, HJ3D_EOVERFLOW = range(6)
