@@ -38,7 +38,18 @@ def main():
     import hj3d
     nR, nS = int(a.nR), int(a.nS)
     t0 = time.perf_counter()
-    R, S = hj3d.exp1_relations_ref(nR, nS)
+    # the reference's relations, generated once per box into the relation cache (bench.py's
+    # reference_columns_cached: $HJ3D_REL_CACHE or $TMPDIR/hj3d_relcache) and mapped by later runs
+    sys.path.insert(0, ROOT)
+    from bench import reference_columns_cached
+    Rk, Sa = reference_columns_cached(nR, nS, True, lambda: None)
+    R = torch.zeros((nR, 3), dtype=torch.int32, device="cuda")
+    S = torch.zeros((nS, 3), dtype=torch.int32, device="cuda")
+    import numpy as np
+    R[:, 0] = torch.from_numpy(np.ascontiguousarray(Rk).view("int32")).to("cuda")
+    S[:, 0] = torch.arange(nS, dtype=torch.int32, device="cuda")
+    S[:, 1] = torch.from_numpy(np.ascontiguousarray(Sa).view("int32")).to("cuda")
+    del Rk, Sa
     gen_s = time.perf_counter() - t0
     ctx = hj3d.Context(0)
     # NB of the plans built on S.a: #dv(S.a) by the distributed pre-pass (per-rank bitmaps, OR-merge)
