@@ -93,9 +93,10 @@ def parse():
                    help="unique chaining probe: packed pairs, two launches (default), or the (hash, row) pair "
                         "partitioned probe (A/B)")
     p.add_argument("--theta", type=float, default=0.8, help="config C Zipf parameter")
-    p.add_argument("--nested-build", default="agg", choices=["agg", "sort", "radix"],
-                   help="3D build: bucket-range partition + LDS aggregation (default), LSD key sort "
-                        "(HJ3D_OPT_NESTED_SORT), radix bucket CSR + per-bucket grouping (HJ3D_OPT_NESTED_RADIX)")
+    p.add_argument("--nested-build", default="agg", choices=["agg", "slices", "sort", "radix"],
+                   help="3D build: bucket-range partition + LDS aggregation (default), the same on the packed "
+                        "partitioner's slices (HJ3D_OPT_NESTED_PK, the form of tables above 2048 partitions), LSD "
+                        "key sort (HJ3D_OPT_NESTED_SORT), radix bucket CSR + per-bucket grouping (HJ3D_OPT_NESTED_RADIX)")
     p.add_argument("--log2R", type=int, default=22, help="config E: |R| = 2^log2R")
     a = p.parse_args()
     if a.workload is None:
@@ -360,6 +361,10 @@ def main():
             torch.distributed.destroy_process_group()
     packed = args.probe_path == "packed" and plan == "Csr"
     ctx.packed_probe(packed)
+    if args.nested_build == "slices":
+        ctx.nested_pk(True)
+    elif args.nested_build == "sort":
+        ctx.nested_sort(True)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
     fx_plan = (fx or {}).get("plans", {}).get(plan)
 
@@ -827,6 +832,8 @@ def main_single_config(args):
         ctx.nested_radix(True)
     elif args.nested_build == "sort":
         ctx.nested_sort(True)
+    elif args.nested_build == "slices":
+        ctx.nested_pk(True)
 
     if args.workload == "C":
         nR, nS = args.nR or 10_000_000, args.nS or 100_000_000
