@@ -656,10 +656,14 @@ void hj3d_part_range(uint64_t nb, uint32_t parts, uint32_t part, uint64_t* lo, u
 
 uint64_t hj3d_partition_stride(uint64_t n, uint32_t parts) {
   // Each tuple's destination is a bucket range of equal width: its count is ~ Binomial(n, 1/parts)
-  // for distinct keys. Area = mean + 8 sigma + 2 tiles of slack (the tile claims), capped at n.
+  // for distinct keys. Repeated keys (config D's S.a: ~10 rows per key) widen that by the spread of
+  // the keys over the ranges: at 1e9 tuples into 8 ranges a destination held ~280 K more than 8
+  // sigma of the binomial (profiles/r04c_ab_xpart.log). Area = mean + max(8 sigma, mean / 64) + 2
+  // tiles of slack (the tile claims), capped at n; a spill is still reported by the counts.
   if (parts <= 1) return n;
   const double m = double(n) / parts, sd = std::sqrt(m * (1.0 - 1.0 / parts));
-  const uint64_t s = uint64_t(std::ceil(m + 8.0 * sd)) + 16384;
+  const double slack = 8.0 * sd > m / 64.0 ? 8.0 * sd : m / 64.0;
+  const uint64_t s = uint64_t(std::ceil(m + slack)) + 16384;
   return s < n ? s : n;
 }
 

@@ -99,11 +99,15 @@ __global__ void k_part_counts(const uint32_t* __restrict__ offs, uint32_t ntiles
 #ifndef HJ3D_XP_NT
 #define HJ3D_XP_NT 1  // pairs stored non-temporal (0: plain; A/B)
 #endif
+// Two 512-thread workgroups per CU (4096-tuple tiles): one workgroup's barrier-separated phases
+// overlap the other's memory waits. 1e9 tuples into 8 destinations, same box: one 1024-thread
+// workgroup per CU 4.81 / 4.80 ms, two of 512 threads 4.20 / 4.19 ms, three 4.80 / 4.76 ms
+// (profiles/r04c_ab_xpart.log).
 #ifndef HJ3D_XP_BLOCK
-#define HJ3D_XP_BLOCK 1024  // threads per workgroup (A/B: 512 with two workgroups per CU)
+#define HJ3D_XP_BLOCK 512  // threads per workgroup
 #endif
 #ifndef HJ3D_XP_WGS
-#define HJ3D_XP_WGS 1  // persistent workgroups per CU
+#define HJ3D_XP_WGS 2  // persistent workgroups per CU
 #endif
 constexpr int kXpBlock = HJ3D_XP_BLOCK;
 constexpr int kXpRounds = HJ3D_XP_ROUNDS;

@@ -287,7 +287,8 @@ hj3d_status hj3d_partition_sel(hj3d_ctx* ctx, const hj3d_rel* rel, const hj3d_se
  * u64) = the number of tuples destined to p. Pairs past a destination's stride are NOT written
  * (a spill): when any counts_dev[p] > stride the caller re-partitions with hj3d_partition (the
  * counts are the same). hj3d_partition_stride gives a bounded stride that distinct keys spill with
- * negligible probability (mean + 8 sigma of the binomial destination count + 2 tiles), so the send
+ * negligible probability (mean + max(8 sigma of the binomial destination count, mean / 64) + 2
+ * tiles; the mean / 64 covers keys repeated ~10 times, as config D's S.a), so the send
  * buffer is ~|rel| pairs instead of nparts x |rel| (stride = rel->n never spills). preds / npred:
  * an optional selection as in hj3d_partition_sel (npred = 0: none). Send it with
  * hj3d_comm_exchange_strided (same stride). Replaces the same seam as hj3d_partition

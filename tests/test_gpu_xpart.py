@@ -113,7 +113,7 @@ def test_single_pass_bounded_stride(ctx, parts):
     rng = np.random.default_rng(parts)
     t = np.stack([rng.permutation(n).astype(np.uint32), np.arange(n, dtype=np.uint32)], axis=1)
     stride = hj3d.partition_stride(n, parts)
-    assert stride < n and parts * stride < n + parts * 40_000
+    assert stride < n and parts * stride < 1.02 * n + parts * 40_000
     counts = _compare(ctx, hj3d.Rel(dev(t), key_word=0, row_word=1), n, nb, parts, stride=stride)
     assert max(counts) <= stride and sum(counts) == n
 
