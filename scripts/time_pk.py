@@ -18,6 +18,9 @@ def main():
     ap.add_argument("--nS", type=float, default=1e8)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-emit", action="store_true")
+    ap.add_argument("--layout", default="tuples", choices=["tuples", "pairs", "tuples_rows"],
+                    help="probe side: 12-B tuples with implicit rows (config B), received {key, row} pairs "
+                         "(8 B, explicit rows: a rank of the multi-GPU strand), or 12-B tuples with an explicit row word")
     ap.add_argument("--label", default=os.path.basename(os.path.dirname(os.environ.get("HJ3D_LIB", "default/x"))))
     a = ap.parse_args()
     import torch
@@ -33,6 +36,14 @@ def main():
     t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nR)
     t.reserve(nR)
     relR, relS = hj3d.Rel(R, 0), hj3d.Rel(S, 1)
+    if a.layout == "pairs":
+        P2 = torch.empty((nS, 2), dtype=torch.int32, device="cuda")
+        P2[:, 0] = S[:, 1]
+        P2[:, 1] = S[:, 0]
+        del S
+        relS = hj3d.Rel(P2, key_word=0, row_word=1)
+    elif a.layout == "tuples_rows":
+        relS = hj3d.Rel(S, key_word=1, row_word=0)
     for _ in range(3):
         t.build(relR)
         ctx.probe(t, relS, unique=True, out=out, fetch=False)
@@ -43,7 +54,7 @@ def main():
         t.build(relR)
         ctx.probe(t, relS, unique=True, out=out, fetch=False)
     ctx.sync()
-    res = {"label": a.label, "nR": nR, "nS": nS, "emit": out is not None}
+    res = {"label": a.label, "layout": a.layout, "nR": nR, "nS": nS, "emit": out is not None}
     for k, ph in (("build", hj3d.T_BUILD), ("probe", hj3d.T_PROBE), ("k_pk_part", hj3d.T_SCATTER),
                   ("k_pk_split", hj3d.T_HIST), ("k_pk_probe", hj3d.T_PROBE_KERNEL)):
         ms, cnt = ctx.timer(ph)
