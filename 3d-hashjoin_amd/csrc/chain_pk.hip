@@ -122,7 +122,10 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   // the key's line; loading it again after the ranking phase fetched that line twice: 15.4 B per
   // 8-B received pair, round 3). {key, row} pairs (stride 8, 8-B aligned) take one 8-B load.
   uint32_t wa[IMPLICIT ? 1 : kPkRounds], wb[IMPLICIT ? 1 : kPkRounds];
-  const bool pair8 = !IMPLICIT && r.stride == 8 && r.key_off == 0 && r.row_off == 4 &&
+#ifndef HJ3D_PK_PAIR8
+#define HJ3D_PK_PAIR8 1  // {key, row} pairs as one 8-B load (0: two 4-B loads; A/B)
+#endif
+  const bool pair8 = HJ3D_PK_PAIR8 && !IMPLICIT && r.stride == 8 && r.key_off == 0 && r.row_off == 4 &&
                      (reinterpret_cast<uintptr_t>(r.base) & 7u) == 0;
   // a wave-uniform 64-bit tile pointer + 32-bit lane offsets (the loads take the scalar-base form)
   auto load = [&](uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
