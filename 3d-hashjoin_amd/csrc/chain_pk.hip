@@ -138,12 +138,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
         const char* t = r.base + uint64_t(i) * r.stride;
         if constexpr (!IMPLICIT) {
           if (pair8) {
-            const uint64_t kv = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(t)) : 0ull;
+            const uint64_t* a8 = reinterpret_cast<const uint64_t*>(t);
+            const uint64_t kv = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(a8) : *a8) : 0ull;
             h[j] = uint32_t(kv);
             rw[j] = uint32_t(kv >> 32);
           } else {
-            h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
-            rw[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.row_off)) : 0u;
+            const uint32_t* ak = reinterpret_cast<const uint32_t*>(t + r.key_off);
+            const uint32_t* ar = reinterpret_cast<const uint32_t*>(t + r.row_off);
+            h[j] = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(ak) : *ak) : 0u;
+            rw[j] = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(ar) : *ar) : 0u;
           }
         } else if (HJ3D_PK_NTLOAD) {
           h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
