@@ -120,10 +120,13 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   uint32_t ha[kPkRounds], hb[kPkRounds], pa[SEL ? kPkRounds : 1], pb[SEL ? kPkRounds : 1];
   // explicit rows: loaded with the key at tile prefetch and kept in registers (the row word shares
   // the key's line; loading it again after the ranking phase fetched that line twice: 15.4 B per
-  // 8-B received pair, round 3). {key, row} pairs (stride 8, 8-B aligned) take one 8-B load.
+  // 8-B received pair, round 3).
   uint32_t wa[IMPLICIT ? 1 : kPkRounds], wb[IMPLICIT ? 1 : kPkRounds];
+// {key, row} pairs: two 4-B loads issued back to back (the second hits the line the first brought
+// in) measured faster than one 8-B load: 1e8 received pairs, same box, 0.505 / 0.505 against 0.597 /
+// 0.593 ms (profiles/r04f_ab_pairs.log). 1: the 8-B form (A/B).
 #ifndef HJ3D_PK_PAIR8
-#define HJ3D_PK_PAIR8 1  // {key, row} pairs as one 8-B load (0: two 4-B loads; A/B)
+#define HJ3D_PK_PAIR8 0
 #endif
   const bool pair8 = HJ3D_PK_PAIR8 && !IMPLICIT && r.stride == 8 && r.key_off == 0 && r.row_off == 4 &&
                      (reinterpret_cast<uintptr_t>(r.base) & 7u) == 0;
