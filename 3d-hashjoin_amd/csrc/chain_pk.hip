@@ -41,6 +41,9 @@ constexpr int kPkBlock = 1024;
 #ifndef HJ3D_PK_NTREG
 #define HJ3D_PK_NTREG 1   // partition: region segments stored non-temporal (0: plain; nt 0.452 -> 0.447 ms, and the probe reading them 0.493 -> 0.489)
 #endif
+#ifndef HJ3D_PK_ST32
+#define HJ3D_PK_ST32 0    // partition: region pairs stored as two 4-B stores (A/B)
+#endif
 #ifndef HJ3D_PK_NTLOAD
 #define HJ3D_PK_NTLOAD 1  // partition: probe keys loaded non-temporal (0: plain; nt 0.447 -> 0.436 ms, probe phase -2 %)
 #endif
@@ -291,10 +294,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       const uint2 e = stage[si.y + j];
       const bool spill = si.x & kOvfFlag;
       if (!spill && HJ3D_PK_DIAG != 1) {
-        if (HJ3D_PK_NTREG)
+        if (HJ3D_PK_ST32) {  // two 4-B stores (A/B)
+          uint32_t* w = reinterpret_cast<uint32_t*>(region + si.x + j);
+          __builtin_nontemporal_store(e.x, w);
+          __builtin_nontemporal_store(e.y, w + 1);
+        } else if (HJ3D_PK_NTREG) {
           __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(region + si.x + j));
-        else
+        } else {
           region[si.x + j] = e;
+        }
       }
       to_ovf(e, si.x & ~kOvfFlag, spill);
     }
@@ -484,6 +492,29 @@ __global__ __launch_bounds__(kSpBlock) void k_pk_split(const uint2* __restrict__
 
 // ---- k_pk_probe ----
 constexpr uint32_t kLdsWords = kPkLdsWords;
+#ifndef HJ3D_PB_LD32
+#define HJ3D_PB_LD32 0  // packed pairs loaded as two 4-B loads instead of one 8-B load (A/B)
+#endif
+#ifndef HJ3D_PB_ST32
+#define HJ3D_PB_ST32 0  // output pairs stored as two 4-B stores instead of one 8-B store (A/B)
+#endif
+__device__ __forceinline__ void pair_st(uint2* p, uint32_t lo, uint32_t hi, bool split) {
+  if (split) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(p);
+    __builtin_nontemporal_store(lo, w);
+    __builtin_nontemporal_store(hi, w + 1);
+  } else {
+    __builtin_nontemporal_store((uint64_t(hi) << 32) | lo, reinterpret_cast<uint64_t*>(p));
+  }
+}
+__device__ __forceinline__ uint64_t pair_ld(const uint2* p) {
+  if (HJ3D_PB_LD32) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    const uint32_t lo = __builtin_nontemporal_load(w), hi = __builtin_nontemporal_load(w + 1);
+    return (uint64_t(hi) << 32) | lo;
+  }
+  return __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
+}
 // K = pairs per lane and chunk (the next chunk in flight), chosen per probe from the expected
 // region length (pk_items): a region of L pairs costs ceil(L / 64K) chunks of 64K item slots, so
 // K = 7 walks config B's ~384-pair regions in one 448-slot chunk where K = 8 spends 512 slots.
@@ -575,7 +606,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t 
           uint2* dst = (ok && slot < out_cap) ? out + slot : sink + (threadIdx.x & 63);
           __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(dst));
         } else if (ok && slot < out_cap) {
-          __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(out + slot));
+          pair_st(out + slot, row, match[j], HJ3D_PB_ST32);
         }
       }
       if (CK && m) {
@@ -743,7 +774,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
         cbase = src_off(cr) - int64_t(nst);
         nst = rpre[wid][cr + 1];
       }
-      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(region + (cbase + int64_t(f))));
+      v[j] = pair_ld(region + (cbase + int64_t(f)));
     }
   };
   // non-flat cursor: region r, offset qq
@@ -757,7 +788,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     const uint32_t last = ll ? ll - 1 : 0u;
 #pragma unroll
     for (int j = 0; j < K; ++j)
-      v[j] = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + min(q0 + j * 64 + lane, last)));
+      v[j] = pair_ld(src + min(q0 + j * 64 + lane, last));
   };
   auto probe_hbm_chunk = [&](const uint64_t (&v)[K], uint32_t valid, uint64_t slot0) __attribute__((always_inline)) {
 #pragma unroll
