@@ -160,6 +160,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       return HJ3D_OK;
     case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_PK: ctx->nested_pk = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_PK_COMPACT: ctx->pk_compact = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);
@@ -356,6 +357,9 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
   t->pending = false;  // a build in flight for the old content is replaced (its copy stays stream-ordered)
+  // the build's row range (implicit rows: row_base + [0, n)); explicit rows: unknown
+  t->row_lo = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base < (1ull << 32) ? uint32_t(build->row_base) : 0u;
+  t->row_rr = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base + build->n <= (1ull << 32) ? build->n : 0u;
   if (t->desc.kind == HJ3D_CHAIN) {
     bool sorted = false;
     t->path = "radix";

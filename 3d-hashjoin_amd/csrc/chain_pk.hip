@@ -705,8 +705,151 @@ __device__ __forceinline__ void pk_stage(const uint32_t* __restrict__ off, const
   }
 }
 
+// ---- compact slice image (k_pk_probe with COMPACT, 512-thread workgroups, two per CU) ----
+// The directory keeps 16-bit entry starts (count = next start - start; a slice holds < 2^16
+// entries), the entries one word each: q * rr + (row - rlo), q = h / NB, which fits 32 bits when
+// q_max * rr < 2^32 (the host checks; b = 1 tables: rr = NB). An entry whose word would reach
+// 0xFFFFFFFF (q = q_max and a large row, ~0.1 % of entries) is stored as kWideEntry, which never
+// matches; a probe that ends without a match after seeing one redoes its bucket in HBM. The image
+// is ~6 B per bucket instead of 12, so two slices' workgroups share a CU (LDS 64 KB each): one
+// workgroup stages while the other walks.
+constexpr uint32_t kWideEntry = 0xFFFFFFFFu;
+constexpr uint32_t kLdsWordsC = 15872;  // 62 KB: the compact image of one slice
+__device__ __forceinline__ void pk_stage_c(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
+                                           uint32_t nbs, uint32_t e0, uint32_t ne, const PkGeom& pk,
+                                           uint16_t* ldir, uint32_t* lent, int block) {
+  constexpr int kStage = 12;
+  const uint32_t nmax = max(nbs + 1, ne);
+  for (uint32_t k0 = threadIdx.x; k0 < nmax; k0 += block * kStage) {
+    uint32_t a[kStage];
+    uint2 x[kStage];
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * block;
+      a[u] = k <= nbs ? off[b0 + k] : 0u;
+      x[u] = k < ne ? ent[e0 + k] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < kStage; ++u) {
+      const uint32_t k = k0 + u * block;
+      if (k <= nbs) ldir[k] = uint16_t(a[u] - e0);
+      if (k < ne) {
+        const uint64_t w = uint64_t(pk.dnb.div(x[u].x)) * pk.rr + (x[u].y - pk.rlo);
+        lent[k] = w >= kWideEntry ? kWideEntry : uint32_t(w);
+      }
+    }
+  }
+}
+
+// pk_probe_items on the compact image; `wide` gets the lanes whose bucket held a kWideEntry and
+// found no match (their item j: bit j), for the HBM redo.
 template <int K, int MODE, bool CK>
-__global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__ region,
+__device__ __forceinline__ void pk_probe_items_c(const uint64_t (&v)[K], uint32_t valid, uint64_t slot0,
+                                                 const uint16_t* ldir, const uint32_t* lent, const PkGeom& pk,
+                                                 uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
+                                                 uint64_t out_cap, uint32_t& wide) {
+  uint32_t nm = 0, sc = 0;
+  uint32_t s[K], nn[K], match[K], cmps[K], base[K];
+  bool live[K], sawwide[K];
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const bool ok = (valid >> j) & 1u;
+    const uint32_t x = uint32_t(v[j]);
+    const uint32_t b = ok ? x >> pk.qbits : 0u;
+    s[j] = ldir[b];
+    nn[j] = ok ? uint32_t(ldir[b + 1]) - s[j] : 0u;
+    base[j] = (x & pk.qmask) * pk.rr;
+    match[j] = kInvalid;
+    cmps[j] = nn[j];
+    live[j] = nn[j] != 0 && nn[j] <= kSortedMaxPk;
+    sawwide[j] = false;
+  }
+#pragma unroll
+  for (uint32_t c = 0; c < 3; ++c) {
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      const bool ok = live[j] && c < nn[j];
+      const uint32_t e = lent[ok ? s[j] + (c == 0 ? 0u : nn[j] - c) : 0u];
+      const bool hit = ok && e != kWideEntry && e - base[j] < pk.rr;
+      sawwide[j] = sawwide[j] || (ok && e == kWideEntry);
+      match[j] = hit ? e - base[j] + pk.rlo : match[j];
+      cmps[j] = hit ? c + 1 : cmps[j];
+      live[j] = live[j] && !hit;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    if (live[j] && nn[j] > 3) {
+      for (uint32_t c = 3; c < nn[j]; ++c) {
+        const uint32_t e = lent[s[j] + nn[j] - c];
+        sawwide[j] = sawwide[j] || e == kWideEntry;
+        if (e != kWideEntry && e - base[j] < pk.rr) {
+          cmps[j] = c + 1;
+          match[j] = e - base[j] + pk.rlo;
+          break;
+        }
+      }
+    } else if (nn[j] > kSortedMaxPk) {  // long bucket in arrival order: order-free form
+      uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, cnt = 0;
+      for (uint32_t k = s[j]; k < s[j] + nn[j]; ++k) {
+        const uint32_t e = lent[k];
+        if (e == kWideEntry) {
+          sawwide[j] = true;
+          continue;
+        }
+        const uint32_t row = e % pk.rr + pk.rlo;  // rare path: a division
+        minrow = min(minrow, row);
+        if (e - base[j] < pk.rr) {
+          ++cnt;
+          lo_m = min(lo_m, row);
+          hi_m = max(hi_m, row);
+        }
+      }
+      if (sawwide[j]) {
+        // the order-free form needs every row of the bucket: redo it in HBM
+      } else if (cnt != 0 && lo_m == minrow) {
+        cmps[j] = 1;
+        match[j] = lo_m;
+      } else if (cnt != 0) {
+        uint32_t gt = 0;
+        for (uint32_t k = s[j]; k < s[j] + nn[j]; ++k) gt += lent[k] % pk.rr + pk.rlo > hi_m;
+        cmps[j] = 2 + gt;
+        match[j] = hi_m;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const bool ok = (valid >> j) & 1u;
+    // a bucket with a wide entry and no match in LDS (or a long one with any wide entry): the whole
+    // item is redone against the table in HBM (counters and output there)
+    const bool redo = ok && sawwide[j] && (match[j] == kInvalid || nn[j] > kSortedMaxPk);
+    wide |= uint32_t(redo) << j;
+    if (redo) continue;
+    const uint32_t row = uint32_t(v[j] >> 32);
+    const bool m = match[j] != kInvalid;
+    nm += m;
+    sc += ok ? cmps[j] : 0u;
+    if (MODE == 1) {
+      const uint64_t slot = slot0 + uint32_t(j * 64);
+      if (ok && slot < out_cap)
+        __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(out + slot));
+    }
+    if (CK && m) {
+      acc[4] += row;
+      acc[5] += match[j];
+      const uint64_t ph = pair_hash(row, match[j]);
+      acc[7] += ph;
+      acc[8] ^= ph;
+    }
+  }
+  acc[1] += nm;
+  acc[2] += nm;
+  acc[3] += sc;
+}
+
+template <int K, int MODE, bool CK, int BLOCK = kPkBlock, bool COMPACT = false>
+__global__ __launch_bounds__(BLOCK) void k_pk_probe(const uint2* __restrict__ region,
                                                        const uint32_t* __restrict__ counts, uint32_t G, uint32_t cap,
                                                        uint32_t splits, bool flat, const uint32_t* __restrict__ off,
                                                        const uint2* __restrict__ ent, PkGeom pk, FastMod fm,
@@ -714,22 +857,27 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
                                                        const uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
                                                        uint64_t* __restrict__ partials, uint64_t* __restrict__ res,
                                                        int accumulate, uint2* __restrict__ sink) {
-  __shared__ uint32_t lds[kLdsWords];
-  __shared__ uint32_t wtot[kPkBlock / kWave];
-  __shared__ uint32_t rpre[kPkBlock / kWave][65];
+  static_assert(COMPACT || BLOCK == kPkBlock, "the full image is staged by 1024 threads");
+  __shared__ uint32_t lds[COMPACT ? kLdsWordsC : kLdsWords];
+  __shared__ uint32_t wtot[BLOCK / kWave];
+  __shared__ uint32_t rpre[BLOCK / kWave][65];
   __shared__ uint64_t bbase;
-  __shared__ uint64_t red[kPkBlock / kWave][kProbeFields];
+  __shared__ uint64_t red[BLOCK / kWave][kProbeFields];
   __shared__ uint32_t flag;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  constexpr int kWaves = kPkBlock / kWave;
+  constexpr int kWaves = BLOCK / kWave;
   const uint32_t P = pk.P;
   const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
   const uint32_t b0 = p * pk.W;
   const uint32_t nbs = min(pk.W, pk.nbl - b0);
   const uint32_t e0 = off[b0], e1 = off[b0 + nbs], ne = e1 - e0;
-  const bool fits = (nbs + 2) + 2ull * ne <= kLdsWords;
+  // compact: 16-bit starts (nbs + 1 of them), then one word per entry
+  const uint32_t dirw = (nbs + 2) / 2 + 1;
+  const bool fits = COMPACT ? uint64_t(dirw) + ne <= kLdsWordsC : (nbs + 2) + 2ull * ne <= kLdsWords;
   uint32_t* ldir = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
+  uint16_t* ldir16 = reinterpret_cast<uint16_t*>(lds);
+  uint32_t* lent32 = lds + dirw;
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   // this block's regions: wave w takes g = g_lo + w + 16 k (lane k holds region k's count)
@@ -847,14 +995,32 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   };
   if (fits) {
     walk([&]() __attribute__((always_inline)) {
-           if (HJ3D_PK_DIAG == 3) {  // no staging: an empty directory (every probe misses)
-             for (uint32_t k = threadIdx.x; k < nbs; k += kPkBlock) ldir[k] = 0;
+           if constexpr (COMPACT) {
+             pk_stage_c(off, ent, b0, nbs, e0, ne, pk, ldir16, lent32, BLOCK);
+           } else if (HJ3D_PK_DIAG == 3) {  // no staging: an empty directory (every probe misses)
+             for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) ldir[k] = 0;
            } else {
              pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent);
            }
          },
          [&](const uint64_t (&v)[K], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
-           pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
+           if constexpr (COMPACT) {
+             uint32_t wide = 0;
+             pk_probe_items_c<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir16, lent32, pk, acc, out, out_cap, wide);
+             if (wide) {  // buckets with an entry too wide for the compact image: redo in HBM
+               const uint64_t slot0 = bbase + wpre + srel;
+#pragma unroll
+               for (int j = 0; j < K; ++j) {
+                 if (!((wide >> j) & 1u)) continue;
+                 const uint32_t x = uint32_t(v[j]), bl = b0 + (x >> pk.qbits);
+                 const uint32_t st = off[bl];
+                 pk_probe_hbm<MODE, CK>(pk.hash_of(x, p), uint32_t(v[j] >> 32), st, off[bl + 1] - st, ent,
+                                        slot0 + j * 64, acc, out, out_cap);
+               }
+             }
+           } else {
+             pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
+           }
          });
   } else {
     walk([&]() __attribute__((always_inline)) {},
@@ -869,8 +1035,8 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
     for (;;) {
       __syncthreads();
       if (threadIdx.x == 0) {
-        const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlOvfCursor), (unsigned long long)kPkBlock);
-        const uint64_t take = c < novf ? min(uint64_t(kPkBlock), novf - c) : 0ull;
+        const uint64_t c = atomicAdd(reinterpret_cast<unsigned long long*>(ctl + kCtlOvfCursor), (unsigned long long)BLOCK);
+        const uint64_t take = c < novf ? min(uint64_t(BLOCK), novf - c) : 0ull;
         bbase = c;
         flag = uint32_t(take);
         if (MODE == 1 && take)
@@ -921,7 +1087,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__
   if (!flag) return;
   // the last block: column sums over every block's row
   uint64_t sum[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kPkBlock) {
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += BLOCK) {
 #pragma unroll
     for (int f = 1; f < kProbeFields; ++f) {
       const uint64_t x = __hip_atomic_load(partials + uint64_t(b) * kProbeFields + f, __ATOMIC_RELAXED,
@@ -1286,6 +1452,51 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   const int items = ctx->pk_items ? ctx->pk_items : flat ? kItemsMax : pk_items(double(r.n) / double(preg));
   uint2* o = static_cast<uint2*>(out);
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
+  // the compact slice image: a known build row range whose words q * rr + row fit 32 bits below
+  // q_max, and a slice image (with 6 sigma of headroom on its entries) within kLdsWordsC
+  PkGeom pkc = pk;
+  bool compact = false;
+  if (ctx->pk_compact && t->row_rr && t->row_rr < (1ull << 32) &&
+      uint64_t(0xFFFFFFFFull / nb) * t->row_rr <= 0xFFFFFFFFull) {
+    const double ex = double(t->n_build) / pl.P;
+    const double words = (pl.W + 2) / 2 + 1 + ex + 6.0 * std::sqrt(ex > 1.0 ? ex : 1.0);
+    compact = words <= double(kLdsWordsC);
+    pkc.rr = uint32_t(t->row_rr);
+    pkc.rlo = t->row_lo;
+  }
+  if (compact) {
+    // twice the workgroups (two per CU): every slice's regions split over two when one wave of
+    // workgroups would leave CUs idle
+    const uint32_t want_c = uint32_t(ctx->num_cus) * 4;
+    uint32_t sp2 = pl.P < want_c ? (want_c + pl.P - 1) / pl.P : 1u;
+    if (sp2 > Gp) sp2 = Gp;
+    const uint32_t nb2 = pl.P * sp2;
+    if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nb2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
+      return e;
+    partials = ctx->scratch[kScrPartial].as<uint64_t>();
+    KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
+#define HJ3D_PKC_LAUNCH(K, MODE, CK)                                                                                 \
+  tk.launch(k_pk_probe<K, MODE, CK, 512, true>, dim3(nb2), dim3(512), s, pregion, pcounts, Gp, pcap, sp2, flat,     \
+            t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pkc, t->fm, o, out_cap, ovf, ctl, partials, res, acc, \
+            reinterpret_cast<uint2*>(ctl + 64))
+#define HJ3D_PKC_LAUNCH_K(MODE, CK)               \
+  switch (items) {                                \
+    case 5: HJ3D_PKC_LAUNCH(5, MODE, CK); break;  \
+    case 6: HJ3D_PKC_LAUNCH(6, MODE, CK); break;  \
+    case 7: HJ3D_PKC_LAUNCH(7, MODE, CK); break;  \
+    default: HJ3D_PKC_LAUNCH(8, MODE, CK); break; \
+  }
+    if (emit) {
+      if (ck) HJ3D_PKC_LAUNCH_K(1, true)
+      else HJ3D_PKC_LAUNCH_K(1, false)
+    } else {
+      if (ck) HJ3D_PKC_LAUNCH_K(0, true)
+      else HJ3D_PKC_LAUNCH_K(0, false)
+    }
+#undef HJ3D_PKC_LAUNCH_K
+#undef HJ3D_PKC_LAUNCH
+    return hipGetLastError();
+  }
   {
     KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
 #define HJ3D_PK_LAUNCH(K, MODE, CK)                                                                                  \

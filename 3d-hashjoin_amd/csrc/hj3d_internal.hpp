@@ -85,6 +85,7 @@ struct hj3d_ctx {
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
+  bool pk_compact = true;         // HJ3D_OPT_PK_COMPACT: the packed probe's compact slice image where it applies
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
@@ -115,6 +116,10 @@ struct hj3d_table {
   uint64_t n_mains = 0;   // nested: main records (distinct keys) of the last build (host-known)
   bool built = false;
   const char* path = "none";  // which build made the table (hj3d_table_build_path)
+  // build rows lie in [row_lo, row_lo + row_rr) (implicit-row builds; 0: unknown): the compact
+  // probe image packs q * row_rr + (row - row_lo) into one word
+  uint32_t row_lo = 0;
+  uint64_t row_rr = 0;
   // nested builds: the counts (main records, give-up flag) are copied to pinned host memory behind
   // the build and read at the table's next use (table_resolve), not waited for inside hj3d_build
   bool pending = false, pending_agg = false;
@@ -287,6 +292,7 @@ PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nb_local, uint64_t n_build);
 struct PkGeom {
   FastDiv32 dnb, dw;  // / NB, / W
   uint32_t nb, lo, nbl, W, P, qbits, qmask;
+  uint32_t rr = 0, rlo = 0;  // compact probe image: build rows in [rlo, rlo + rr), entries q * rr + row - rlo
   // hash of a packed pair in slice p
   __device__ __forceinline__ uint32_t hash_of(uint32_t v, uint32_t p) const {
     return (v & qmask) * nb + lo + p * W + (v >> qbits);

@@ -182,7 +182,12 @@ enum {
    * partitioner's slices (k_pk_part + k_pk_split, the form tables of more than 2048 partitions take,
    * e.g. config D's 1e8-bucket Nrs table) whenever it applies, not only above 2048 partitions
    * (tests). Region overflow (skewed keys) falls back to the sort build. */
-  HJ3D_OPT_NESTED_PK = 11
+  HJ3D_OPT_NESTED_PK = 11,
+  /* HJ3D_OPT_PK_COMPACT (0/1, default 1): the packed unique probe stages its table slices as a
+   * compact image (16-bit bucket starts, one word per entry: ~6 B per bucket instead of 12) and runs
+   * two 512-thread workgroups per CU, where the table's build rows are implicit (a known row range)
+   * and the slice fits; 0 keeps the full image, one 1024-thread workgroup per slice (A/B, tests). */
+  HJ3D_OPT_PK_COMPACT = 12
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
