@@ -183,10 +183,11 @@ enum {
    * e.g. config D's 1e8-bucket Nrs table) whenever it applies, not only above 2048 partitions
    * (tests). Region overflow (skewed keys) falls back to the sort build. */
   HJ3D_OPT_NESTED_PK = 11,
-  /* HJ3D_OPT_PK_COMPACT (0/1, default 1): the packed unique probe stages its table slices as a
+  /* HJ3D_OPT_PK_COMPACT (0/1, default 0): the packed unique probe stages its table slices as a
    * compact image (16-bit bucket starts, one word per entry: ~6 B per bucket instead of 12) and runs
    * two 512-thread workgroups per CU, where the table's build rows are implicit (a known row range)
-   * and the slice fits; 0 keeps the full image, one 1024-thread workgroup per slice (A/B, tests). */
+   * and the slice fits. Measured slower at config B (0.61 against 0.49 ms), so off by default; kept
+   * for A/B measurements and its parity test. */
   HJ3D_OPT_PK_COMPACT = 12
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);

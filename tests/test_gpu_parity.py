@@ -444,7 +444,7 @@ def test_packed_probe_compact_image_equals_full(ctx, nR, nb, nS):
             host = out.cpu().numpy().view(np.uint32)
             got[compact] = (g["c_probe"], g["c_cmp"], g["c_top"], g["out"], host_checksums(host))
     finally:
-        ctx.pk_compact(True)
+        ctx.pk_compact(False)
     assert got[True] == got[False]
     assert got[True][:3] == (e.c_probe, e.c_cmp, e.c_top) and got[True][3] == e.out
     if nR == 1_000_000:
