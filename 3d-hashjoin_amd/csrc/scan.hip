@@ -261,10 +261,12 @@ hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, 
   const uint64_t tiles = (n + kTile - 1) / kTile;
   if (tiles >= (1ull << 31)) return excl_scan<uint32_t>(ctx, in, out, n, s);
   DevBuf& st = ctx->scan_status;
-  const void* before = st.p;
+  const size_t before = st.bytes;
   hipError_t e = st.ensure(tiles * sizeof(uint64_t));
-  // fresh memory could hold a word that looks published for this epoch: clear it once
-  if (e == hipSuccess && st.p != before) e = hipMemsetAsync(st.p, 0, st.bytes, s);
+  // fresh memory could hold a word that looks published for this epoch (stale u32 data of a
+  // freed buffer often does): clear it whenever the buffer was reallocated. The test is on the
+  // size, not the address: the allocator readily returns the freed block's address again.
+  if (e == hipSuccess && st.bytes != before) e = hipMemsetAsync(st.p, 0, st.bytes, s);
   if (e == hipSuccess) e = ctx->ensure_ctl();
   if (e != hipSuccess) return e;
   // the ticket: a control word kept zero between calls (the last tile resets it)

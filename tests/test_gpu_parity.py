@@ -156,6 +156,39 @@ def test_nested_many_keys_per_bucket(ctx, nb, path):
         ctx.nested_radix(False)
 
 
+def test_scan_status_regrowth_ignores_stale_memory():
+    """exclusive_scan_u32's look-back status words are cleared whenever their buffer is
+    reallocated, also when the allocator hands back the freed block's address. Device memory
+    is first filled with words that read as 'published' for the first 64 scan epochs and
+    released to HIP; a fresh context then runs sort-built nested tables of growing size (each
+    regrows the status buffer and the sort scratch), whose distinct-key counts must equal numpy's.
+    Before the fix a reallocation at the old address skipped the clear (a rare wrong main count)."""
+    import torch
+    import hj3d
+    k = torch.arange(1 << 24, dtype=torch.int64, device="cuda")
+    poison = (((k % 64) + 1) << 34) | (1 << 32) | 7  # epoch 1..64, flag 'aggregate', value 7
+    del k, poison
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    c = hj3d.Context()
+    c.force_direct(True)
+    c.nested_sort(True)
+    try:
+        rng = np.random.default_rng(5)
+        for n in (20_000, 90_000, 400_000, 1_700_000, 4_000_000):
+            a = rng.integers(0, n // 10, n, dtype=np.uint32)
+            S = O.tuples3(np.arange(n, dtype=np.uint32), a)
+            dS = dev(S)
+            t = hj3d.Table(c, hj3d.HJ3D_NESTED, max(n // 7, 1))
+            t.build(hj3d.Rel(dS, 1, 0))
+            st = t.stats()
+            t.close()
+            assert st["distinct"] == len(np.unique(a)), n
+            assert st["entries"] == n, n
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("zipf", [False, True], ids=["uniform", "zipf"])
 @pytest.mark.parametrize("nb", [2000, 7000, 20000, 100000, 250000])
 def test_nested_agg_build_vs_oracle(ctx, nb, zipf):
