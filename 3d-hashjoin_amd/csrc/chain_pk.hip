@@ -73,6 +73,12 @@ static_assert(kPkSeg == 8 || kPkSeg == 16, "64- or 128-B segments");
 constexpr uint32_t kPkStage = kPkTile + (kPkSeg - 1) * 1024 > HJ3D_PK_STAGE ? HJ3D_PK_STAGE : kPkTile + (kPkSeg - 1) * 1024;
 static_assert(kPkTile <= kPkStage && kPkStage < 65536, "the tile alone fits the stage; stage offsets in 16 bits");
 constexpr uint32_t kSortedMaxPk = 32;
+#ifndef HJ3D_PK_SWZ
+#define HJ3D_PK_SWZ 0  // partition: stage[] slots XOR-swizzled (i ^ (i >> 5) & 31) against the ~16-pair stride of per-slice runs (A/B)
+#endif
+// stage slot of pair i of k_pk_part's stage: a bijection inside each 32-pair (256-B) block, so the
+// per-thread run accesses (thread me at its run start, runs ~16 pairs apart) spread over the banks
+__device__ __forceinline__ uint32_t pk_sw(uint32_t i) { return HJ3D_PK_SWZ ? i ^ ((i >> 5) & 31u) : i; }
 constexpr uint32_t kOvfFlag = 0x80000000u;
 
 // control words (u64) of one probe strand
@@ -264,7 +270,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       sbase[me] = my_loc + my_kc;
 #pragma unroll
       for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
+        if (uint32_t(j) < my_kc) stage[pk_sw(my_loc + j)] = creg[j];
       for (uint32_t sg = 0; sg < my_len / kPkSeg; ++sg) {
         // segment-aligned (cap is a multiple of kPkSeg) unless a mid-stream flush moved the cursor:
         // a segment goes to the region only whole, else (all of it) to the overflow list
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       uint32_t row;
       if constexpr (IMPLICIT) row = rb + li;
       else row = rw[j];
-      stage[sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1))] = make_uint2(h[j], row);
+      stage[pk_sw(sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1)))] = make_uint2(h[j], row);
     }
     load(h, pw, rw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
     __syncthreads();
@@ -291,7 +297,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     for (uint32_t kk = me; kk < nfull * kPkSeg; kk += kPkBlock) {
       const uint2 si = seginfo[kk / kPkSeg];
       const uint32_t j = kk % kPkSeg;
-      const uint2 e = stage[si.y + j];
+      const uint2 e = stage[pk_sw(si.y + j)];
       const bool spill = si.x & kOvfFlag;
       if (!spill && HJ3D_PK_DIAG != 1) {
         if (HJ3D_PK_ST32) {  // two 4-B stores (A/B)
@@ -311,7 +317,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       const uint32_t F = my_len - my_len % kPkSeg;
 #pragma unroll
       for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_len - F) creg[j] = stage[my_loc + F + j];
+        if (uint32_t(j) < my_len - F) creg[j] = stage[pk_sw(my_loc + F + j)];
       my_cur += F;
       my_kc = my_len - F;
     }

@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--nS", type=float, default=1e8)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-emit", action="store_true")
-    ap.add_argument("--compact", type=int, default=1, help="HJ3D_OPT_PK_COMPACT (the probe's compact slice image)")
+    ap.add_argument("--compact", type=int, default=0, help="HJ3D_OPT_PK_COMPACT (the probe's compact slice image)")
     ap.add_argument("--layout", default="tuples", choices=["tuples", "pairs", "tuples_rows"],
                     help="probe side: 12-B tuples with implicit rows (config B), received {key, row} pairs "
                          "(8 B, explicit rows: a rank of the multi-GPU strand), or 12-B tuples with an explicit row word")
