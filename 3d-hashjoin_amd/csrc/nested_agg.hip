@@ -56,6 +56,15 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_PER_CU
 #define HJ3D_NAGG_PER_CU 2  // target partitions per CU when the table is small (A/B: 4 with 256 threads)
 #endif
+#ifndef HJ3D_NAGG_WHOLE
+#define HJ3D_NAGG_WHOLE 1  // a round over the partition's whole bucket range skips the per-pair range test (0: A/B)
+#endif
+#ifndef HJ3D_NAGG_STATIC
+#define HJ3D_NAGG_STATIC 1  // fixed load / store counts per pass step (0: A/B, the guarded form)
+#endif
+#ifndef HJ3D_NAGG_DIAG
+#define HJ3D_NAGG_DIAG 0  // diagnostic variants (tables wrong): 1 pass B without its sub-row stores, 2 without pass B
+#endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
@@ -98,10 +107,21 @@ __device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h, u
   return s;
 }
 
+// min over the wave's 64 lanes (all active), for every lane: DPP butterflies inside each row of 16
+// lanes (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror), then the four row minima by
+// readlane. (__shfl_xor compiled to six ds_bpermute rounds, each waiting on LDS.)
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_min_step(uint32_t v) {
+  return min(v, uint32_t(__builtin_amdgcn_update_dpp(int(kInvalid), int(v), CTRL, 0xF, 0xF, false)));
+}
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v = min(v, uint32_t(__shfl_xor(int(v), o, kWave)));
-  return v;
+  v = dpp_min_step<0xB1>(v);
+  v = dpp_min_step<0x4E>(v);
+  v = dpp_min_step<0x141>(v);
+  v = dpp_min_step<0x140>(v);
+  const uint32_t a = uint32_t(__builtin_amdgcn_readlane(int(v), 0)), b = uint32_t(__builtin_amdgcn_readlane(int(v), 16));
+  const uint32_t c = uint32_t(__builtin_amdgcn_readlane(int(v), 32)), d = uint32_t(__builtin_amdgcn_readlane(int(v), 48));
+  return min(min(a, b), min(c, d));
 }
 
 // Exclusive scan of a[0..n) in LDS by BLOCK threads (contiguous chunks per thread); returns
@@ -161,6 +181,7 @@ struct NaggTabs {
   uint32_t* sub[2] = {nullptr, nullptr};
   uint4* main[2] = {nullptr, nullptr};
   uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
+  uint32_t* sink = nullptr;  // pass B's stores of items without a row (the context's store-sink words)
 };
 template <int BLOCK, int SLOTS, bool PK>
 __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
@@ -222,13 +243,17 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     }
   };
   // kAggU pairs per thread of the partition's stream from f0 (coalesced: item f0 + u * BLOCK + tid)
+  // HJ3D_NAGG_STATIC: every call issues exactly kAggU loads per lane (indices clamped to the last
+  // pair; callers only load when total > 0), so the compiler can wait for the batch in flight with a
+  // counted s_waitcnt at its use instead of vmcnt(0) right after issuing it (a data-dependent number
+  // of loads, or of stores in pass B, made every step wait for the next step's loads)
   const auto load = [&](uint32_t f0, uint2 (&v)[kAggU]) __attribute__((always_inline)) {
 #pragma unroll
     for (int u = 0; u < kAggU; ++u) {
-      const uint32_t f = f0 + u * BLOCK + threadIdx.x;
+      const uint32_t f = HJ3D_NAGG_STATIC ? min(f0 + u * BLOCK + threadIdx.x, total - 1) : f0 + u * BLOCK + threadIdx.x;
       if constexpr (PK) {
         v[u] = make_uint2(0, 0);
-        if (f < total) {
+        if (HJ3D_NAGG_STATIC || f < total) {
           while (f >= nst) {
             ++cr;
             nst = rstart[cr + 1];
@@ -245,6 +270,7 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
   uint32_t c0 = 0, span = (nbs + kAggRounds - 1) / kAggRounds;
   while (c0 < nbs) {
     const uint32_t c1 = min(nbs, c0 + span);
+    const bool whole = HJ3D_NAGG_WHOLE && c0 == 0 && c1 == nbs;
     // a key that no key of this round is: its bucket lies outside [b0 + c0, b0 + c1)
     const uint32_t empty = PK ? (c1 << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
     for (uint32_t s = threadIdx.x; s < cap; s += BLOCK) {
@@ -261,27 +287,42 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     // ---- pass A: count and min row per key ----
     uint2 v[kAggU], nv[kAggU];
     restart();
-    load(0, v);
+    if (HJ3D_NAGG_STATIC) {
+      if (total) load(0, nv);
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
+    } else {
+      load(0, v);
+    }
     for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
-      if (i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
+      if (HJ3D_NAGG_STATIC || i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
       // home slots of all items read together (one LDS latency for the batch); only items whose
       // key is not in its home slot walk the probe sequence
-      bool act[kAggU];
+      // active items as one bit mask (a bool array was re-materialised from exec masks per item)
+      uint32_t actm = 0;
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-        const uint32_t lb = lbk(v[u].x);
-        act[u] = i < total && lb >= c0 && lb < c1;
-        k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
+        // one round over the whole range (the common case): every pair of the partition is in it,
+        // so no bucket (a 64-bit multiply-high per pair on the modulo path) is computed
+        bool inr = true;
+        if (!whole) {
+          const uint32_t lb = lbk(v[u].x);
+          inr = lb >= c0 && lb < c1;
+        }
+        const bool a = i < total && inr;
+        actm |= uint32_t(a) << u;
+        k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint64_t am = __ballot(act[u]);
+        bool a = (actm >> u) & 1u;
+        const uint64_t am = __ballot(a);
         if (am) {  // the wave's first active key, if several lanes hold it (a Zipf hot key)
           const int leader = __ffsll((unsigned long long)am) - 1;
           const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
-          const bool mine = act[u] && v[u].x == hl;
+          const bool mine = a && v[u].x == hl;
           const uint64_t same = __ballot(mine);
           if (__popcll(same) > 1) {
             const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
@@ -294,10 +335,10 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
                 atomicMin(&tmin[s], rmin);
               }
             }
-            act[u] = act[u] && !mine;
+            a = a && !mine;
           }
         }
-        if (act[u]) {
+        if (a) {
           const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_insert(tkey, v[u].x, empty, &nkeys, cap, limit);
           if (s == kInvalid) {
             ovf = 1;
@@ -356,38 +397,57 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
     __syncthreads();
     // ---- pass B: rows into their keys' sub ranges ----
     restart();
-    load(0, v);
-    for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
-      if (i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
-      bool act[kAggU];
+    if (HJ3D_NAGG_STATIC) {
+      if (total) load(0, nv);
+#pragma unroll
+      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
+    } else {
+      load(0, v);
+    }
+    for (uint32_t i0 = 0; i0 < (HJ3D_NAGG_DIAG == 2 ? 0u : total); i0 += BLOCK * kAggU) {
+      if (HJ3D_NAGG_STATIC || i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
+      // active items as one bit mask (a bool array was re-materialised from exec masks per item)
+      uint32_t actm = 0;
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-        const uint32_t lb = lbk(v[u].x);
-        act[u] = i < total && lb >= c0 && lb < c1;
-        k0[u] = tkey[act[u] ? slot_of(v[u].x, cap) : 0u];
+        // one round over the whole range (the common case): every pair of the partition is in it,
+        // so no bucket (a 64-bit multiply-high per pair on the modulo path) is computed
+        bool inr = true;
+        if (!whole) {
+          const uint32_t lb = lbk(v[u].x);
+          inr = lb >= c0 && lb < c1;
+        }
+        const bool a = i < total && inr;
+        actm |= uint32_t(a) << u;
+        k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint64_t am = __ballot(act[u]);
+        bool a = (actm >> u) & 1u;
+        uint32_t* dst = tabs.sink;
+        const uint64_t am = __ballot(a);
         if (am) {
           const int leader = __ffsll((unsigned long long)am) - 1;
           const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
-          const bool mine = act[u] && v[u].x == hl;
+          const bool mine = a && v[u].x == hl;
           const uint64_t same = __ballot(mine);
           if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive sub slots
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl, cap)], uint32_t(__popcll(same)));
             base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
-            if (mine) sub[base + uint32_t(__popcll(same & lt))] = v[u].y;
-            act[u] = act[u] && !mine;
+            if (mine) dst = sub + base + uint32_t(__popcll(same & lt));
+            a = a && !mine;
           }
         }
-        if (act[u]) {
+        if (a) {
           const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find(tkey, v[u].x, cap);
-          sub[atomicAdd(&tcnt[s], 1u)] = v[u].y;
+          dst = sub + atomicAdd(&tcnt[s], 1u);
         }
+        // one store per item and lane, in straight-line code (items without a row store to the
+        // sink): a fixed store count per step (see load)
+        if (HJ3D_NAGG_DIAG != 1 && (HJ3D_NAGG_STATIC || dst != tabs.sink)) *dst = v[u].y;
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
@@ -544,9 +604,11 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + PT + 1;
+  if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   NaggTabs tabs;
   tabs.P = P;
   tabs.nt = nt;
+  tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
   for (uint32_t k = 0; k < nt; ++k) {
     tabs.pbase[k] = k ? uint32_t(rr[0].n) : 0u;
     tabs.off[k] = tt[k]->off.as<uint32_t>();
