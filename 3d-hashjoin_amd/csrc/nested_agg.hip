@@ -62,6 +62,12 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_STATIC
 #define HJ3D_NAGG_STATIC 1  // fixed load / store counts per pass step (0: A/B, the guarded form)
 #endif
+#ifndef HJ3D_NAGG_PKW
+#define HJ3D_NAGG_PKW 1536  // buckets per partition on the packed slices (0: the kAggW-based width).
+// Uniform keys, 1e9 tuples / 1e8 buckets: 26.1 ms (5,357 buckets, one 1024-thread workgroup per CU)
+// -> 19.9 ms (2,048) -> 18.5 ms (1,536; two 512-thread workgroups per CU, a quarter of the sub-row
+// window); 1,024 exceeds the 65,536 slices (profiles/r04n_ab_pkw.log)
+#endif
 #ifndef HJ3D_NAGG_DIAG
 #define HJ3D_NAGG_DIAG 0  // diagnostic variants (tables wrong): 1 pass B without its sub-row stores, 2 without pass B
 #endif
@@ -589,6 +595,10 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (P0 > 2048 || ctx->nested_pk) {
       pk = true;
       W = uint32_t(W1 >= 1024 ? W1 : W);
+      // the slices take any partition count: HJ3D_NAGG_PKW buckets per partition (0: as above),
+      // narrow enough for the small form's two workgroups per CU and a small sub-row window
+      // (at most 65536 slices: pk_slices' two levels of 1024 x 64)
+      if (HJ3D_NAGG_PKW) W = std::min<uint32_t>(W, std::max<uint32_t>(HJ3D_NAGG_PKW, (nbl + 65535) / 65536));
     }
   }
   const uint32_t P = (nbl + W - 1) / W;
@@ -662,6 +672,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
     for (const void* k : {reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
+                          reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, true>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, true>)})
       if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
@@ -670,10 +681,14 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
-  if (!pk && HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
+  if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps, t->fm,
-                       lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
+    if (pk)
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
+    else
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
   } else {
     const uint32_t cap = kAggCapMax;
     const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
