@@ -143,11 +143,15 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
   __shared__ uint32_t loc[kMaxParts];   // local counts, then local run starts
   __shared__ uint32_t gb[kMaxParts];    // global run start of each partition for this tile
   __shared__ uint32_t wsum[kPBlock / kWave];
-  uint32_t h[kPRounds];
+  // explicit row ids are loaded with the keys, a tile ahead (loading them at the stage write after
+  // the ranking phase waited for every load separately: one round trip per tuple and round)
+  const bool explicit_rows = r.row_off != 0xFFFFFFFFu;
+  uint32_t h[kPRounds], rw[kPRounds];
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
     h[j] = i < r.n ? key_ld(r, i) : 0u;
+    rw[j] = explicit_rows && i < r.n ? r.row(i) : 0u;
   }
   // this workgroup's write cursor per partition: partition start + its run's offset (k_rp_hist)
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = cur[p];
@@ -184,7 +188,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
     for (int j = 0; j < kPRounds; ++j) {
       if (rk[j] == kInvalid) continue;
       const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], r.row(i));
+      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], explicit_rows ? rw[j] : r.row(i));
     }
     __syncthreads();
     const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
@@ -192,6 +196,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
     for (int j = 0; j < kPRounds; ++j) {
       const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
       h[j] = i < r.n ? key_ld(r, i) : 0u;
+      rw[j] = explicit_rows && i < r.n ? r.row(i) : 0u;
     }
     for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
       const uint2 e = stage[k];
@@ -635,10 +640,12 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
   const uint64_t gbase = uint64_t(blockIdx.x) * P;
   for (uint32_t p = threadIdx.x; p < P; p += BLOCK) cur[p] = 0;
   uint32_t h[ROUNDS];
+  uint32_t rw[IMPLICIT ? 1 : ROUNDS];  // explicit row ids, loaded with the keys a tile ahead
 #pragma unroll
   for (int j = 0; j < ROUNDS; ++j) {
     const uint64_t i = uint64_t(blockIdx.x) * TILE + uint64_t(j) * BLOCK + threadIdx.x;
     h[j] = i < r.n ? r.key(i) : 0u;
+    if constexpr (!IMPLICIT) rw[j] = i < r.n ? r.row(i) : 0u;
   }
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
@@ -666,7 +673,8 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
     for (int j = 0; j < ROUNDS; ++j) {
       if (rk[j] == kInvalid) continue;
       const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
-      const uint32_t y = IMPLICIT ? (((rk[j] >> TBITS) << 16) | li) : r.row(base + li);
+      uint32_t y = ((rk[j] >> TBITS) << 16) | li;
+      if constexpr (!IMPLICIT) y = rw[j];
       stage[loc[rk[j] >> TBITS] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
     }
     __syncthreads();
@@ -675,6 +683,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1(RelView r, FastMod fm, uint3
     for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = nbase + uint64_t(j) * BLOCK + threadIdx.x;
       h[j] = i < r.n ? r.key(i) : 0u;
+      if constexpr (!IMPLICIT) rw[j] = i < r.n ? r.row(i) : 0u;
     }
     // kOutU staged pairs per thread and step: their LDS reads and stores are independent, so the
     // step exposes kOutU-way parallelism instead of one dependent LDS -> LDS -> store chain
@@ -776,9 +785,11 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
   for (int j = 0; j < int(kSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
   uint32_t h[ROUNDS];
   uint32_t pw[SEL ? ROUNDS : 1];  // the predicate word of the tile in flight
+  uint32_t rw[IMPLICIT ? 1 : ROUNDS];  // explicit row ids, loaded with the keys a tile ahead
   uint32_t npassed = 0;
   auto load_pw = [&](int j, uint64_t i) {
     if constexpr (SEL) pw[j] = i < r.n ? *reinterpret_cast<const uint32_t*>(r.base + i * r.stride + sel.word_off) : 0u;
+    if constexpr (!IMPLICIT) rw[j] = i < r.n ? r.row(i) : 0u;
   };
 #pragma unroll
   for (int j = 0; j < ROUNDS; ++j) {
@@ -869,7 +880,8 @@ __global__ __launch_bounds__(BLOCK) void k_rp_part1r(RelView r, FastMod fm, uint
       if (rk[j] == kInvalid) continue;
       const uint32_t part = rk[j] >> TBITS;
       const uint32_t li = uint32_t(j) * BLOCK + threadIdx.x;
-      const uint32_t y = IMPLICIT ? li : r.row(base + li);
+      uint32_t y = li;
+      if constexpr (!IMPLICIT) y = rw[j];
       stage[sbase[part] + (rk[j] & (TILE - 1))] = make_uint2(h[j], y);
     }
     const uint64_t nbase = uint64_t(tile + gridDim.x) * TILE;  // next tile: loads in flight
