@@ -252,6 +252,11 @@ __global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict
 // workgroup form one (nearly) contiguous, coalesced range. Heavier slots are queued and written
 // by k_expand_heavy_flat with all workgroups.
 constexpr uint32_t kHeavyOut = 8192;
+#ifndef HJ3D_EXP_U
+#define HJ3D_EXP_U 4  // k_expand_light: outputs per thread and step (1: one at a time, A/B)
+#endif
+constexpr int kExpU = HJ3D_EXP_U;
+static_assert(kBlock == 256, "k_expand_light's binary search covers 256 slots in 8 steps");
 
 struct SlotSrc {
   RelView r;                   // direct: probe relation (row of slot i = r.row(i))
@@ -275,7 +280,8 @@ template <bool SLOTS, bool CK>
 __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t nslots, const uint64_t* __restrict__ ooff,
                                                          const uint32_t* __restrict__ sub, uint2* __restrict__ out,
                                                          uint64_t out_cap, uint32_t* __restrict__ heavy,
-                                                         uint32_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
+                                                         uint32_t* __restrict__ nheavy, uint64_t* __restrict__ partials,
+                                                         uint2* __restrict__ sink) {
   __shared__ uint32_t loff[kBlock + 1];
   __shared__ uint32_t lz[kBlock];
   __shared__ uint32_t lpr[kBlock];
@@ -313,23 +319,49 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t n
   lpr[threadIdx.x] = pr;
   lpos[threadIdx.x] = pos;
   __syncthreads();
-  for (uint32_t p = threadIdx.x; p < tot; p += kBlock) {
-    uint32_t lo = 0, hi = kBlock;  // largest t with loff[t] <= p (slots with c = 0 are skipped over)
+  // kExpU outputs per thread and step: their binary searches interleave and their sub-row loads are
+  // all in flight before the first is used (one output per step waited for each load in turn).
+  // Indices past the end are clamped to the last output (a fixed load count per step), and only
+  // valid outputs are stored.
+  for (uint32_t p0 = threadIdx.x; p0 < tot; p0 += kExpU * kBlock) {
+    uint32_t lo[kExpU], q[kExpU], br[kExpU];
+    bool ok[kExpU];
 #pragma unroll
-    for (int step = 0; step < 8; ++step) {
-      const uint32_t md = (lo + hi) >> 1;
-      if (loff[md] <= p) lo = md; else hi = md;
+    for (int u = 0; u < kExpU; ++u) {
+      const uint32_t p = p0 + u * kBlock;
+      ok[u] = p < tot;
+      lo[u] = 0;
     }
-    const uint32_t q = p - loff[lo];
-    const uint32_t br = sub[lz[lo] + q], prow = lpr[lo];
-    const uint64_t o = lpos[lo] + q;
-    if (o < out_cap) __builtin_nontemporal_store((uint64_t(br) << 32) | prow, reinterpret_cast<uint64_t*>(out + o));
-    if (CK) {
-      acc[4] += prow;
-      acc[5] += br;
-      const uint64_t ph = pair_hash(prow, br);
-      acc[7] += ph;
-      acc[8] ^= ph;
+#pragma unroll
+    for (int step = 0; step < 8; ++step) {  // largest t with loff[t] <= p (slots with c = 0 skipped)
+#pragma unroll
+      for (int u = 0; u < kExpU; ++u) {
+        const uint32_t p = min(p0 + u * kBlock, tot - 1);
+        const uint32_t md = lo[u] + (128u >> step);
+        if (loff[md] <= p) lo[u] = md;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kExpU; ++u) {
+      const uint32_t p = min(p0 + u * kBlock, tot - 1);
+      q[u] = p - loff[lo[u]];
+      br[u] = sub[lz[lo[u]] + q[u]];
+    }
+#pragma unroll
+    for (int u = 0; u < kExpU; ++u) {
+      // one store per output slot of the step, straight-line (an invalid one goes to the sink):
+      // a store under a branch drew its load into the branch, right before the store
+      const uint32_t prow = lpr[lo[u]];
+      const uint64_t o = lpos[lo[u]] + q[u];
+      uint2* dst = ok[u] && o < out_cap ? out + o : sink;
+      __builtin_nontemporal_store((uint64_t(br[u]) << 32) | prow, reinterpret_cast<uint64_t*>(dst));
+      if (CK && ok[u]) {
+        acc[4] += prow;
+        acc[5] += br[u];
+        const uint64_t ph = pair_hash(prow, br[u]);
+        acc[7] += ph;
+        acc[8] ^= ph;
+      }
     }
   }
   // the output checksums only (the counts are the probe's): no partials without HJ3D_PROBE_CHECKSUM
@@ -581,10 +613,11 @@ hipError_t expand(hj3d_ctx* ctx, const SlotSrc& src, bool slots, bool ck, uint64
                   uint64_t* partials, uint64_t* res, hipStream_t s) {
   const uint32_t nblk = uint32_t((nslots + kBlock - 1) / kBlock);
   uint64_t* hoff = ctx->scratch[kScrD].as<uint64_t>();
+  if (hipError_t e = ctx->ensure_ctl(); e != hipSuccess) return e;  // ctl words [64, 128): store sink
   auto launch = [&](auto slots_c, auto ck_c) {
     constexpr bool SL = decltype(slots_c)::value, CK = decltype(ck_c)::value;
     hipLaunchKernelGGL((k_expand_light<SL, CK>), dim3(nblk), dim3(kBlock), 0, s, src, nslots, ooff, sub, out, out_cap,
-                       heavy, nheavy, partials);
+                       heavy, nheavy, partials, reinterpret_cast<uint2*>(ctx->ctl.as<uint64_t>() + 64));
     hipLaunchKernelGGL(k_heavy_offsets, dim3(1), dim3(1024), 0, s, heavy, nheavy, ooff, hoff);
     hipLaunchKernelGGL((k_expand_heavy_flat<SL, CK>), dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, src, ooff, sub,
                        heavy, nheavy, hoff, out, out_cap, res);
