@@ -256,6 +256,9 @@ constexpr uint32_t kHeavyOut = 8192;
 #define HJ3D_EXP_U 4  // k_expand_light: outputs per thread and step (1: one at a time, A/B)
 #endif
 constexpr int kExpU = HJ3D_EXP_U;
+#ifndef HJ3D_RN_STATIC
+#define HJ3D_RN_STATIC 1  // k_rn_probe_seg, materialised unnest: fixed store count per chunk (0: A/B)
+#endif
 static_assert(kBlock == 256, "k_expand_light's binary search covers 256 slots in 8 steps");
 
 struct SlotSrc {
@@ -543,7 +546,8 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
                                                           bool flat, uint2* __restrict__ out, uint64_t out_cap,
                                                           uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
                                                           uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
-                                                          uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials) {
+                                                          uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials,
+                                                          uint64_t* __restrict__ sink) {
   __shared__ uint32_t lds[kProbeLdsWords];
   const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
   const uint32_t b0 = p * W;
@@ -558,6 +562,52 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
   uint32_t* ldir = lds;
   uint4* lmain = reinterpret_cast<uint4*>(lds + dirw);
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  if constexpr (MODE == kCountUN && FITS && HJ3D_RN_STATIC) {
+    // materialised unnest: every item of a chunk writes its three slot words, in straight-line
+    // code (absent items to the sink), so the chunk's store count is fixed and the wait for the
+    // next chunk's pairs (loaded before these stores) leaves the stores in flight
+    uint32_t* zsink = reinterpret_cast<uint32_t*>(sink + 1);
+    seg_walk<true>(region, counts, seg, G, cap, P, p, splits, sp, flat,
+                   [&] { stage_nested(off, mains, b0, nbs, m0, nm, ldir, lmain); },
+                   [&](const uint64_t (&v)[kSegItems], const uint64_t (&sl)[kSegItems], uint32_t vm) {
+#pragma unroll
+                     for (int j = 0; j < kSegItems; ++j) {
+                       const bool valid = (vm >> j) & 1u;
+                       const uint32_t hv = uint32_t(v[j]), row = uint32_t(v[j] >> 32);
+                       const uint32_t bl = fm.mod(hv) - lo - b0;
+                       const uint32_t d = valid ? ldir[bl] : 0u;
+                       const uint32_t s0 = d >> 16, n = d & 0xFFFFu;
+                       uint32_t found = kInvalid;
+                       uint4 F = make_uint4(0, 0, 0, 0);
+                       for (uint32_t k = s0; k < s0 + n; ++k) {
+                         const uint4 c = lmain[k];
+                         if (c.x == hv) {
+                           found = k;
+                           F = c;
+                           break;
+                         }
+                       }
+                       uint32_t before = 0;  // mains of this bucket inserted before the matching one
+                       if (found != kInvalid)
+                         for (uint32_t k = s0; k < s0 + n; ++k) before += lmain[k].y < F.y;
+                       if (valid) {
+                         acc[0] += 1;
+                         acc[1] += found != kInvalid;
+                         acc[2] += found != kInvalid ? F.w : 0u;
+                         acc[3] += found != kInvalid ? 1 + before : n;
+                       }
+                       const uint64_t i = sl[j];
+                       uint64_t* cd = valid ? cnt + i : sink;
+                       uint32_t* zd = valid ? zo + i : zsink;
+                       uint32_t* pd = valid ? po + i : zsink + 1;
+                       *cd = found != kInvalid ? F.w : 0u;
+                       *zd = F.z;
+                       *pd = row;
+                     }
+                   });
+    block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+    return;
+  }
   seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
            [&] { if (FITS) stage_nested(off, mains, b0, nbs, m0, nm, ldir, lmain); },
            [&](uint32_t hv, uint32_t row, uint64_t i) {
@@ -798,16 +848,18 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
     hq = reinterpret_cast<Heavy*>(nhq + 2);
     if ((e = hipMemsetAsync(nhq, 0, sizeof(uint64_t), s)) != hipSuccess) return e;
   }
+  if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
+  uint64_t* sink = ctx->ctl.as<uint64_t>() + 64;  // ctl words [64, 128): store sink
   {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
     auto launch = [&](auto mode_c) {
       constexpr int M = decltype(mode_c)::value;
       hipLaunchKernelGGL((k_rn_probe_seg<M, true>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
                          pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials);
+                         zo, po, hq, nhq, partials, sink);
       hipLaunchKernelGGL((k_rn_probe_seg<M, false>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
                          pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials);
+                         zo, po, hq, nhq, partials, sink);
       hipLaunchKernelGGL((k_rn_probe_ovf<M>), dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf,
                          pp.seg + uint64_t(pp.G) * pp.P, off, mains, sub, t->fm, lo, o, out_cap, cnt, zo, po, hq, nhq,
                          res);

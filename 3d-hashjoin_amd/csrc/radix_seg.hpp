@@ -75,7 +75,10 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
           }
         }
         const uint2* src = region + region_idx(g_lo + wid + kWaves * r, p, G, P) * cap;
-        v[j] = f < total ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + (f - pr))) : 0ull;
+        // unconditional (an absent item reads the region base): a fixed load count per chunk, so
+        // waiting for it needs no vmcnt(0)
+        const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(f < total ? src + (f - pr) : region));
+        v[j] = f < total ? x : 0ull;
         slot[j] = sg + (f - pr);
       }
     };
@@ -122,7 +125,9 @@ __device__ __forceinline__ void seg_walk(const uint2* __restrict__ region, const
 #pragma unroll
     for (int j = 0; j < kSegItems; ++j) {
       const uint32_t k = qq + j * 64 + lane;
-      v[j] = (rr < nr && k < ll) ? __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(src + k)) : 0ull;
+      const bool ok = rr < nr && k < ll;
+      const uint64_t x = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(ok ? src + k : region));
+      v[j] = ok ? x : 0ull;
     }
   };
   uint64_t cur[kSegItems];
