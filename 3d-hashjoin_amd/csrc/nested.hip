@@ -256,6 +256,10 @@ constexpr uint32_t kHeavyOut = 8192;
 #define HJ3D_EXP_U 4  // k_expand_light: outputs per thread and step (1: one at a time, A/B)
 #endif
 constexpr int kExpU = HJ3D_EXP_U;
+#ifndef HJ3D_RN_XCD
+#define HJ3D_RN_XCD 1  // nested probe on slices wider than LDS: shared slices, XCD-ordered blocks (0: A/B)
+#endif
+constexpr uint32_t kHbmSplits = 16;  // workgroups per wide slice (one region stream per wave at G = 256)
 #ifndef HJ3D_RN_STATIC
 #define HJ3D_RN_STATIC 1  // k_rn_probe_seg, materialised unnest: fixed store count per chunk (0: A/B)
 #endif
@@ -547,9 +551,15 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
                                                           uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
                                                           uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
                                                           uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials,
-                                                          uint64_t* __restrict__ sink) {
+                                                          uint64_t* __restrict__ sink, bool xcd) {
   __shared__ uint32_t lds[kProbeLdsWords];
-  const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
+  // xcd: workgroup b runs on XCD b % 8; XCD x takes the x-th eighth of the (slice, share) pairs
+  uint32_t bid = blockIdx.x;
+  if (xcd) {
+    const uint32_t per = gridDim.x / 8;
+    if (bid < per * 8) bid = (bid % 8) * per + bid / 8;
+  }
+  const uint32_t p = bid / splits, sp = bid % splits;
   const uint32_t b0 = p * W;
   const uint32_t nbs = min(W, nbl - b0);
   const uint32_t m0 = off[b0], nm = off[b0 + nbs] - m0;
@@ -810,9 +820,15 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   const double fill = double(t->n_mains) / double(nbl);
   ProbeParts pp;
   unsigned long long* npass = nullptr;  // fused selection: tuples passing it (n_probe)
-  if ((e = radix_partition_probe(ctx, t, r, uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill)), &pp, s, sel,
-                                 sel ? &npass : nullptr)) != hipSuccess)
-    return e;
+  const uint32_t w_fit = uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill));
+  if ((e = radix_partition_probe(ctx, t, r, w_fit, &pp, s, sel, sel ? &npass : nullptr)) != hipSuccess) return e;
+  // slices wider than LDS (more than the partitioner's 2048 slices at the fitting width: config D's
+  // 1e8-bucket table) are probed through the cache. Then kHbmSplits workgroups share each slice and
+  // the blocks are ordered so that an XCD's workgroups take consecutive (slice, share) pairs: the
+  // ~32 workgroups of an XCD work on two slices at a time, whose directory and main records
+  // (~1 MB each) stay in its 4 MB L2 instead of 32 different slices thrashing it.
+  const bool wide = HJ3D_RN_XCD && pp.W > w_fit && pp.splits < kHbmSplits && pp.G >= kHbmSplits;
+  if (wide) pp.splits = kHbmSplits;
   const uint32_t nblocks = pp.P * pp.splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
@@ -856,10 +872,10 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
       constexpr int M = decltype(mode_c)::value;
       hipLaunchKernelGGL((k_rn_probe_seg<M, true>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
                          pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials, sink);
+                         zo, po, hq, nhq, partials, sink, wide);
       hipLaunchKernelGGL((k_rn_probe_seg<M, false>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
                          pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials, sink);
+                         zo, po, hq, nhq, partials, sink, wide);
       hipLaunchKernelGGL((k_rn_probe_ovf<M>), dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf,
                          pp.seg + uint64_t(pp.G) * pp.P, off, mains, sub, t->fm, lo, o, out_cap, cnt, zo, po, hq, nhq,
                          res);
