@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--layout", default="tuples", choices=["tuples", "pairs", "tuples_rows"],
                     help="probe side: 12-B tuples with implicit rows (config B), received {key, row} pairs "
                          "(8 B, explicit rows: a rank of the multi-GPU strand), or 12-B tuples with an explicit row word")
+    ap.add_argument("--chunks", type=int, default=1, help="probe S as this many contiguous chunks (accumulated)")
     ap.add_argument("--label", default=os.path.basename(os.path.dirname(os.environ.get("HJ3D_LIB", "default/x"))))
     a = ap.parse_args()
     import torch
@@ -46,22 +47,33 @@ def main():
         relS = hj3d.Rel(P2, key_word=0, row_word=1)
     elif a.layout == "tuples_rows":
         relS = hj3d.Rel(S, key_word=1, row_word=0)
+    def probe_all():
+        if a.chunks <= 1:
+            ctx.probe(t, relS, unique=True, out=out, fetch=False)
+            return
+        assert a.layout == "tuples"
+        for c in range(a.chunks):
+            lo, hi = nS * c // a.chunks, nS * (c + 1) // a.chunks
+            rc = hj3d.Rel(S[lo:hi], 1, row_base=lo)
+            ctx.probe(t, rc, unique=True, out=None if out is None else out[lo:hi], fetch=False, accumulate=c > 0)
+
     for _ in range(3):
         t.build(relR)
-        ctx.probe(t, relS, unique=True, out=out, fetch=False)
+        probe_all()
     ctx.sync()
     ctx.timing(True)
     ctx.timer_reset()
     for _ in range(a.reps):
         t.build(relR)
-        ctx.probe(t, relS, unique=True, out=out, fetch=False)
+        probe_all()
     ctx.sync()
-    res = {"label": a.label, "compact": a.compact, "layout": a.layout, "nR": nR, "nS": nS, "emit": out is not None}
+    res = {"label": a.label, "compact": a.compact, "layout": a.layout, "nR": nR, "nS": nS, "emit": out is not None,
+           "chunks": a.chunks}
     for k, ph in (("build", hj3d.T_BUILD), ("probe", hj3d.T_PROBE), ("k_pk_part", hj3d.T_SCATTER),
                   ("k_pk_split", hj3d.T_HIST), ("k_pk_probe", hj3d.T_PROBE_KERNEL)):
         ms, cnt = ctx.timer(ph)
         if cnt:
-            res[k] = round(ms / cnt, 4)
+            res[k] = round(ms / a.reps, 4)  # per step (all chunks)
     r = ctx.probe_result()
     res["n_out"] = r.n_out
     print(json.dumps(res), flush=True)
