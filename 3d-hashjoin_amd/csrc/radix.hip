@@ -62,6 +62,9 @@ __device__ __forceinline__ void nt_st(uint32_t* p, uint32_t v) {
 __device__ __forceinline__ uint32_t key_ld(const RelView& r, uint64_t i) { return HJ3D_NT_BUILD ? r.key_nt(i) : r.key(i); }
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
+#ifndef HJ3D_PROBE_WAVES
+#define HJ3D_PROBE_WAVES 1  // partitioned probes: slice count rounded up to whole waves of workgroups (0: A/B)
+#endif
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
 constexpr uint32_t kSortedMax = 32;             // buckets up to this size are kept sorted by row
 
@@ -1194,6 +1197,20 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   // more than kMaxParts slices: wider slices that no longer fit LDS (probed through L2 by the
   // non-fitting kernel, still one bucket range per workgroup)
   if ((uint64_t(nbl) + W - 1) / W > kMaxParts) W = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
+  if (HJ3D_PROBE_WAVES) {
+    // the probe runs one LDS-bound workgroup per CU and slice: round the slice count up to whole
+    // waves of workgroups (narrower slices), so no last wave of a few slices costs a full one
+    // (config C: 1302 slices = 5.1 waves -> 1536 = 6). Not past the whole-segment partitioner's
+    // 1024 slices nor the plain one's 2048.
+    const uint32_t G = uint32_t(ctx->num_cus);
+    const uint32_t P0 = uint32_t((uint64_t(nbl) + W - 1) / W);
+    uint32_t P1 = (P0 + G - 1) / G * G;
+    if (P0 <= 1024 && P1 > 1024) P1 = 1024;
+    if (P0 >= G && P1 <= kMaxParts && P1 > P0) {
+      const uint32_t W1 = uint32_t((uint64_t(nbl) + P1 - 1) / P1);
+      if (W1 >= 64) W = W1;
+    }
+  }
   Plan pl = plan_for(nbl, W, r.n);
   const uint32_t P = pl.P;
   if (P > kMaxParts) return hipErrorNotSupported;
