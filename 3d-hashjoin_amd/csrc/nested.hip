@@ -259,7 +259,10 @@ constexpr int kExpU = HJ3D_EXP_U;
 #ifndef HJ3D_RN_XCD
 #define HJ3D_RN_XCD 1  // nested probe on slices wider than LDS: shared slices, XCD-ordered blocks (0: A/B)
 #endif
-constexpr uint32_t kHbmSplits = 16;  // workgroups per wide slice (one region stream per wave at G = 256)
+#ifndef HJ3D_RN_SPLITS
+#define HJ3D_RN_SPLITS 16  // workgroups per wide slice (16: one region stream per wave at G = 256)
+#endif
+constexpr uint32_t kHbmSplits = HJ3D_RN_SPLITS;
 #ifndef HJ3D_RN_STATIC
 #define HJ3D_RN_STATIC 1  // k_rn_probe_seg, materialised unnest: fixed store count per chunk (0: A/B)
 #endif
