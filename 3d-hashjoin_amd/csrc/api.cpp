@@ -161,6 +161,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_PK: ctx->nested_pk = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_COMPACT: ctx->pk_compact = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_SYNC_BUILD: ctx->sync_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);
@@ -326,10 +327,13 @@ hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d
   if (count == 2 && tables[0]->desc.kind == HJ3D_NESTED && tables[1]->desc.kind == HJ3D_NESTED &&
       !ctx->nested_sort && !ctx->nested_pk && !nested_radix_applicable(ctx, tables[0], builds[0].n) &&
       !nested_radix_applicable(ctx, tables[1], builds[1].n)) {
-    PhaseTimer tm(ctx, HJ3D_T_BUILD);
+    hipError_t e;
     const char* path = "nested_agg";
-    for (uint32_t k = 0; k < 2; ++k) tables[k]->pending = false;
-    hipError_t e = nested_build_agg_many(ctx, tables, builds, 2, ctx->stream, &path);
+    {
+      PhaseTimer tm(ctx, HJ3D_T_BUILD);
+      for (uint32_t k = 0; k < 2; ++k) tables[k]->pending = false;
+      e = nested_build_agg_many(ctx, tables, builds, 2, ctx->stream, &path);
+    }
     if (e == hipErrorOutOfMemory) {
       (void)hipGetLastError();
       e = hipErrorNotSupported;
@@ -340,6 +344,7 @@ hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d
         e = nested_pending(ctx, tables[k], builds[k], true);
       }
       for (uint32_t k = 0; k < 2; ++k) tables[k]->built = e == hipSuccess;
+      for (uint32_t k = 0; k < 2 && e == hipSuccess && ctx->sync_build; ++k) e = table_resolve(ctx, tables[k]);
       return from_hip(ctx, e, "hj3d_build_many");
     }
   }
@@ -350,10 +355,9 @@ hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d
   return HJ3D_OK;
 }
 
-hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
-  if (!ctx || !t) return HJ3D_EINVAL;
-  if (!rel_ok(build)) return fail(ctx, HJ3D_EINVAL, "hj3d_build: invalid relation");
-  if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
+}  // extern "C"
+
+static hipError_t build_one(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
   t->pending = false;  // a build in flight for the old content is replaced (its copy stays stream-ordered)
@@ -401,6 +405,18 @@ hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
     if (e == hipSuccess) e = nested_pending(ctx, t, *build, agg);
   }
   t->built = e == hipSuccess;
+  return e;
+}
+
+extern "C" {
+
+hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  if (!rel_ok(build)) return fail(ctx, HJ3D_EINVAL, "hj3d_build: invalid relation");
+  if (build->n >= (1ull << 32)) return fail(ctx, HJ3D_EUNSUPPORTED, "hj3d_build: more than 2^32-1 build tuples");
+  hipError_t e = build_one(ctx, t, build);
+  // HJ3D_OPT_SYNC_BUILD: finished here (its own timer interval if the sort build has to run)
+  if (e == hipSuccess && ctx->sync_build) e = table_resolve(ctx, t);
   return from_hip(ctx, e, "hj3d_build");
 }
 
@@ -418,6 +434,8 @@ hipError_t table_resolve(hj3d_ctx* ctx, hj3d_table* t) {
   uint64_t hc[4];
   std::memcpy(hc, t->hc, sizeof(hc));
   if (t->pending_agg && uint32_t(hc[3]) != 0) {  // a key range too dense for the LDS table
+    // the rest of the build: timed as build work (not inside the probe that triggered it)
+    PhaseTimer tm(ctx, HJ3D_T_BUILD);
     t->path = "nested_sort";
     e = nested_build(ctx, t, t->pending_rel, ctx->stream);
     if (e == hipSuccess) e = hipMemcpyAsync(hc, t->counts.p, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream);
@@ -436,8 +454,17 @@ static hipError_t resolve(hj3d_ctx* ctx, const hj3d_table* t) {
 extern "C" {
 
 const char* hj3d_table_build_path(const hj3d_table* t) {
-  if (t && t->pending && t->pending_ctx) (void)resolve(t->pending_ctx, t);
-  return t && t->built ? t->path : "none";
+  if (!t || !t->built) return "none";
+  if (!t->pending) return t->path;
+  // not resolved yet: the started path, marked (no wait, no build from a read-only getter)
+  hj3d_table* w = const_cast<hj3d_table*>(t);
+  std::snprintf(w->path_buf, sizeof(w->path_buf), "%s?", t->path);
+  return w->path_buf;
+}
+
+hj3d_status hj3d_table_finish(hj3d_ctx* ctx, hj3d_table* t) {
+  if (!ctx || !t) return HJ3D_EINVAL;
+  return from_hip(ctx, table_resolve(ctx, t), "hj3d_table_finish");
 }
 
 hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off, void* payload, uint32_t* sub,

@@ -376,8 +376,10 @@ hj3d_status hj3d_comm_exchange_strided(hj3d_ctx* ctx, const void* send_dev, uint
   if (!c || !send_counts || !recv_counts || !elem_bytes) return HJ3D_EINVAL;
   uint64_t ns = 0, nr = 0;
   for (int p = 0; p < c->world; ++p) {
-    // a count above the stride is an argument error every rank can see coming only for its own
-    // sends: hj3d_partition_strided never writes one (stride >= its relation's size)
+    // a count above the stride means hj3d_partition_strided spilled (a bounded stride, skewed
+    // keys): the caller must check every count against the stride and re-partition BEFORE any rank
+    // calls this (hj3d.h). Refused here only on this rank, so a caller that skipped the check
+    // leaves its peers waiting in the collective.
     if (send_counts[p] < 0 || recv_counts[p] < 0 || (send_stride && uint64_t(send_counts[p]) > send_stride))
       return HJ3D_EINVAL;
     ns += uint64_t(send_counts[p]);

@@ -85,6 +85,7 @@ struct hj3d_ctx {
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
+  bool sync_build = false;        // HJ3D_OPT_SYNC_BUILD: nested builds resolved before hj3d_build returns
   bool pk_compact = false;        // HJ3D_OPT_PK_COMPACT: the packed probe's compact slice image where it applies
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
@@ -116,6 +117,7 @@ struct hj3d_table {
   uint64_t n_mains = 0;   // nested: main records (distinct keys) of the last build (host-known)
   bool built = false;
   const char* path = "none";  // which build made the table (hj3d_table_build_path)
+  char path_buf[40] = {0};    // hj3d_table_build_path of a table not resolved yet: path + "?"
   // build rows lie in [row_lo, row_lo + row_rr) (implicit-row builds; 0: unknown): the compact
   // probe image packs q * row_rr + (row - row_lo) into one word
   uint32_t row_lo = 0;

@@ -362,7 +362,12 @@ hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, 
   // the ticket: a control word kept zero between calls (the last tile resets it)
   uint32_t* ticket = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + kCtlScanTicket);
   ctx->scan_epoch = (ctx->scan_epoch + 1) & ((1u << 28) - 1);  // below the u64 form's flag bits
-  if (ctx->scan_epoch == 0) ctx->scan_epoch = 1;  // 0 is the epoch of cleared memory
+  if (ctx->scan_epoch == 0) {
+    // wrapped: words published 2^28 calls ago carry epochs the next calls will use again, so the
+    // buffer starts over from cleared memory (epoch 0) before epoch 1 is reused
+    ctx->scan_epoch = 1;
+    if ((e = hipMemsetAsync(st.p, 0, st.bytes, s)) != hipSuccess) return e;
+  }
   const uint32_t epoch = ctx->scan_epoch;
   hipLaunchKernelGGL(k_scan_lb, dim3(unsigned(tiles)), dim3(kBlock), 0, s, in, out, n,
                      st.as<uint64_t>(), ticket, epoch, uint32_t(tiles));

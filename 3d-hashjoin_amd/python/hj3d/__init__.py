@@ -27,7 +27,7 @@ PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
 OPT_PROBE_ITEMS = 7
-OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_PK_COMPACT = 8, 9, 10, 11, 12
+OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_PK_COMPACT, OPT_SYNC_BUILD = 8, 9, 10, 11, 12, 13
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -116,6 +116,7 @@ def lib():
         "hj3d_build": (st, [p, p, R]),
         "hj3d_build_many": (st, [p, C.POINTER(p), R, u32]),
         "hj3d_table_build_path": (C.c_char_p, [p]),
+        "hj3d_table_finish": (st, [p, p]),
         "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
         "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe": (st, [p, p, R, u32, p, u64]),
@@ -398,6 +399,11 @@ class Context:
         """The packed probe's compact slice image (two 512-thread workgroups per CU) where it applies."""
         self.set_option(OPT_PK_COMPACT, int(on))
 
+    def sync_build(self, on: bool = True):
+        """Nested builds finished inside hj3d_build (HJ3D_OPT_SYNC_BUILD): the build relation may
+        be released when the call returns."""
+        self.set_option(OPT_SYNC_BUILD, int(on))
+
     def nested_pk(self, on: bool = True):
         """Nested aggregation builds always on the packed partitioner's slices (the form tables of
         more than 2048 partitions take; tests)."""
@@ -677,8 +683,15 @@ class Table:
     def clear(self):
         self.ctx._check(lib().hj3d_table_clear(self.ctx.h, self.h), "hj3d_table_clear")
 
-    def build_path(self) -> str:
-        """Which build made the table (hj3d_table_build_path)."""
+    def finish(self):
+        """Finish a nested build now (hj3d_table_finish): counts read, sort-build fallback run."""
+        self.ctx._check(lib().hj3d_table_finish(self.ctx.h, self.h), "hj3d_table_finish")
+
+    def build_path(self, finish: bool = True) -> str:
+        """Which build made the table (hj3d_table_build_path); finish=True resolves a pending
+        nested build first, else a pending one reads as the started path + "?"."""
+        if finish:
+            self.finish()
         return lib().hj3d_table_build_path(self.h).decode()
 
     def stats(self) -> dict:

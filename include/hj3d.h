@@ -188,7 +188,12 @@ enum {
    * two 512-thread workgroups per CU, where the table's build rows are implicit (a known row range)
    * and the slice fits. Measured slower at config B (0.61 against 0.49 ms), so off by default; kept
    * for A/B measurements and its parity test. */
-  HJ3D_OPT_PK_COMPACT = 12
+  HJ3D_OPT_PK_COMPACT = 12,
+  /* HJ3D_OPT_SYNC_BUILD (0/1, default 0): hj3d_build / hj3d_build_many finish a nested table before
+   * they return (they wait for its counts and run the sort build there if the LDS aggregation build
+   * gave up), so the build relation's device memory may be released as soon as the call returns.
+   * Default: the table finishes at its next use (see hj3d_build). */
+  HJ3D_OPT_SYNC_BUILD = 13
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
@@ -224,7 +229,8 @@ hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t);
 /* Build: replaces the table content with the tuples of `build` (asynchronous). A nested table's
  * build finishes at the table's next use (probe, statistics, export): its counts are read then, and
  * when the LDS aggregation build gave up on a key range too dense for it, the sort build runs then,
- * from `build` again -- so the build relation's device memory must stay valid until that use. */
+ * from `build` again -- so the build relation's device memory must stay valid until that use (or set
+ * HJ3D_OPT_SYNC_BUILD). That fallback build is timed as HJ3D_T_BUILD, not as part of the probe. */
 hj3d_status hj3d_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build);
 /* Builds several tables, tables[k] from builds[k] (asynchronous; as hj3d_build for each). Two nested
  * tables of one geometry (equal num_buckets and bucket range: experiment 4's S and T tables,
@@ -250,8 +256,14 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
 /* Which build made the table's current content (diagnostic, static string): chaining "radix",
  * "slices" (pk_slices, tables beyond the radix build's range) or "direct"; nested "nested_agg",
  * "nested_agg_slices" (more than 2048 partitions), "nested_sort" or "nested_radix"; "none" before a
- * build. Replaces nothing of the reference (which has one insert path). */
+ * build. A nested table whose build has not been resolved yet (no use since hj3d_build) reports the
+ * path that was started, with "?" appended ("nested_agg?"): the getter never waits or builds. Replaces
+ * nothing of the reference (which has one insert path). */
 const char* hj3d_table_build_path(const hj3d_table* t);
+/* Finishes a nested table's build now (waits for its counts; runs the sort build from the build
+ * relation if the LDS aggregation build gave up), as its next use would. No-op for a finished table.
+ * Replaces nothing of the reference (whose insert is synchronous). */
+hj3d_status hj3d_table_finish(hj3d_ctx* ctx, hj3d_table* t);
 /* Synchronous statistics (makeStatistics). */
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out);
 /* Number of tuples / distinct keys currently stored (synchronous). */
@@ -357,7 +369,10 @@ hj3d_status hj3d_comm_exchange(hj3d_ctx* ctx, const void* send_dev, const int64_
                                const int64_t* recv_counts, uint64_t recv_cap, uint32_t elem_bytes,
                                uint32_t* ticket);
 /* The same with peer p's elements at send_dev + p * send_stride elements (hj3d_partition_strided's
- * layout; send_stride = 0: back to back); a send count above send_stride is HJ3D_EINVAL. */
+ * layout; send_stride = 0: back to back); a send count above send_stride is HJ3D_EINVAL.
+ * MANDATORY before this call on every rank: check the partitioner's counts against the stride and
+ * re-partition a spilled chunk (hj3d_partition_strided above). The EINVAL is local to the rank
+ * that spilled; its peers, already inside the collective, would wait for it forever. */
 hj3d_status hj3d_comm_exchange_strided(hj3d_ctx* ctx, const void* send_dev, uint64_t send_stride,
                                        const int64_t* send_counts, void* recv_dev, const int64_t* recv_counts,
                                        uint64_t recv_cap, uint32_t elem_bytes, uint32_t* ticket);

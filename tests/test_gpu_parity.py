@@ -492,3 +492,59 @@ def _fmix32_u64(x):
     x = (x * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
     x ^= x >> np.uint64(16)
     return x
+
+
+@pytest.mark.parametrize("sync", [False, True], ids=["lazy", "sync"])
+@pytest.mark.parametrize("dense", [0, 1])
+def test_build_many_one_table_gives_up(ctx, dense, sync):
+    """hj3d_build_many over two nested tables of one geometry where table `dense` holds ~50 keys
+    per bucket (the LDS aggregation build gives up; the sort build replaces that table) and the
+    other ~2 (aggregation build kept). Both tables' statistics and probe counters equal the
+    oracle's. Lazy: the replacement runs at the table's next use, is timed as HJ3D_T_BUILD (not as
+    probe work), and build_path(finish=False) reports the started path with "?". Sync
+    (HJ3D_OPT_SYNC_BUILD): the tables are finished inside the call, so the build relations are
+    overwritten and released before the first use."""
+    import torch
+    import hj3d
+    rng = np.random.default_rng(17 + dense)
+    nb, n = 2000, 400_000
+    dom = (100_000, 4_000) if dense == 0 else (4_000, 100_000)
+    rels = [O.tuples3(np.arange(n, dtype=np.uint32), rng.integers(0, d, n, dtype=np.uint32)) for d in dom]
+    P = O.tuples3(np.arange(120_000, dtype=np.uint32) % 110_000, np.zeros(120_000, dtype=np.uint32))
+    exp = [O.nested_plan(r, 1, P, 0, nb, True) for r in rels]
+    ctx.radix_min(0)
+    ctx.sync_build(sync)
+    ctx.timing(True)
+    try:
+        ts = [hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb) for _ in range(2)]
+        dr = [dev(r) for r in rels]
+        ctx.build_many(ts, [hj3d.Rel(d, 1) for d in dr])
+        if sync:
+            assert not ts[dense].build_path(finish=False).endswith("?")
+            for d in dr:
+                d.fill_(-1)
+            del dr
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+        else:
+            assert ts[dense].build_path(finish=False) == "nested_agg?"
+        ctx.sync()
+        ctx.timer_reset()
+        dP = dev(P)
+        for k in range(2):
+            got = ctx.probe(ts[k], hj3d.Rel(dP, 0), unnest=True)
+            e = exp[k]
+            assert (got.n_matched, got.n_cmps, got.n_out) == (e.c_probe, e.c_cmp, e.c_unnest), k
+            assert {f: getattr(got, f) for f in ("sum_a", "sum_b", "sum_h", "xor_h")} == \
+                {f: e.out[f] for f in ("sum_a", "sum_b", "sum_h", "xor_h")}, k
+            assert {f: ts[k].stats()[f] for f in STAT_KEYS} == {f: e.stats[f] for f in STAT_KEYS}, k
+        build_ms, build_cnt = ctx.timer(hj3d.T_BUILD)
+        assert build_cnt == (0 if sync else 1)  # the fallback build, counted as build work
+        assert ts[dense].build_path() == "nested_sort"
+        assert ts[1 - dense].build_path() == "nested_agg"
+        for t in ts:
+            t.close()
+    finally:
+        ctx.timing(False)
+        ctx.sync_build(False)
+        ctx.radix_min(1 << 20)
