@@ -71,6 +71,9 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_DIAG
 #define HJ3D_NAGG_DIAG 0  // diagnostic variants (tables wrong): 1 pass B without its sub-row stores, 2 without pass B
 #endif
+#ifndef HJ3D_NAGG_REG
+#define HJ3D_NAGG_REG 1  // slices of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
+#endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
@@ -189,13 +192,12 @@ struct NaggTabs {
   uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
   uint32_t* sink = nullptr;  // pass B's stores of items without a row (the context's store-sink words)
 };
+// one partition (global index gp) of k_nagg
 template <int BLOCK, int SLOTS, bool PK>
-__global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
-                                                uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
-                                                const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
-                                                NaggTabs tabs) {
-  extern __shared__ uint32_t agg_lds[];
+__device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                         FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
+                                         uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount, uint32_t cap,
+                                         const NaggSrc& src, const NaggTabs& tabs, uint32_t* agg_lds) {
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
   uint32_t* tmin = tcnt + cap;   // min row, then (after the main records are written) unused
@@ -205,7 +207,6 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
   uint32_t& ovf = wsum[BLOCK / kWave + 1];
   uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
   const uint32_t limit = cap - BLOCK - 64;
-  const uint32_t gp = PK ? blockIdx.x : order[blockIdx.x];  // partition over all tables
   const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
   const uint32_t p = gp - ti * tabs.P;                      // partition inside table ti
   uint32_t* __restrict__ off = tabs.off[ti];
@@ -468,6 +469,258 @@ __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs,
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
 }
 
+// One workgroup per partition (gp = blockIdx.x, or order[blockIdx.x]), or, with `list` ({count,
+// partition ids...}: the partitions k_nagg_reg deferred), a grid looping over the listed ones.
+template <int BLOCK, int SLOTS, bool PK>
+__global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
+                                                uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
+                                                const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
+                                                NaggTabs tabs, const uint32_t* __restrict__ list) {
+  extern __shared__ uint32_t agg_lds[];
+  if (!list) {
+    nagg_one<BLOCK, SLOTS, PK>(PK || !order ? blockIdx.x : order[blockIdx.x], pairs, ps, fm, lo, nbl, nb_global, W,
+                               mtmp, dcount, cap, src, tabs, agg_lds);
+    return;
+  }
+  const uint32_t nwork = list[0];
+  for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
+    nagg_one<BLOCK, SLOTS, PK>(list[1 + w], pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs, agg_lds);
+    __syncthreads();
+  }
+}
+
+// ---- k_nagg_reg: the partition held in registers, its sub rows assembled in LDS ----
+// k_nagg streams every partition twice from HBM (pass A, pass B) and scatters each sub row with a
+// 4-B store into the partition's sub window, whose lines the L2 evicts before they are complete
+// (3.8x write amplification at config C). Here one persistent 1024-thread workgroup per CU takes
+// partitions (slices) q = blockIdx.x, + gridDim.x, ...: a partition of <= kRegCap pairs is loaded
+// into registers ONCE (the next partition's loads are issued as soon as pass B has read them, and
+// overlap the image write-out and the next table's initialisation), pass A and pass B run on the
+// registers, pass B places every row into an LDS image of the partition's sub range, and the image
+// goes out as whole lines. Per pair: 8 B
+// read + 4 B written. A partition with more pairs than kRegCap, or more distinct keys than the
+// table holds, is appended to `defer` ({count, ids...}) and left to k_nagg (list form) afterwards.
+#ifndef HJ3D_NAGG_REGK
+#define HJ3D_NAGG_REGK 16
+#endif
+constexpr int kRegBlock = 1024;
+constexpr int kRegK = HJ3D_NAGG_REGK;                          // pairs per lane and buffer
+constexpr uint32_t kRegCap = uint32_t(kRegK) * kRegBlock;      // pairs per partition (16384)
+__host__ __device__ constexpr uint32_t reg_lds_words(uint32_t cap, uint32_t W) {
+  return 3 * cap + W + kRegCap + kRegBlock / 64 + 2 + 2 * (kAggMaxS2 + 2);
+}
+template <bool PK, int SLOTS>
+__global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global,
+                                                        uint32_t W, uint32_t P, uint4* __restrict__ mtmp,
+                                                        uint32_t* __restrict__ dcount, uint32_t cap, NaggSrc src,
+                                                        NaggTabs tabs, uint32_t* __restrict__ defer) {
+  extern __shared__ uint32_t agg_lds[];
+  uint32_t* tkey = agg_lds;
+  uint32_t* tcnt = tkey + cap;
+  uint32_t* tmin = tcnt + cap;
+  uint32_t* bcnt = tmin + cap;
+  uint32_t* img = bcnt + W;
+  uint32_t* wsum = img + kRegCap;
+  uint32_t& nkeys = wsum[kRegBlock / kWave];
+  uint32_t& ovf = wsum[kRegBlock / kWave + 1];
+  uint32_t* rst = wsum + kRegBlock / kWave + 2;  // [2][kAggMaxS2 + 2]: region starts of the two buffers' slices
+  const uint32_t limit = cap - kRegBlock - 64;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  uint32_t* __restrict__ off = tabs.off[0];
+  uint32_t* __restrict__ sub = tabs.sub[0];
+  auto* maxlen = reinterpret_cast<unsigned long long*>(tabs.counts[0] + 2);
+  uint32_t mxlen = 0;
+  // region starts of slice q into rst[b] (PK; wave 0)
+  const auto starts = [&](uint32_t q, uint32_t b) __attribute__((always_inline)) {
+    if constexpr (PK) {
+      if (wid == 0 && q < P) {
+        const uint32_t len = uint32_t(lane) < src.S2 ? src.fcnt[uint64_t(lane) * src.pk.P + q] : 0u;
+        uint32_t tot;
+        const uint32_t pre = wave_excl_scan(len, &tot);
+        uint32_t* r = rst + b * (kAggMaxS2 + 2);
+        if (uint32_t(lane) < src.S2) r[lane] = pre;
+        if (lane == 0) {
+          r[src.S2] = tot;
+          r[src.S2 + 1] = tot;
+        }
+      }
+    }
+  };
+  const auto count_of = [&](uint32_t q, uint32_t b) __attribute__((always_inline)) {
+    if constexpr (PK) return rst[b * (kAggMaxS2 + 2) + src.S2];
+    else return ps[q + 1] - ps[q];
+  };
+  // kRegK loads per lane, always (indices clamped to the slice's last pair; a slice of more than
+  // kRegCap pairs is deferred, so its registers are never used)
+  const auto load = [&](uint32_t q, uint32_t b, uint2 (&v)[kRegK]) __attribute__((always_inline)) {
+    if (q >= P) return;  // (past the last slice: rst[b] was not written)
+    const uint32_t m = count_of(q, b);
+    const uint32_t last = m ? m - 1 : 0u;
+    if constexpr (PK) {
+      const uint32_t* r = rst + b * (kAggMaxS2 + 2);
+      uint32_t cr = 0;
+#pragma unroll
+      for (int u = 0; u < kRegK; ++u) {
+        const uint32_t f = min(uint32_t(u) * kRegBlock + threadIdx.x, last);
+        while (cr + 1 < src.S2 && f >= r[cr + 1]) ++cr;
+        v[u] = src.fine[(uint64_t(cr) * src.pk.P + q) * src.cap2 + (f - r[cr])];
+      }
+    } else {
+      const uint32_t e0 = ps[q];
+#pragma unroll
+      for (int u = 0; u < kRegK; ++u) v[u] = pairs[e0 + min(uint32_t(u) * kRegBlock + threadIdx.x, last)];
+    }
+  };
+  uint2 v[kRegK];
+  const auto process = [&](uint32_t q, uint32_t b, uint32_t qn) __attribute__((always_inline)) {
+    const uint32_t b0 = q * W, nbs = min(W, nbl - b0);
+    const uint32_t e0 = ps[q], m = count_of(q, b);
+    const uint32_t empty = PK ? (nbs << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + nbs) % nb_global);
+    const auto lbk = [&](uint32_t x) __attribute__((always_inline)) {
+      if constexpr (PK) return x >> src.pk.qbits;
+      else return fm.mod(x) - lo - b0;
+    };
+    for (uint32_t s = threadIdx.x; s < cap; s += kRegBlock) {
+      tkey[s] = empty;
+      tcnt[s] = 0;
+      tmin[s] = kInvalid;
+    }
+    for (uint32_t k = threadIdx.x; k < nbs; k += kRegBlock) bcnt[k] = 0;
+    if (threadIdx.x == 0) {
+      nkeys = 0;
+      ovf = m > kRegCap;
+    }
+    starts(qn, b ^ 1u);  // the next slice's region starts (PK)
+    __syncthreads();
+    const bool big = m > kRegCap;
+    // ---- pass A: count and min row per key (registers) ----
+    if (!big) {
+#pragma unroll
+      for (int u0 = 0; u0 < kRegK; u0 += 8) {
+        uint32_t actm = 0, k0[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool a = uint32_t(u0 + u) * kRegBlock + threadIdx.x < m;
+          actm |= uint32_t(a) << u;
+          k0[u] = tkey[a ? slot_of(v[u0 + u].x, cap) : 0u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const uint2 e = v[u0 + u];
+          bool a = (actm >> u) & 1u;
+          const uint64_t am = __ballot(a);
+          if (am) {  // the wave's first active key, if several lanes hold it (a hot key)
+            const int leader = __ffsll((unsigned long long)am) - 1;
+            const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(e.x), leader));
+            const bool mine = a && e.x == hl;
+            const uint64_t same = __ballot(mine);
+            if (__popcll(same) > 1) {
+              const uint32_t rmin = wave_min_u32(mine ? e.y : kInvalid);
+              if (lane == leader) {
+                const uint32_t s = tab_insert(tkey, hl, empty, &nkeys, cap, limit);
+                if (s == kInvalid) {
+                  ovf = 1;
+                } else {
+                  atomicAdd(&tcnt[s], uint32_t(__popcll(same)));
+                  atomicMin(&tmin[s], rmin);
+                }
+              }
+              a = a && !mine;
+            }
+          }
+          if (a) {
+            const uint32_t s = k0[u] == e.x ? slot_of(e.x, cap) : tab_insert(tkey, e.x, empty, &nkeys, cap, limit);
+            if (s == kInvalid) {
+              ovf = 1;
+            } else {
+              atomicAdd(&tcnt[s], 1u);
+              atomicMin(&tmin[s], e.y);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (ovf) {  // too many pairs or keys for this form: k_nagg takes the slice afterwards
+      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1u)] = q;
+      load(qn, b ^ 1u, v);
+      return;
+    }
+    // ---- main slots: rank of every key inside its bucket, bucket offsets, sub ranges ----
+    uint32_t rank[SLOTS], cnt[SLOTS];
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * kRegBlock + threadIdx.x;
+      rank[j] = s < cap && tcnt[s] ? atomicAdd(&bcnt[lbk(tkey[s])], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t nk = block_scan_lds<kRegBlock>(bcnt, nbs, wsum);
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * kRegBlock + threadIdx.x;
+      cnt[j] = s < cap ? tcnt[s] : 0u;
+    }
+    __syncthreads();
+    block_scan_lds<kRegBlock>(tcnt, cap, wsum);  // tcnt: the key's first slot in the image
+    const uint32_t sb = e0 - tabs.pbase[0];       // the slice's sub range starts at its first pair
+#pragma unroll
+    for (int j = 0; j < SLOTS; ++j) {
+      const uint32_t s = j * kRegBlock + threadIdx.x;
+      if (cnt[j]) {
+        const uint32_t h = tkey[s];
+        uint32_t hash;
+        if constexpr (PK) hash = src.pk.hash_of(h, q);
+        else hash = h;
+        mtmp[e0 + bcnt[lbk(h)] + rank[j]] = make_uint4(hash, tmin[s], sb + tcnt[s], cnt[j]);
+        mxlen = max(mxlen, cnt[j]);
+      }
+    }
+    for (uint32_t k = threadIdx.x; k < nbs; k += kRegBlock) off[b0 + k] = bcnt[k];
+    __syncthreads();
+    // ---- pass B: every row to its key's next image slot ----
+#pragma unroll
+    for (int u = 0; u < kRegK; ++u) {
+      const uint2 e = v[u];
+      bool a = uint32_t(u) * kRegBlock + threadIdx.x < m;
+      const uint64_t am = __ballot(a);
+      if (am) {
+        const int leader = __ffsll((unsigned long long)am) - 1;
+        const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(e.x), leader));
+        const bool mine = a && e.x == hl;
+        const uint64_t same = __ballot(mine);
+        if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive slots
+          uint32_t base = 0;
+          if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl, cap)], uint32_t(__popcll(same)));
+          base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+          if (mine) img[base + uint32_t(__popcll(same & lt))] = e.y;
+          a = a && !mine;
+        }
+      }
+      if (a) img[atomicAdd(&tcnt[tab_find(tkey, e.x, cap)], 1u)] = e.y;
+    }
+    __syncthreads();
+    // the registers are free: the next slice's loads go out now and overlap the image write-out and
+    // the next table's initialisation
+    load(qn, b ^ 1u, v);
+    // ---- the image out: the slice's sub range as whole lines ----
+    for (uint32_t k = threadIdx.x; k < m; k += kRegBlock) sub[sb + k] = img[k];
+    if (threadIdx.x == 0) dcount[q] = nk;
+  };
+  uint32_t q = blockIdx.x;
+  starts(q, 0);
+  __syncthreads();
+  load(q, 0, v);
+  for (uint32_t it = 0; q < P; ++it, q += gridDim.x) {
+    process(q, it & 1u, q + gridDim.x);
+    __syncthreads();
+  }
+  const uint64_t wm = wave_max(uint64_t(mxlen));
+  if (lane == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+}
+
 // order = the partitions by size class, heavy first (> 8x the mean pairs, then > 2x, then the
 // rest), each class in index order: k_nagg takes its partitions in this order, so a Zipf hot
 // key's partition starts in the first wave of workgroups instead of extending the tail. One
@@ -529,8 +782,9 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
-__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail) {
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail, uint32_t* __restrict__ defer) {
   if (threadIdx.x == 0 && ctl[0] != 0) *fail = 1u;  // ctl[0]: chain_pk.hip's overflow count
+  if (threadIdx.x == 0) defer[0] = 0;                // k_nagg_reg's deferred-slice list: empty
   __syncthreads();
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
@@ -610,10 +864,11 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // (n uint4) | starts | key counts, order
   if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(PT) + 4) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSlot].ensure((4 * uint64_t(PT) + 6) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + PT + 1;
+  uint32_t* defer = order + PT + 1;  // k_nagg_reg: {count, deferred slices}
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   NaggTabs tabs;
   tabs.P = P;
@@ -642,7 +897,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
     hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(),
-                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3));
+                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3), defer);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
@@ -671,7 +926,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   };
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
-    for (const void* k : {reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
+    for (const void* k : {reinterpret_cast<const void*>(&k_nagg_reg<true, 4>),
+                          reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, true>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, true>)})
@@ -681,23 +937,38 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
+  // the register form (k_nagg_reg) on the slices, where their expected pairs fit its registers with
+  // room (deferred slices then go through k_nagg's list form below)
+  const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
+  const bool reg = HJ3D_NAGG_REG && pk && double(n) / P <= 0.85 * kRegCap && capr <= 4 * kRegBlock &&
+                   reg_lds_words(capr, W) * 4 <= 160 * 1024;
+  const uint32_t* list = nullptr;
+  if (reg) {
+    const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);
+    hipLaunchKernelGGL((k_nagg_reg<true, 4>), dim3(std::min<uint32_t>(P, G)), dim3(kRegBlock), lds, s, pairs, ps, t->fm,
+                       lo, nbl, nbg, W, P, mtmp, dcount, capr, src, tabs, defer);
+    list = defer;
+    if (path) *path = "nested_agg_slices_reg";
+  }
+  // k_nagg: one workgroup per partition, or (list) a grid over the deferred slices
+  auto grid = [&](uint32_t per_cu) { return list ? std::min<uint32_t>(PT, G * per_cu) : PT; };
   if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
     if (pk)
-      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(grid(2)), dim3(kSmallBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs, list);
     else
       hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs, list);
   } else {
     const uint32_t cap = kAggCapMax;
     const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
     if (pk)
-      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs);
+      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(grid(1)), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap, src, tabs, list);
     else
       hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs);
+                         mtmp, dcount, order, cap, src, tabs, list);
   }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // for its table and the caller, which reads the counts at the table's next use, runs the sort

@@ -213,6 +213,201 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
   }
 }
 
+// The same scatter with WHOLE-SEGMENT write-out into the exact runs k_rp_hist claimed.
+// k_rp_scatter writes each tile's run of a partition as it comes: at ~8 pairs per partition and
+// tile nearly every run starts and ends inside a 64/128-B segment, and the two halves of such a
+// segment reach the L2 from tiles written microseconds apart (the first half evicted by then):
+// partial-line writes, 2.7 TB/s at config C. Here thread p owns partition p (and p + 1024 with
+// PPT = 2): the pairs of a run that do not complete an aligned SEG-pair segment stay in its
+// registers (the carry) and ride in front of the partition's next run, so every store the tiles
+// issue covers a whole segment; only the first segment of the workgroup's run (which starts at the
+// run's exact position: phantom lanes in front of it are skipped) and the last (flushed at the end)
+// are partial -- the lines shared with the neighbouring workgroups' runs. This is k_pk_part's
+// write-out (chain_pk.hip) on exact runs instead of fixed-capacity regions: skewed keys cannot
+// overflow anything, and the output is one contiguous range per partition, as k_rp_scatter's.
+// Tuples: the tiles of k_rp_hist (kPTile = 16384), as two 8192-tuple halves.
+// PPT = 1: P <= 1024, 128-B segments; PPT = 2: P <= 2048, 64-B segments (a smaller carry).
+#ifndef HJ3D_RP_WS
+#define HJ3D_RP_WS 1  // the build-side partition writes whole segments (k_rp_wscatter; 0: k_rp_scatter, A/B)
+#endif
+constexpr int kWsRounds = 8;
+constexpr int kWsSub = kPBlock * kWsRounds;  // 8192 tuples per half tile
+template <int PPT>
+struct WsGeom {
+  static constexpr uint32_t kSeg = PPT == 1 ? 16u : 8u;
+  static constexpr uint32_t kStage = PPT == 1 ? 17408u : 15360u;  // the half tile + carries (pairs)
+};
+template <int PPT, bool EXPL>
+__global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
+                                                         const uint32_t* __restrict__ cur, uint32_t* __restrict__ cur_next,
+                                                         uint32_t* __restrict__ ps, uint2* __restrict__ out) {
+  constexpr uint32_t SEG = WsGeom<PPT>::kSeg, STAGE = WsGeom<PPT>::kStage;
+  __shared__ uint2 stage[STAGE];
+  __shared__ uint32_t loc[kPBlock * PPT];    // per partition: rank counter of the half tile
+  __shared__ uint32_t sbase[kPBlock * PPT];  // per partition: stage slot of the half tile's first pair
+  __shared__ uint2 seginfo[STAGE / SEG];     // whole segment: {output index, stage start | skip << 16}
+  __shared__ uint32_t wsum[kPBlock / kWave];
+  const uint32_t me = threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  // partition starts (scan of the sizes k_rp_hist left in cur), published by workgroup 0
+  for (uint32_t p = me; p < P; p += kPBlock) loc[p] = cur[p];
+  __syncthreads();
+  const uint32_t total = lds_excl_scan<kPBlock>(loc, P, wsum);
+  if (blockIdx.x == 0) {
+    for (uint32_t p = me; p < P; p += kPBlock) ps[p] = loc[p];
+    if (me == 0) ps[P] = total;
+    for (uint32_t p = me; p <= kMaxParts; p += kPBlock) cur_next[p] = 0;
+  }
+  // per owned partition: output cursor (segment-aligned after the first segment), carried pairs
+  // (the first `skip` of them phantoms standing for the run's unaligned start)
+  uint32_t my_cur[PPT], my_kc[PPT], my_skip[PPT];
+  uint2 creg[PPT][SEG - 1];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const uint32_t p = me + k * kPBlock;
+    const uint32_t st = p < P ? loc[p] + offs[uint64_t(blockIdx.x) * P + p] : 0u;
+    my_skip[k] = st % SEG;
+    my_cur[k] = st - my_skip[k];
+    my_kc[k] = my_skip[k];
+#pragma unroll
+    for (int j = 0; j < int(SEG) - 1; ++j) creg[k][j] = make_uint2(0, 0);
+  }
+  __syncthreads();
+  for (uint32_t p = me; p < kPBlock * PPT; p += kPBlock) loc[p] = 0;
+  __syncthreads();  // (the first half tile's rank atomics)
+  uint32_t h[kWsRounds], rw[EXPL ? kWsRounds : 1];
+  auto load = [&](uint64_t base) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < kWsRounds; ++j) {
+      const uint64_t i = base + uint64_t(j) * kPBlock + me;
+      h[j] = i < r.n ? key_ld(r, i) : 0u;
+      if constexpr (EXPL) rw[j] = i < r.n ? r.row(i) : 0u;
+    }
+  };
+  auto flush_carry = [&]() __attribute__((always_inline)) {  // the partial segments at the cursors
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+#pragma unroll
+      for (int j = 0; j < int(SEG) - 1; ++j)
+        if (uint32_t(j) < my_kc[k] && uint32_t(j) >= my_skip[k]) out[my_cur[k] + j] = creg[k][j];
+      my_cur[k] += my_kc[k];
+      my_kc[k] = 0;
+      my_skip[k] = 0;
+    }
+  };
+  auto scan = [&](uint32_t v, uint32_t* tot) __attribute__((always_inline)) {
+    uint32_t wt;
+    const uint32_t pre = wave_excl_scan(v, &wt);
+    if (lane == 0) wsum[wid] = wt;
+    __syncthreads();
+    uint32_t base = 0, all = 0;
+#pragma unroll
+    for (int w = 0; w < kPBlock / kWave; ++w) {
+      const uint32_t t = wsum[w];
+      base += w < wid ? t : 0u;
+      all += t;
+    }
+    __syncthreads();
+    *tot = all;
+    return base + pre;
+  };
+  // one half tile; `next`: the next half tile's first tuple (its keys are loaded once this one is
+  // staged, so the loads overlap the write-out); ~0: none
+  auto process = [&](uint64_t base, uint64_t next) __attribute__((always_inline)) {
+    uint32_t rk[kWsRounds];  // partition << 13 | rank in the half tile
+#pragma unroll
+    for (int j = 0; j < kWsRounds; ++j) {
+      const uint64_t i = base + uint64_t(j) * kPBlock + me;
+      h[j] = murmur32(h[j]);
+      const uint32_t bl = fm.mod(h[j]) - lo;
+      rk[j] = kInvalid;
+      if (i < r.n && bl < nbl) {
+        const uint32_t p = fw.div(bl);
+        rk[j] = (p << 13) | atomicAdd(&loc[p], 1u);
+      }
+    }
+    __syncthreads();
+    uint32_t c[PPT], L[PPT], pack = 0;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const uint32_t p = me + k * kPBlock;
+      c[k] = p < P ? loc[p] : 0u;
+      loc[p] = 0;  // read once per half tile; the next writes come after the next ranking barrier
+      L[k] = my_kc[k] + c[k];
+      pack += (L[k] << 16) | (L[k] / SEG);
+    }
+    uint32_t tot;
+    uint32_t pre = scan(pack, &tot);
+    if ((tot >> 16) > STAGE) {  // the carries and the half tile exceed the stage: carries out first (rare)
+      flush_carry();
+      pack = 0;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        L[k] = c[k];
+        pack += (L[k] << 16) | (L[k] / SEG);
+      }
+      pre = scan(pack, &tot);
+    }
+    const uint32_t nfull = tot & 0xFFFFu;
+    uint32_t at = pre >> 16, fseg = pre & 0xFFFFu;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const uint32_t p = me + k * kPBlock;
+      if (p < P) {
+        sbase[p] = at + my_kc[k];
+#pragma unroll
+        for (int j = 0; j < int(SEG) - 1; ++j)
+          if (uint32_t(j) < my_kc[k]) stage[at + j] = creg[k][j];
+        for (uint32_t sg = 0; sg < L[k] / SEG; ++sg)
+          seginfo[fseg + sg] = make_uint2(my_cur[k] + sg * SEG, (at + sg * SEG) | ((sg == 0 ? my_skip[k] : 0u) << 16));
+      }
+      at += L[k];
+      fseg += L[k] / SEG;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kWsRounds; ++j) {
+      if (rk[j] == kInvalid) continue;
+      const uint64_t i = base + uint64_t(j) * kPBlock + me;
+      uint32_t row;
+      if constexpr (EXPL) row = rw[j];
+      else row = uint32_t(r.row_base + i);
+      stage[sbase[rk[j] >> 13] + (rk[j] & (kWsSub - 1))] = make_uint2(h[j], row);
+    }
+    if (next != ~0ull) load(next);
+    __syncthreads();
+    for (uint32_t kk = me; kk < nfull * SEG; kk += kPBlock) {
+      const uint2 si = seginfo[kk / SEG];
+      const uint32_t j = kk % SEG;
+      const uint2 e = stage[(si.y & 0xFFFFu) + j];
+      if (j >= (si.y >> 16)) nt_st(out + si.x + j, e);
+    }
+    // each run's tail (< one segment) becomes the partition's carry. (The next half tile's first
+    // stage / seginfo writes follow its ranking barrier, which every thread reaches only after
+    // these reads: no barrier here.)
+    at = pre >> 16;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const uint32_t F = L[k] - L[k] % SEG;
+#pragma unroll
+      for (int j = 0; j < int(SEG) - 1; ++j)
+        if (uint32_t(j) < L[k] - F) creg[k][j] = stage[at + F + j];
+      if (F) my_skip[k] = 0;
+      my_cur[k] += F;
+      my_kc[k] = L[k] - F;
+      at += L[k];
+    }
+  };
+  if (blockIdx.x < ntiles) load(uint64_t(blockIdx.x) * kPTile);
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint64_t base = uint64_t(tile) * kPTile;
+    process(base, base + kWsSub);
+    process(base + kWsSub, tile + gridDim.x < ntiles ? uint64_t(tile + gridDim.x) * kPTile : ~0ull);
+  }
+  flush_carry();
+}
+
 // Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. BLOCK threads.
 template <int BLOCK>
 __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
@@ -273,7 +468,8 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
 
 // Staged build partitions: kBuildSlice2 buckets, at most kBuildStage pairs through LDS.
 constexpr uint32_t kBuildSlice2 = 8192;
-constexpr uint32_t kBuildStage = 15000;
+constexpr uint32_t kBuildSlice2Max = 10240;  // wider slices keep the partition count <= 1024 (k_rp_wscatter<1>)
+constexpr uint32_t kBuildStage = 14400;
 
 // The staged build as a persistent kernel (one 1024-thread workgroup per CU takes partitions
 // blockIdx.x, blockIdx.x + gridDim.x, ...): the next partition's pairs are loaded into registers
@@ -288,7 +484,7 @@ constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up
 __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                        FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
                                                        uint32_t* __restrict__ off, uint2* __restrict__ ent) {
-  __shared__ uint32_t cnt[kBuildSlice2 + 1];
+  __shared__ uint32_t cnt[kBuildSlice2Max + 1];
   __shared__ uint2 stage[kBuildStage];
   __shared__ uint32_t wsum[kJBlock / kWave];
   constexpr uint32_t kCap = kB3Per * kJBlock;
@@ -1063,8 +1259,24 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   }
   {
     PhaseTimer tm(ctx, t_scatter);
-    hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
-                       pl.ntiles, hist, cur, cur_next, ps, out);
+    const bool ex = r.row_off != HJ3D_ROW_IMPLICIT;
+#define HJ3D_WS_LAUNCH(PPT, EX)                                                                                  \
+  hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P, \
+                     pl.ntiles, hist, cur, cur_next, ps, out)
+    // whole segments pay once a workgroup takes two or more tiles (its carries ride into a later
+    // tile); with one tile each (config E's 4.2 M tuples) every run is flushed partial anyway and
+    // the plain write-out is faster (0.303 vs 0.317 ms build, same box)
+    const bool ws = HJ3D_RP_WS && pl.ntiles >= 2 * g;
+    if (ws && pl.P <= kPBlock) {
+      if (ex) HJ3D_WS_LAUNCH(1, true);
+      else HJ3D_WS_LAUNCH(1, false);
+    } else if (ws) {
+      if (ex) HJ3D_WS_LAUNCH(2, true);
+      else HJ3D_WS_LAUNCH(2, false);
+    } else
+#undef HJ3D_WS_LAUNCH
+      hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
+                         pl.ntiles, hist, cur, cur_next, ps, out);
   }
   return hipGetLastError();
 }
@@ -1120,8 +1332,14 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   // staged build (8192-bucket slices, small buckets sorted in LDS) while the fill leaves room in
   // the stage; else the 16384-bucket counting build; beyond 2048 slices the direct build
   const double fill = nbl ? double(r.n) / nbl : 0.0;
-  const bool staged = fill * kBuildSlice2 * 1.25 <= kBuildStage && (uint64_t(nbl) + kBuildSlice2 - 1) / kBuildSlice2 <= kMaxParts;
-  const Plan pl = plan_for(nbl, staged ? kBuildSlice2 : kBuildSlice, r.n);
+  // staged slices: 8192 buckets, or up to kBuildSlice2Max where that brings the partition count to
+  // 1024 (one partition per partitioner thread: 128-B segments in k_rp_wscatter, and whole waves
+  // of k_rp_build3's persistent workgroups; config B: 1221 -> 1024 partitions of 9766 buckets)
+  uint32_t W2 = kBuildSlice2;
+  const uint32_t Wk = uint32_t((uint64_t(nbl) + kPBlock - 1) / kPBlock);
+  if (HJ3D_RP_WS && Wk > W2 && Wk <= kBuildSlice2Max && fill * Wk * 1.25 <= kBuildStage) W2 = Wk;
+  const bool staged = fill * W2 * 1.25 <= kBuildStage && (uint64_t(nbl) + W2 - 1) / W2 <= kMaxParts;
+  const Plan pl = plan_for(nbl, staged ? W2 : kBuildSlice, r.n);
   if (pl.P > kMaxParts) return hipErrorNotSupported;  // > 2048 x 16384 buckets: the direct build
   if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(pl.P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;

@@ -255,7 +255,8 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
                               uint64_t* n_payload, uint64_t* n_sub);
 /* Which build made the table's current content (diagnostic, static string): chaining "radix",
  * "slices" (pk_slices, tables beyond the radix build's range) or "direct"; nested "nested_agg",
- * "nested_agg_slices" (more than 2048 partitions), "nested_sort" or "nested_radix"; "none" before a
+ * "nested_agg_slices" (more than 2048 partitions; "nested_agg_slices_reg" when the slices took the
+ * register form), "nested_sort" or "nested_radix"; "none" before a
  * build. A nested table whose build has not been resolved yet (no use since hj3d_build) reports the
  * path that was started, with "?" appended ("nested_agg?"): the getter never waits or builds. Replaces
  * nothing of the reference (which has one insert path). */
