@@ -1530,7 +1530,8 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
 }
 
 
-hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s) {
+hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s,
+                     bool sums) {
   hipError_t e;
   const uint32_t nbl = t->nb_local, nb = uint32_t(t->desc.num_buckets);
   if (nbl < 64 || r.n == 0 || r.n >= (1ull << 31) || W < 2) return hipErrorNotSupported;
@@ -1564,7 +1565,7 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPk2].ensure(nreg2 * cap2 * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrPk2Cnt].ensure(nreg2 * sizeof(uint32_t))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
+  if (sums && (e = ctx->scratch[kScrPStart].ensure((uint64_t(P) + 1) * sizeof(uint32_t))) != hipSuccess) return e;
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   auto geom = [&](uint32_t w, uint32_t p) {
     PkGeom g;
@@ -1585,7 +1586,7 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   uint2* ovf = ctx->scratch[kScrSortV].as<uint2>();
   uint2* fine = ctx->scratch[kScrPk2].as<uint2>();
   uint32_t* fcnt = ctx->scratch[kScrPk2Cnt].as<uint32_t>();
-  uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
+  uint32_t* ps = sums ? ctx->scratch[kScrPStart].as<uint32_t>() : nullptr;
   uint64_t* ctl = ctx->ctl.as<uint64_t>();
   const RelView v = view_of(r);
   SelRange sr{};
@@ -1599,9 +1600,11 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kSpBlock), 0, s, static_cast<const uint2*>(region),
                      static_cast<const uint32_t*>(counts), G, P1, uint32_t(cap), S2, pk, C, bits(C - 1), uint32_t(cap2),
                      fine, fcnt, ovf, ctl);
-  hipLaunchKernelGGL(k_pk_slice_sums, dim3((P + 255) / 256), dim3(256), 0, s, static_cast<const uint32_t*>(fcnt), S2, P, ps);
-  if ((e = hipGetLastError()) != hipSuccess) return e;
-  if ((e = exclusive_scan_u32(ctx, ps, ps, P, s)) != hipSuccess) return e;
+  if (sums) {
+    hipLaunchKernelGGL(k_pk_slice_sums, dim3((P + 255) / 256), dim3(256), 0, s, static_cast<const uint32_t*>(fcnt), S2, P, ps);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = exclusive_scan_u32(ctx, ps, ps, P, s)) != hipSuccess) return e;
+  }
   o->pk = pk;
   o->P = P;
   o->S2 = S2;
@@ -1609,7 +1612,13 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   o->fine = fine;
   o->fcnt = fcnt;
   o->ps = ps;
-  return hipSuccess;
+  o->ovf = ovf;
+  o->novf = reinterpret_cast<const unsigned long long*>(ctl + kCtlNovf);
+  return hipGetLastError();
+}
+
+hipError_t pk_ctl_reset(hj3d_ctx* ctx, hipStream_t s) {
+  return hipMemsetAsync(ctx->ctl.p, 0, kCtlWords * sizeof(uint64_t), s);
 }
 
 hipError_t pk_overflow_check(hj3d_ctx* ctx, hipStream_t s, uint64_t* novf) {

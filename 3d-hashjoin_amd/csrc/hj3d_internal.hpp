@@ -251,6 +251,13 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
 // Uses scratch kScrPHist. hipErrorNotSupported beyond 2048 partitions.
 hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
                                  uint32_t* ps, uint32_t* nparts, hipStream_t s);
+// The same into narrow partitions (Wf buckets, up to 8192 of them), exact under any skew: a fine
+// histogram, the whole-segment scatter into coarse partitions of C fine ones, then the split of
+// every coarse partition (k_rp_hist2, k_rp_wscatter, k_rp_split2). Partition p is out[fps[p] ..
+// fps[p+1]). Uses kScrPHist, kScrSortV, kScrPStart. hipErrorNotSupported beyond 8192 partitions
+// or where one level suffices.
+hipError_t radix_partition_pairs_2l(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t Wf, uint2* out,
+                                    uint32_t* fps, uint32_t* nparts, hipStream_t s);
 // after every chaining build: buckets of <= 32 entries sorted by row (single-pass probe order)
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
 // sel (nullable, <= 2 predicates): the selection fused into the probe-side partitioner; tuples
@@ -310,9 +317,20 @@ struct PkSlices {
   uint32_t P = 0, S2 = 0, cap2 = 0;
   const uint2* fine = nullptr;
   const uint32_t* fcnt = nullptr;
-  const uint32_t* ps = nullptr;
+  const uint32_t* ps = nullptr;             // (sums = false: not computed)
+  const uint2* ovf = nullptr;               // region-overflow pairs {h, row}
+  const unsigned long long* novf = nullptr;  // their count: control word kCtlNovf (reset by the caller)
 };
-hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s);
+hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, PkSlices* o, hipStream_t s,
+                     bool sums = true);
+// The probe side of a nested table wider than the one-level partitioner's 2048 LDS slices: pk_slices
+// (two levels, packed pairs) into slices of W buckets, plus the dense output slots of its fine
+// regions (seg, partition-major); pp's region layout is radix_seg.hpp's with G = S2 regions per
+// slice. Overflow pairs: pp->ovf / pp->novf (the packed probe's control word: the caller resets the
+// control words after the probe, pk_ctl_reset).
+hipError_t pk_probe_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
+                           PkGeom* pk, hipStream_t s);
+hipError_t pk_ctl_reset(hj3d_ctx* ctx, hipStream_t s);
 hipError_t pk_overflow_check(hj3d_ctx* ctx, hipStream_t s, uint64_t* novf);
 // The chaining build of tables beyond the radix build's range (> 2048 x 16384 buckets): R
 // partitioned by the packed partitioner's two levels into 8192-bucket slices, each built in LDS

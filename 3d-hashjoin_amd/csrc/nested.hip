@@ -263,6 +263,9 @@ constexpr int kExpU = HJ3D_EXP_U;
 #define HJ3D_RN_SPLITS 16  // workgroups per wide slice (16: one region stream per wave at G = 256)
 #endif
 constexpr uint32_t kHbmSplits = HJ3D_RN_SPLITS;
+#ifndef HJ3D_RN_PK
+#define HJ3D_RN_PK 1  // nested probe of more than 2048 LDS slices on the packed two-level partition (0: A/B, wide slices)
+#endif
 #ifndef HJ3D_RN_STATIC
 #define HJ3D_RN_STATIC 1  // k_rn_probe_seg, materialised unnest: fixed store count per chunk (0: A/B)
 #endif
@@ -542,7 +545,9 @@ __device__ __forceinline__ void nested_bucket(uint32_t h, uint32_t pr, const MT*
   }
 }
 
-template <int MODE, bool FITS>
+// PKD: the regions hold packed pairs {v, row} of pk_probe_slices (bucket in the slice v >> qbits, hash
+// pk.hash_of(v, p): no modulo per pair), else {hash, row}.
+template <int MODE, bool FITS, bool PKD>
 __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restrict__ region,
                                                           const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap,
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
                                                           uint64_t* __restrict__ cnt, uint32_t* __restrict__ zo,
                                                           uint32_t* __restrict__ po, Heavy* __restrict__ heavy,
                                                           uint64_t* __restrict__ nheavy, uint64_t* __restrict__ partials,
-                                                          uint64_t* __restrict__ sink, bool xcd) {
+                                                          uint64_t* __restrict__ sink, bool xcd, PkGeom pk) {
   __shared__ uint32_t lds[kProbeLdsWords];
   // xcd: workgroup b runs on XCD b % 8; XCD x takes the x-th eighth of the (slice, share) pairs
   uint32_t bid = blockIdx.x;
@@ -586,8 +591,9 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
 #pragma unroll
                      for (int j = 0; j < kSegItems; ++j) {
                        const bool valid = (vm >> j) & 1u;
-                       const uint32_t hv = uint32_t(v[j]), row = uint32_t(v[j] >> 32);
-                       const uint32_t bl = fm.mod(hv) - lo - b0;
+                       const uint32_t w0 = uint32_t(v[j]), row = uint32_t(v[j] >> 32);
+                       const uint32_t hv = PKD ? pk.hash_of(w0, p) : w0;
+                       const uint32_t bl = PKD ? w0 >> pk.qbits : fm.mod(hv) - lo - b0;
                        const uint32_t d = valid ? ldir[bl] : 0u;
                        const uint32_t s0 = d >> 16, n = d & 0xFFFFu;
                        uint32_t found = kInvalid;
@@ -623,8 +629,9 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
   }
   seg_walk(region, counts, seg, G, cap, P, p, splits, sp, flat,
            [&] { if (FITS) stage_nested(off, mains, b0, nbs, m0, nm, ldir, lmain); },
-           [&](uint32_t hv, uint32_t row, uint64_t i) {
-             const uint32_t bl = fm.mod(hv) - lo - b0;
+           [&](uint32_t w0, uint32_t row, uint64_t i) {
+             const uint32_t hv = PKD ? pk.hash_of(w0, p) : w0;
+             const uint32_t bl = PKD ? w0 >> pk.qbits : fm.mod(hv) - lo - b0;
              if (FITS) {
                const uint32_t d = ldir[bl];
                nested_bucket<MODE>(hv, row, lmain, d >> 16, d & 0xFFFFu, m0, acc, i, out, out_cap, cnt, zo, po, sub,
@@ -823,14 +830,31 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   const double fill = double(t->n_mains) / double(nbl);
   ProbeParts pp;
   unsigned long long* npass = nullptr;  // fused selection: tuples passing it (n_probe)
-  const uint32_t w_fit = uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill));
-  if ((e = radix_partition_probe(ctx, t, r, w_fit, &pp, s, sel, sel ? &npass : nullptr)) != hipSuccess) return e;
+  uint32_t w_fit = uint32_t(0.8 * kProbeLdsWords / (1.0 + 4.0 * fill));
+  if (ctx->pk_slice_max && w_fit > ctx->pk_slice_max) w_fit = ctx->pk_slice_max;  // HJ3D_OPT_PK_SLICE (tests)
+  // more LDS slices than the one-level partitioner's 2048 (config D's 1e8-bucket table on one GPU,
+  // 2.5e7 / 5e7 buckets per rank at 4 / 2 owners): the packed partitioner's two levels give every
+  // slice its LDS width (pk_probe_slices); before, such tables were probed in ~1 MB slices through L2
+  PkGeom pk{};
+  bool pkd = false;
+  {
+    const uint64_t P0 = (uint64_t(nbl) + w_fit - 1) / w_fit;
+    if (HJ3D_RN_PK && !sel && w_fit >= 64 && P0 > 2048 && P0 <= 65536) {
+      const uint64_t G = uint64_t(ctx->num_cus);
+      const uint64_t P1 = (P0 + G - 1) / G * G;  // whole waves of probe workgroups
+      const uint32_t W1 = uint32_t((uint64_t(nbl) + P1 - 1) / P1);
+      e = pk_probe_slices(ctx, t, r, W1 >= 64 ? W1 : w_fit, &pp, &pk, s);
+      if (e == hipSuccess) pkd = true;
+      else if (e != hipErrorNotSupported) return e;
+    }
+  }
+  if (!pkd && (e = radix_partition_probe(ctx, t, r, w_fit, &pp, s, sel, sel ? &npass : nullptr)) != hipSuccess) return e;
   // slices wider than LDS (more than the partitioner's 2048 slices at the fitting width: config D's
   // 1e8-bucket table) are probed through the cache. Then kHbmSplits workgroups share each slice and
   // the blocks are ordered so that an XCD's workgroups take consecutive (slice, share) pairs: the
   // ~32 workgroups of an XCD work on two slices at a time, whose directory and main records
   // (~1 MB each) stay in its 4 MB L2 instead of 32 different slices thrashing it.
-  const bool wide = HJ3D_RN_XCD && pp.W > w_fit && pp.splits < kHbmSplits && pp.G >= kHbmSplits;
+  const bool wide = !pkd && HJ3D_RN_XCD && pp.W > w_fit && pp.splits < kHbmSplits && pp.G >= kHbmSplits;
   if (wide) pp.splits = kHbmSplits;
   const uint32_t nblocks = pp.P * pp.splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
@@ -873,12 +897,17 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
     auto launch = [&](auto mode_c) {
       constexpr int M = decltype(mode_c)::value;
-      hipLaunchKernelGGL((k_rn_probe_seg<M, true>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
-                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials, sink, wide);
-      hipLaunchKernelGGL((k_rn_probe_seg<M, false>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg,
-                         pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o, out_cap, cnt,
-                         zo, po, hq, nhq, partials, sink, wide);
+      auto seg_kernels = [&](auto pkd_c) {
+        constexpr bool PKD = decltype(pkd_c)::value;
+        hipLaunchKernelGGL((k_rn_probe_seg<M, true, PKD>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts,
+                           pp.seg, pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o,
+                           out_cap, cnt, zo, po, hq, nhq, partials, sink, wide, pk);
+        hipLaunchKernelGGL((k_rn_probe_seg<M, false, PKD>), dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts,
+                           pp.seg, pp.G, pp.cap, off, mains, sub, t->fm, lo, nbl, pp.W, pp.P, pp.splits, pp.flat, o,
+                           out_cap, cnt, zo, po, hq, nhq, partials, sink, wide, pk);
+      };
+      if (pkd) seg_kernels(std::true_type{});
+      else seg_kernels(std::false_type{});
       hipLaunchKernelGGL((k_rn_probe_ovf<M>), dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf,
                          pp.seg + uint64_t(pp.G) * pp.P, off, mains, sub, t->fm, lo, o, out_cap, cnt, zo, po, hq, nhq,
                          res);
@@ -893,6 +922,9 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
       hipLaunchKernelGGL(k_expand_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, hq, nhq, mains, sub, res);
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  // the packed partitioner's control words (overflow count, n_probe) back to zero, the invariant of
+  // the probes that share them
+  if (pkd && (e = pk_ctl_reset(ctx, s)) != hipSuccess) return e;
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
   if ((e = reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, sel ? 0ull : r.n, base0)) != hipSuccess)
     return e;

@@ -72,7 +72,10 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_DIAG 0  // diagnostic variants (tables wrong): 1 pass B without its sub-row stores, 2 without pass B
 #endif
 #ifndef HJ3D_NAGG_REG
-#define HJ3D_NAGG_REG 1  // slices of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
+#define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
+#endif
+#ifndef HJ3D_NAGG_2L
+#define HJ3D_NAGG_2L 1  // one-level partitions too large for k_nagg_reg: the exact two-level partition (0: A/B)
 #endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
@@ -469,43 +472,34 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
 }
 
-// One workgroup per partition (gp = blockIdx.x, or order[blockIdx.x]), or, with `list` ({count,
-// partition ids...}: the partitions k_nagg_reg deferred), a grid looping over the listed ones.
+// One workgroup per partition: gp = blockIdx.x, or order[blockIdx.x] (heavy first).
 template <int BLOCK, int SLOTS, bool PK>
 __global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                 FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                                 uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
                                                 const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
-                                                NaggTabs tabs, const uint32_t* __restrict__ list) {
+                                                NaggTabs tabs) {
   extern __shared__ uint32_t agg_lds[];
-  if (!list) {
-    nagg_one<BLOCK, SLOTS, PK>(PK || !order ? blockIdx.x : order[blockIdx.x], pairs, ps, fm, lo, nbl, nb_global, W,
-                               mtmp, dcount, cap, src, tabs, agg_lds);
-    return;
-  }
-  const uint32_t nwork = list[0];
-  for (uint32_t w = blockIdx.x; w < nwork; w += gridDim.x) {
-    nagg_one<BLOCK, SLOTS, PK>(list[1 + w], pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs, agg_lds);
-    __syncthreads();
-  }
+  nagg_one<BLOCK, SLOTS, PK>(PK || !order ? blockIdx.x : order[blockIdx.x], pairs, ps, fm, lo, nbl, nb_global, W, mtmp,
+                             dcount, cap, src, tabs, agg_lds);
 }
 
 // ---- k_nagg_reg: the partition held in registers, its sub rows assembled in LDS ----
 // k_nagg streams every partition twice from HBM (pass A, pass B) and scatters each sub row with a
 // 4-B store into the partition's sub window, whose lines the L2 evicts before they are complete
 // (3.8x write amplification at config C). Here one persistent 1024-thread workgroup per CU takes
-// partitions (slices) q = blockIdx.x, + gridDim.x, ...: a partition of <= kRegCap pairs is loaded
-// into registers ONCE (the next partition's loads are issued as soon as pass B has read them, and
-// overlap the image write-out and the next table's initialisation), pass A and pass B run on the
-// registers, pass B places every row into an LDS image of the partition's sub range, and the image
-// goes out as whole lines. Per pair: 8 B
-// read + 4 B written. A partition with more pairs than kRegCap, or more distinct keys than the
-// table holds, is appended to `defer` ({count, ids...}) and left to k_nagg (list form) afterwards.
+// partitions idx = blockIdx.x, + gridDim.x, ... (partition order[idx], heavy first, or idx itself):
+// a partition of <= kRegCap pairs is loaded into registers ONCE (the next partition's loads are
+// issued as soon as pass B has read them, and overlap the image write-out and the next table's
+// initialisation), pass A and pass B run on the registers, pass B places every row into an LDS image
+// of the partition's sub range, and the image goes out as whole lines. Per pair: 8 B read + 4 B
+// written. A partition with more pairs than kRegCap (a Zipf hot key's) or more distinct keys than
+// the table holds takes k_nagg's streaming form (nagg_one) in place, in the same workgroup.
 #ifndef HJ3D_NAGG_REGK
 #define HJ3D_NAGG_REGK 16
 #endif
 constexpr int kRegBlock = 1024;
-constexpr int kRegK = HJ3D_NAGG_REGK;                          // pairs per lane and buffer
+constexpr int kRegK = HJ3D_NAGG_REGK;                          // pairs per lane
 constexpr uint32_t kRegCap = uint32_t(kRegK) * kRegBlock;      // pairs per partition (16384)
 __host__ __device__ constexpr uint32_t reg_lds_words(uint32_t cap, uint32_t W) {
   return 3 * cap + W + kRegCap + kRegBlock / 64 + 2 + 2 * (kAggMaxS2 + 2);
@@ -513,9 +507,9 @@ __host__ __device__ constexpr uint32_t reg_lds_words(uint32_t cap, uint32_t W) {
 template <bool PK, int SLOTS>
 __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                         FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global,
-                                                        uint32_t W, uint32_t P, uint4* __restrict__ mtmp,
+                                                        uint32_t W, uint32_t PT, uint4* __restrict__ mtmp,
                                                         uint32_t* __restrict__ dcount, uint32_t cap, NaggSrc src,
-                                                        NaggTabs tabs, uint32_t* __restrict__ defer) {
+                                                        NaggTabs tabs, const uint32_t* __restrict__ order) {
   extern __shared__ uint32_t agg_lds[];
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;
@@ -525,19 +519,18 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
   uint32_t* wsum = img + kRegCap;
   uint32_t& nkeys = wsum[kRegBlock / kWave];
   uint32_t& ovf = wsum[kRegBlock / kWave + 1];
-  uint32_t* rst = wsum + kRegBlock / kWave + 2;  // [2][kAggMaxS2 + 2]: region starts of the two buffers' slices
+  uint32_t* rst = wsum + kRegBlock / kWave + 2;  // [2][kAggMaxS2 + 2]: region starts of the two slices in turn
   const uint32_t limit = cap - kRegBlock - 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  uint32_t* __restrict__ off = tabs.off[0];
-  uint32_t* __restrict__ sub = tabs.sub[0];
-  auto* maxlen = reinterpret_cast<unsigned long long*>(tabs.counts[0] + 2);
   uint32_t mxlen = 0;
-  // region starts of slice q into rst[b] (PK; wave 0)
-  const auto starts = [&](uint32_t q, uint32_t b) __attribute__((always_inline)) {
+  const auto part_of = [&](uint32_t idx) __attribute__((always_inline)) { return order ? order[idx] : idx; };
+  // region starts of slice gp into rst[b] (PK: one table; wave 0)
+  const auto starts = [&](uint32_t idx, uint32_t b) __attribute__((always_inline)) {
     if constexpr (PK) {
-      if (wid == 0 && q < P) {
-        const uint32_t len = uint32_t(lane) < src.S2 ? src.fcnt[uint64_t(lane) * src.pk.P + q] : 0u;
+      if (wid == 0 && idx < PT) {
+        const uint32_t gp = part_of(idx);
+        const uint32_t len = uint32_t(lane) < src.S2 ? src.fcnt[uint64_t(lane) * src.pk.P + gp] : 0u;
         uint32_t tot;
         const uint32_t pre = wave_excl_scan(len, &tot);
         uint32_t* r = rst + b * (kAggMaxS2 + 2);
@@ -549,15 +542,17 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
       }
     }
   };
-  const auto count_of = [&](uint32_t q, uint32_t b) __attribute__((always_inline)) {
+  const auto count_of = [&](uint32_t gp, uint32_t b) __attribute__((always_inline)) {
     if constexpr (PK) return rst[b * (kAggMaxS2 + 2) + src.S2];
-    else return ps[q + 1] - ps[q];
+    else return ps[gp + 1] - ps[gp];
   };
-  // kRegK loads per lane, always (indices clamped to the slice's last pair; a slice of more than
-  // kRegCap pairs is deferred, so its registers are never used)
-  const auto load = [&](uint32_t q, uint32_t b, uint2 (&v)[kRegK]) __attribute__((always_inline)) {
-    if (q >= P) return;  // (past the last slice: rst[b] was not written)
-    const uint32_t m = count_of(q, b);
+  // kRegK loads per lane, always (indices clamped to the partition's last pair); a partition of more
+  // than kRegCap pairs takes the streaming form, so its registers are never used
+  uint2 v[kRegK];
+  const auto load = [&](uint32_t idx, uint32_t b) __attribute__((always_inline)) {
+    if (idx >= PT) return;  // (past the last partition: rst[b] was not written)
+    const uint32_t gp = part_of(idx);
+    const uint32_t m = count_of(gp, b);
     const uint32_t last = m ? m - 1 : 0u;
     if constexpr (PK) {
       const uint32_t* r = rst + b * (kAggMaxS2 + 2);
@@ -566,36 +561,42 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
       for (int u = 0; u < kRegK; ++u) {
         const uint32_t f = min(uint32_t(u) * kRegBlock + threadIdx.x, last);
         while (cr + 1 < src.S2 && f >= r[cr + 1]) ++cr;
-        v[u] = src.fine[(uint64_t(cr) * src.pk.P + q) * src.cap2 + (f - r[cr])];
+        v[u] = src.fine[(uint64_t(cr) * src.pk.P + gp) * src.cap2 + (f - r[cr])];
       }
     } else {
-      const uint32_t e0 = ps[q];
+      const uint32_t e0 = ps[gp];
 #pragma unroll
       for (int u = 0; u < kRegK; ++u) v[u] = pairs[e0 + min(uint32_t(u) * kRegBlock + threadIdx.x, last)];
     }
   };
-  uint2 v[kRegK];
-  const auto process = [&](uint32_t q, uint32_t b, uint32_t qn) __attribute__((always_inline)) {
-    const uint32_t b0 = q * W, nbs = min(W, nbl - b0);
-    const uint32_t e0 = ps[q], m = count_of(q, b);
+  const auto process = [&](uint32_t idx, uint32_t b) __attribute__((always_inline)) {
+    const uint32_t gp = part_of(idx);
+    const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
+    const uint32_t p = gp - ti * tabs.P;  // partition inside table ti
+    uint32_t* __restrict__ off = tabs.off[ti];
+    uint32_t* __restrict__ sub = tabs.sub[ti];
+    const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
+    const uint32_t e0 = ps[gp], m = count_of(gp, b);
     const uint32_t empty = PK ? (nbs << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + nbs) % nb_global);
     const auto lbk = [&](uint32_t x) __attribute__((always_inline)) {
       if constexpr (PK) return x >> src.pk.qbits;
       else return fm.mod(x) - lo - b0;
     };
-    for (uint32_t s = threadIdx.x; s < cap; s += kRegBlock) {
-      tkey[s] = empty;
-      tcnt[s] = 0;
-      tmin[s] = kInvalid;
-    }
-    for (uint32_t k = threadIdx.x; k < nbs; k += kRegBlock) bcnt[k] = 0;
-    if (threadIdx.x == 0) {
-      nkeys = 0;
-      ovf = m > kRegCap;
-    }
-    starts(qn, b ^ 1u);  // the next slice's region starts (PK)
-    __syncthreads();
     const bool big = m > kRegCap;
+    if (!big) {
+      for (uint32_t s = threadIdx.x; s < cap; s += kRegBlock) {
+        tkey[s] = empty;
+        tcnt[s] = 0;
+        tmin[s] = kInvalid;
+      }
+      for (uint32_t k = threadIdx.x; k < nbs; k += kRegBlock) bcnt[k] = 0;
+      if (threadIdx.x == 0) {
+        nkeys = 0;
+        ovf = 0;
+      }
+    }
+    starts(idx + gridDim.x, b ^ 1u);  // the next partition's region starts (PK)
+    __syncthreads();
     // ---- pass A: count and min row per key (registers) ----
     if (!big) {
 #pragma unroll
@@ -642,11 +643,14 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
           }
         }
       }
+      __syncthreads();
     }
-    __syncthreads();
-    if (ovf) {  // too many pairs or keys for this form: k_nagg takes the slice afterwards
-      if (threadIdx.x == 0) defer[1 + atomicAdd(defer, 1u)] = q;
-      load(qn, b ^ 1u, v);
+    if (big || ovf) {
+      // more pairs than the registers hold, or more keys than one table round: k_nagg's streaming
+      // form (rounds over halves of the bucket range) on this partition, here
+      nagg_one<kRegBlock, SLOTS, PK>(gp, pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs, agg_lds);
+      __syncthreads();
+      load(idx + gridDim.x, b ^ 1u);
       return;
     }
     // ---- main slots: rank of every key inside its bucket, bucket offsets, sub ranges ----
@@ -665,14 +669,14 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
     }
     __syncthreads();
     block_scan_lds<kRegBlock>(tcnt, cap, wsum);  // tcnt: the key's first slot in the image
-    const uint32_t sb = e0 - tabs.pbase[0];       // the slice's sub range starts at its first pair
+    const uint32_t sb = e0 - tabs.pbase[ti];      // the partition's sub range starts at its first pair
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
       const uint32_t s = j * kRegBlock + threadIdx.x;
       if (cnt[j]) {
         const uint32_t h = tkey[s];
         uint32_t hash;
-        if constexpr (PK) hash = src.pk.hash_of(h, q);
+        if constexpr (PK) hash = src.pk.hash_of(h, p);
         else hash = h;
         mtmp[e0 + bcnt[lbk(h)] + rank[j]] = make_uint4(hash, tmin[s], sb + tcnt[s], cnt[j]);
         mxlen = max(mxlen, cnt[j]);
@@ -702,45 +706,52 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
       if (a) img[atomicAdd(&tcnt[tab_find(tkey, e.x, cap)], 1u)] = e.y;
     }
     __syncthreads();
-    // the registers are free: the next slice's loads go out now and overlap the image write-out and
-    // the next table's initialisation
-    load(qn, b ^ 1u, v);
-    // ---- the image out: the slice's sub range as whole lines ----
+    // the registers are free: the next partition's loads go out now and overlap the image
+    // write-out and the next table's initialisation
+    load(idx + gridDim.x, b ^ 1u);
+    // ---- the image out: the partition's sub range as whole lines ----
     for (uint32_t k = threadIdx.x; k < m; k += kRegBlock) sub[sb + k] = img[k];
-    if (threadIdx.x == 0) dcount[q] = nk;
+    if (threadIdx.x == 0) dcount[gp] = nk;
   };
-  uint32_t q = blockIdx.x;
-  starts(q, 0);
+  uint32_t idx = blockIdx.x;
+  starts(idx, 0);
   __syncthreads();
-  load(q, 0, v);
-  for (uint32_t it = 0; q < P; ++it, q += gridDim.x) {
-    process(q, it & 1u, q + gridDim.x);
+  load(idx, 0);
+  for (uint32_t it = 0; idx < PT; ++it, idx += gridDim.x) {
+    process(idx, it & 1u);
     __syncthreads();
   }
   const uint64_t wm = wave_max(uint64_t(mxlen));
-  if (lane == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+  for (uint32_t ti = 0; ti < tabs.nt; ++ti) {
+    // (the longest key over both tables is an upper bound for each; the probe only sizes by it)
+    auto* maxlen = reinterpret_cast<unsigned long long*>(tabs.counts[ti] + 2);
+    if (lane == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+  }
 }
 
 // order = the partitions by size class, heavy first (> 8x the mean pairs, then > 2x, then the
-// rest), each class in index order: k_nagg takes its partitions in this order, so a Zipf hot
+// rest), each class in index order: the aggregation takes its partitions in this order, so a Zipf hot
 // key's partition starts in the first wave of workgroups instead of extending the tail. One
-// workgroup, P <= 2048 (a stable three-way split by block scans; a full sort by size cost 27 us).
+// workgroup, P <= 8192 (a stable three-way split by block scans; a full sort by size cost 27 us).
+constexpr int kOrdPer = 8;  // partitions per thread
 __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict__ ps, uint32_t P,
                                                      uint32_t* __restrict__ order) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t base;
   const uint32_t mean = P ? (ps[P] - ps[0]) / P : 0u;
-  uint32_t cls[2];
+  uint32_t cls[kOrdPer];
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {  // thread t holds partitions 2t, 2t + 1
-    const uint32_t p = 2 * threadIdx.x + k;
+  for (int k = 0; k < kOrdPer; ++k) {  // thread t holds partitions kOrdPer t + k
+    const uint32_t p = kOrdPer * threadIdx.x + k;
     const uint32_t sz = p < P ? ps[p + 1] - ps[p] : 0u;
     cls[k] = p >= P ? 3u : sz > 8u * mean ? 0u : sz > 2u * mean ? 1u : 2u;
   }
   if (threadIdx.x == 0) base = 0;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t c = 0; c < 3; ++c) {
-    const uint32_t a0 = cls[0] == c, a1 = cls[1] == c, t = a0 + a1;
+    uint32_t t = 0;
+#pragma unroll
+    for (int k = 0; k < kOrdPer; ++k) t += cls[k] == c;
     uint32_t wt;
     const uint32_t wpre = wave_excl_scan(t, &wt);
     if (lane == 0) wsum[wid] = wt;
@@ -751,9 +762,10 @@ __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict_
       pre += w < wid ? wsum[w] : 0u;
       tot += wsum[w];
     }
-    const uint32_t at = base + pre + wpre;
-    if (a0) order[at] = 2 * threadIdx.x;
-    if (a1) order[at + a0] = 2 * threadIdx.x + 1;
+    uint32_t at = base + pre + wpre;
+#pragma unroll
+    for (int k = 0; k < kOrdPer; ++k)
+      if (cls[k] == c) order[at++] = kOrdPer * threadIdx.x + k;
     __syncthreads();
     if (threadIdx.x == 0) base += tot;
     __syncthreads();
@@ -782,9 +794,8 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
-__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail, uint32_t* __restrict__ defer) {
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail) {
   if (threadIdx.x == 0 && ctl[0] != 0) *fail = 1u;  // ctl[0]: chain_pk.hip's overflow count
-  if (threadIdx.x == 0) defer[0] = 0;                // k_nagg_reg's deferred-slice list: empty
   __syncthreads();
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
@@ -855,20 +866,34 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
       if (HJ3D_NAGG_PKW) W = std::min<uint32_t>(W, std::max<uint32_t>(HJ3D_NAGG_PKW, (nbl + 65535) / 65536));
     }
   }
+  // one level too coarse for the register form (config C: 1792 partitions of ~56 K pairs): the exact
+  // two-level partition into up to 8192 narrow ones (radix_partition_pairs_2l; skew-safe, unlike the
+  // slices' fixed regions), rounded to whole waves of the aggregation's workgroups
+  bool two = false;
+  if (!pk && nt == 1 && HJ3D_NAGG_2L && double(n) * W / nbl > 0.85 * kRegCap) {
+    uint64_t Pf = std::max<uint64_t>((uint64_t(nbl) + 8191) / 8192, uint64_t(double(n) / (0.6 * kRegCap)));
+    Pf = std::min<uint64_t>((Pf + G - 1) / G * G, 8192);
+    const uint32_t Wf = uint32_t((uint64_t(nbl) + Pf - 1) / Pf);
+    const uint32_t Pf2 = (nbl + Wf - 1) / Wf, C = (Pf2 + 1023) / 1024;
+    if (Wf >= 256 && C >= 2 && C <= 16) {
+      two = true;
+      W = Wf;
+    }
+  }
   const uint32_t P = (nbl + W - 1) / W;
   if (pk && nt > 1) return hipErrorNotSupported;  // one table at a time on the slices
-  if (!pk && uint64_t(P) * nt > 2048) return hipErrorNotSupported;  // k_nagg_order's limit
+  if (!pk && uint64_t(P) * nt > (two ? 8192u : 2048u)) return hipErrorNotSupported;  // k_nagg_order's limit
   const uint32_t PT = P * nt;  // partitions over every table
-  if (path) *path = pk ? "nested_agg_slices" : "nested_agg";
+  if (path) *path = pk ? "nested_agg_slices" : two ? "nested_agg_2l" : "nested_agg";
   // scratch: pairs (n uint2; PK: the fine regions of pk_slices) | main records before compaction
   // (n uint4) | starts | key counts, order
   if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSlot].ensure((4 * uint64_t(PT) + 6) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(PT) + 6) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + PT + 1;
-  uint32_t* defer = order + PT + 1;  // k_nagg_reg: {count, deferred slices}
+  uint32_t* fps = order + PT + 1;  // two levels: the fine partitions' starts (PT + 1)
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   NaggTabs tabs;
   tabs.P = P;
@@ -897,7 +922,15 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
     hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(),
-                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3), defer);
+                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3));
+  } else if (two) {
+    uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
+    uint32_t np = 0;
+    if ((e = radix_partition_pairs_2l(ctx, t, rr[0], W, pw, fps, &np, s)) != hipSuccess) return e;
+    if (np != P) return hipErrorNotSupported;
+    pairs = pw;
+    ps = fps;
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
@@ -927,6 +960,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
     for (const void* k : {reinterpret_cast<const void*>(&k_nagg_reg<true, 4>),
+                          reinterpret_cast<const void*>(&k_nagg_reg<false, 4>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, true>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
@@ -937,38 +971,37 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
   const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
-  // the register form (k_nagg_reg) on the slices, where their expected pairs fit its registers with
-  // room (deferred slices then go through k_nagg's list form below)
+  // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
+  // (a larger partition takes k_nagg's streaming form inside it)
   const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
-  const bool reg = HJ3D_NAGG_REG && pk && double(n) / P <= 0.85 * kRegCap && capr <= 4 * kRegBlock &&
+  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= 0.85 * kRegCap && capr <= 4 * kRegBlock &&
                    reg_lds_words(capr, W) * 4 <= 160 * 1024;
-  const uint32_t* list = nullptr;
   if (reg) {
     const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);
-    hipLaunchKernelGGL((k_nagg_reg<true, 4>), dim3(std::min<uint32_t>(P, G)), dim3(kRegBlock), lds, s, pairs, ps, t->fm,
-                       lo, nbl, nbg, W, P, mtmp, dcount, capr, src, tabs, defer);
-    list = defer;
-    if (path) *path = "nested_agg_slices_reg";
-  }
-  // k_nagg: one workgroup per partition, or (list) a grid over the deferred slices
-  auto grid = [&](uint32_t per_cu) { return list ? std::min<uint32_t>(PT, G * per_cu) : PT; };
-  if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
+    if (pk)
+      hipLaunchKernelGGL((k_nagg_reg<true, 4>), dim3(std::min<uint32_t>(PT, G)), dim3(kRegBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, PT, mtmp, dcount, capr, src, tabs, nullptr);
+    else
+      hipLaunchKernelGGL((k_nagg_reg<false, 4>), dim3(std::min<uint32_t>(PT, G)), dim3(kRegBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, PT, mtmp, dcount, capr, src, tabs, order);
+    if (path) *path = pk ? "nested_agg_slices_reg" : two ? "nested_agg_2l_reg" : "nested_agg_reg";
+  } else if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
     if (pk)
-      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(grid(2)), dim3(kSmallBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs, list);
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
     else
       hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs, list);
+                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
   } else {
     const uint32_t cap = kAggCapMax;
     const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
     if (pk)
-      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(grid(1)), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs, list);
+      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap, src, tabs);
     else
       hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs, list);
+                         mtmp, dcount, order, cap, src, tabs);
   }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // for its table and the caller, which reads the counts at the table's next use, runs the sort

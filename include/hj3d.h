@@ -167,7 +167,8 @@ enum {
   /* HJ3D_OPT_PK_SLICE (buckets, 0 or >= 2; default 0): upper bound on the packed probe's slice
    * width (normally the largest that fits one workgroup's LDS). Tables of more than 1024 slices
    * take the two-level partition (k_pk_part into coarse ranges, k_pk_split by slice), so a small
-   * bound puts small tables on that path (tests). */
+   * bound puts small tables on that path (tests). It bounds the partitioned nested probe's slice
+   * width too: beyond 2048 slices that probe takes the same two-level partition. */
   HJ3D_OPT_PK_SLICE = 8,
   /* HJ3D_OPT_PK_STAGE (pairs, default 0 = the whole LDS stage): the packed partitioner writes its
    * carried partial segments out early once the carries plus a tile exceed this many pairs
@@ -255,8 +256,9 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
                               uint64_t* n_payload, uint64_t* n_sub);
 /* Which build made the table's current content (diagnostic, static string): chaining "radix",
  * "slices" (pk_slices, tables beyond the radix build's range) or "direct"; nested "nested_agg",
- * "nested_agg_slices" (more than 2048 partitions; "nested_agg_slices_reg" when the slices took the
- * register form), "nested_sort" or "nested_radix"; "none" before a
+ * "nested_agg_slices" (more than 2048 partitions), "nested_agg_2l" (the exact two-level partition
+ * into narrow partitions), each with "_reg" appended when the register form aggregated them,
+ * "nested_sort" or "nested_radix"; "none" before a
  * build. A nested table whose build has not been resolved yet (no use since hj3d_build) reports the
  * path that was started, with "?" appended ("nested_agg?"): the getter never waits or builds. Replaces
  * nothing of the reference (which has one insert path). */

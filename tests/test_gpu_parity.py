@@ -580,3 +580,69 @@ def test_nested_slices_register_form(ctx, keys_per_bucket):
     finally:
         ctx.radix_min(1 << 20)
         ctx.nested_pk(False)
+
+
+@pytest.mark.parametrize("plan", ["Nrs", "NrsNU", "Nsr"])
+def test_nested_probe_two_level_slices(ctx, plan):
+    """The partitioned nested probe beyond the one-level partitioner's 2048 LDS slices (config D's
+    1e8-bucket table on one GPU) runs on the packed partitioner's two levels (pk_probe_slices:
+    k_pk_part + k_pk_split, packed pairs, every slice in LDS). A slice bound of 64 buckets
+    (HJ3D_OPT_PK_SLICE) puts a 200K-bucket table there (3125 slices); Zipf duplicates overflow some
+    regions, whose pairs the overflow kernel probes. Counters, checksums and the materialised pairs
+    equal the oracle's."""
+    import torch
+    import hj3d
+    rng = np.random.default_rng(41)
+    nb, nR, nS = 200_000, 300_000, 800_000
+    Rk = rng.permutation(nR).astype(np.uint32)
+    Sa = np.minimum(rng.zipf(1.5, nS) - 1, nR - 1).astype(np.uint32)
+    Sa[: nS // 2] = rng.integers(0, nR, nS // 2, dtype=np.uint32)
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    e = _oracle_plans(R, S, nb, nb)[plan]
+    ctx.radix_min(0)
+    ctx.pk_slice_max(64)
+    try:
+        got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb)
+        assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
+            (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), plan
+        assert got["out"] == e.out, plan
+        cap = max(e.out["n"], nS, nR, 1)
+        out = torch.zeros((cap, 2), dtype=torch.int32, device="cuda")
+        got = hj3d.exp1_plan(ctx, plan, dev(R), dev(S), nb, out=out, stats=False)
+        host = out.cpu().numpy().view(np.uint32)
+        if plan == "NrsNU":  # one slot per probe tuple (R), unmatched slots carry 0xFFFFFFFF
+            host = host[:nR]
+            host = host[host[:, 1] != 0xFFFFFFFF]
+        else:
+            host = host[: e.out["n"]]
+        assert host_checksums(host) == e.out, plan
+    finally:
+        ctx.radix_min(1 << 20)
+        ctx.pk_slice_max(0)
+
+
+@pytest.mark.parametrize("zipf", [False, True], ids=["uniform", "zipf"])
+def test_nested_build_two_level_partition(ctx, zipf):
+    """Nested builds whose one-level partitions are too large for the register form take the exact
+    two-level partition (radix_partition_pairs_2l: fine histogram, whole-segment scatter into coarse
+    partitions, split into up to 8192 narrow ones) and the register aggregation, with Zipf hot keys'
+    partitions streamed inside it. 12M build tuples over 300K buckets: 1024 narrow partitions of
+    ~12K pairs. Counters, output checksums and statistics equal the oracle's."""
+    import hj3d
+    rng = np.random.default_rng(53 + zipf)
+    nb, nS, dom = 300_000, 12_000_000, 600_000
+    Sa = (np.minimum(rng.zipf(1.4, nS) - 1, dom - 1) if zipf else rng.integers(0, dom, nS)).astype(np.uint32)
+    Rk = rng.permutation(dom).astype(np.uint32)[:400_000]
+    R = O.tuples3(Rk, np.zeros_like(Rk))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
+    e = O.nested_plan(S, 1, R, 0, nb, True)
+    t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+    got = hj3d.exp1_plan(ctx, "Nrs", dev(R), dev(S), nb, table=t)
+    path = t.build_path()
+    st = t.stats()
+    t.close()
+    assert path == "nested_agg_2l_reg" or path == "nested_sort", path
+    assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_unnest, e.c_top)
+    assert got["out"] == e.out
+    assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
