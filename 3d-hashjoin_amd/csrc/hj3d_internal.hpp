@@ -249,8 +249,10 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
 // Partition r into (hash, row) pairs by ranges of W local buckets (LDS-histogram pass, scan,
 // LDS-staged scatter): partition p is out[ps[p] .. ps[p+1]), *nparts = ceil(nb_local / W).
 // Uses scratch kScrPHist. hipErrorNotSupported beyond 2048 partitions.
+// r1 (optional): a second relation of the same geometry in the same two launches; its partitions are
+// P .. 2P - 1 (ps[P .. 2P]), its pairs follow r's.
 hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
-                                 uint32_t* ps, uint32_t* nparts, hipStream_t s);
+                                 uint32_t* ps, uint32_t* nparts, hipStream_t s, const hj3d_rel* r1 = nullptr);
 // The same into narrow partitions (Wf buckets, up to 8192 of them), exact under any skew: a fine
 // histogram, the whole-segment scatter into coarse partitions of C fine ones, then the split of
 // every coarse partition (k_rp_hist2, k_rp_wscatter, k_rp_split2). Partition p is out[fps[p] ..

@@ -217,7 +217,8 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   auto* maxlen = reinterpret_cast<unsigned long long*>(tabs.counts[ti] + 2);
   auto* fail = reinterpret_cast<uint32_t*>(tabs.counts[ti] + 3);
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
-  const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = tabs.pbase[ti];
+  // (table ti's sub rows are numbered from its first pair: ps[ti * P])
+  const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = ps[ti * tabs.P];
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   if constexpr (PK) {
@@ -669,7 +670,7 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
     }
     __syncthreads();
     block_scan_lds<kRegBlock>(tcnt, cap, wsum);  // tcnt: the key's first slot in the image
-    const uint32_t sb = e0 - tabs.pbase[ti];      // the partition's sub range starts at its first pair
+    const uint32_t sb = e0 - ps[ti * tabs.P];     // the partition's sub range starts at its first pair
 #pragma unroll
     for (int j = 0; j < SLOTS; ++j) {
       const uint32_t s = j * kRegBlock + threadIdx.x;
@@ -735,9 +736,10 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
 // workgroup, P <= 8192 (a stable three-way split by block scans; a full sort by size cost 27 us).
 constexpr int kOrdPer = 8;  // partitions per thread
 __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict__ ps, uint32_t P,
-                                                     uint32_t* __restrict__ order) {
+                                                     uint32_t* __restrict__ order, NaggTabs tabs) {
   __shared__ uint32_t wsum[16];
   __shared__ uint32_t base;
+  if (threadIdx.x < 4 * tabs.nt) tabs.counts[threadIdx.x / 4][threadIdx.x % 4] = 0;  // (the build's counts words)
   const uint32_t mean = P ? (ps[P] - ps[0]) / P : 0u;
   uint32_t cls[kOrdPer];
 #pragma unroll
@@ -775,17 +777,29 @@ __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict_
 // off[b] += first main of b's partition; main records moved to their final slots.
 // k_nagg_rebase / k_nagg_mains / k_nagg_counts run only when no partition gave up (`fail`: the
 // sort build replaces the table then; the host checks the flag once, after the whole build).
-__global__ __launch_bounds__(kBlock) void k_nagg_rebase(uint32_t* __restrict__ off, uint32_t nbl, FastDiv32 dw,
-                                                        const uint32_t* __restrict__ mbase,
-                                                        const uint32_t* __restrict__ fail) {
-  if (*fail) return;
-  const uint32_t m0 = mbase[0];  // the table's first main record in the scan over every table
-  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mbase[dw.div(b)] - m0;
+__global__ __launch_bounds__(kBlock) void k_nagg_rebase(NaggTabs tabs, uint32_t nbl, FastDiv32 dw,
+                                                        const uint32_t* __restrict__ mbase) {
+  const uint32_t ti = blockIdx.y;  // one grid row per table
+  if (reinterpret_cast<const uint32_t*>(tabs.counts[ti] + 3)[0]) return;  // fail flag
+  uint32_t* __restrict__ off = tabs.off[ti];
+  const uint32_t* mb = mbase + ti * tabs.P;
+  const uint32_t m0 = mb[0];  // the table's first main record in the scan over every table
+  for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b < nbl; b += gridDim.x * kBlock) off[b] += mb[dw.div(b)] - m0;
 }
 
 __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
-                                                       const uint32_t* __restrict__ mbase, NaggTabs tabs) {
+                                                       const uint32_t* __restrict__ mbase, NaggTabs tabs, uint32_t nbl) {
   const uint32_t gp = blockIdx.x, ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
+  if (gp == 0 && threadIdx.x < tabs.nt) {  // every table's counts (entries, main records, off[nbl])
+    const uint32_t tj = threadIdx.x;
+    uint64_t* counts = tabs.counts[tj];
+    if (!reinterpret_cast<const uint32_t*>(counts + 3)[0]) {
+      const uint32_t a = tj * tabs.P, b = (tj + 1) * tabs.P;
+      counts[0] = ps[b] - ps[a];
+      counts[1] = mbase[b] - mbase[a];
+      tabs.off[tj][nbl] = mbase[b] - mbase[a];
+    }
+  }
   if (reinterpret_cast<const uint32_t*>(tabs.counts[ti] + 3)[0]) return;  // fail flag
   uint4* __restrict__ mains = tabs.main[ti];
   const uint32_t n = mbase[gp + 1] - mbase[gp], m0 = mbase[gp] - mbase[ti * tabs.P];
@@ -794,28 +808,12 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
-__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint32_t* __restrict__ fail) {
-  if (threadIdx.x == 0 && ctl[0] != 0) *fail = 1u;  // ctl[0]: chain_pk.hip's overflow count
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts) {
+  if (threadIdx.x < 4) counts[threadIdx.x] = threadIdx.x == 3 && ctl[0] != 0 ? 1u : 0u;  // ctl[0]: the overflow count
   __syncthreads();
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
 
-__global__ void k_nagg_counts(const uint32_t* __restrict__ ps, const uint32_t* __restrict__ mbase, uint32_t nbl,
-                              NaggTabs tabs) {
-  const uint32_t ti = threadIdx.x;
-  if (ti >= tabs.nt) return;
-  uint64_t* counts = tabs.counts[ti];
-  if (reinterpret_cast<const uint32_t*>(counts + 3)[0]) return;  // fail flag
-  const uint32_t a = ti * tabs.P, b = (ti + 1) * tabs.P;
-  counts[0] = ps[b] - ps[a];
-  counts[1] = mbase[b] - mbase[a];
-  tabs.off[ti][nbl] = mbase[b] - mbase[a];
-}
-
-// table 1's partition starts (written 0-based by its partition pass) moved behind table 0's pairs
-__global__ void k_nagg_ps_shift(uint32_t* __restrict__ ps, uint32_t n, uint32_t by) {
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) ps[i] += by;
-}
 
 }  // namespace
 
@@ -844,6 +842,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if ((e = tt[k]->sub.ensure(rr[k].n * sizeof(uint32_t))) != hipSuccess) return e;
     if ((e = tt[k]->counts.ensure(4 * sizeof(uint64_t))) != hipSuccess) return e;
   }
+  // (the counts words are zeroed by the first kernel after the partition: k_nagg_order / k_nagg_pk_ovf)
   // partition width: kAggW buckets, narrower when that would leave the chip with fewer than two
   // partitions per CU (config E: 2M buckets -> 512 partitions of 4K instead of 342 of 6K)
   // Then the count is rounded up to whole waves of workgroups (one k_nagg workgroup per CU at a
@@ -905,7 +904,6 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     tabs.sub[k] = tt[k]->sub.as<uint32_t>();
     tabs.main[k] = tt[k]->main.as<uint4>();
     tabs.counts[k] = tt[k]->counts.as<uint64_t>();
-    if ((e = hipMemsetAsync(tabs.counts[k], 0, 4 * sizeof(uint64_t), s)) != hipSuccess) return e;
   }
   const uint2* pairs = nullptr;
   const uint32_t* ps = nullptr;
@@ -921,8 +919,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     src.pk = sl.pk;
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
-    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(),
-                       reinterpret_cast<uint32_t*>(tabs.counts[0] + 3));
+    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0]);
   } else if (two) {
     uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
     uint32_t np = 0;
@@ -930,22 +927,19 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = fps;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
     uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
-    for (uint32_t k = 0; k < nt; ++k) {
-      uint32_t np = 0;
-      if ((e = radix_partition_pairs(ctx, tt[k], rr[k], W, pw + tabs.pbase[k], pst + k * P, &np, s)) != hipSuccess)
-        return e;
-      if (np != P) return hipErrorNotSupported;
-    }
-    if (nt > 1)  // table 1's starts were written 0-based into pst[P .. 2P]
-      hipLaunchKernelGGL(k_nagg_ps_shift, dim3((P + 256) / 256), dim3(256), 0, s, pst + P, P + 1, tabs.pbase[1]);
+    // both tables' relations in one partition pass (two launches): table 1's partitions are P .. 2P-1
+    uint32_t np = 0;
+    if ((e = radix_partition_pairs(ctx, t, rr[0], W, pw, pst, &np, s, nt > 1 ? &rr[1] : nullptr)) != hipSuccess)
+      return e;
+    if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = pst;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs);
   }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
@@ -1007,11 +1001,9 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // for its table and the caller, which reads the counts at the table's next use, runs the sort
   // build instead
   if ((e = exclusive_scan_u32(ctx, dcount, dcount, PT, s)) != hipSuccess) return e;
-  for (uint32_t k = 0; k < nt; ++k)
-    hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock)), dim3(kBlock), 0, s, tabs.off[k], nbl,
-                       FastDiv32::make(W), dcount + k * P, reinterpret_cast<const uint32_t*>(tabs.counts[k] + 3));
-  hipLaunchKernelGGL(k_nagg_mains, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs);
-  hipLaunchKernelGGL(k_nagg_counts, dim3(1), dim3(64), 0, s, ps, dcount, nbl, tabs);
+  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock), nt), dim3(kBlock), 0, s, tabs, nbl,
+                     FastDiv32::make(W), dcount);
+  hipLaunchKernelGGL(k_nagg_mains, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs, nbl);
   for (uint32_t k = 0; k < nt; ++k) tt[k]->n_build = rr[k].n;
   return hipGetLastError();
 }

@@ -84,40 +84,58 @@ inline FastDiv make_div(uint32_t d) {
   return f;
 }
 
+// The tuples of one relation, or of two back to back (hj3d_build_many's two tables of one geometry,
+// experiment 4's S and T: one partition pass for both): relation 1's tiles follow relation 0's
+// (nt0 of them), its partitions follow at P + p and its pairs after relation 0's.
+struct RelTiles {
+  RelView r0, r1;
+  uint32_t nt0;  // kPTile-tiles of r0
+  uint32_t P;    // partitions per relation
+  __device__ __forceinline__ bool second(uint32_t tile) const { return tile >= nt0; }
+  __device__ __forceinline__ const RelView& rel(uint32_t tile) const { return tile >= nt0 ? r1 : r0; }
+  __device__ __forceinline__ uint64_t base(uint32_t tile) const {
+    return uint64_t(tile >= nt0 ? tile - nt0 : tile) * kPTile;
+  }
+  __device__ __forceinline__ uint32_t pofs(uint32_t tile) const { return tile >= nt0 ? P : 0u; }
+};
+
 // Partition sizes per scatter workgroup: workgroup g of the G = gridDim.x persistent workgroups
 // counts the tiles g, g + G, ... that k_rp_scatter's workgroup g will write, then claims its run
 // inside every partition with one atomic on the partition's cursor (cur[p] ends as the partition's
 // size) and keeps the run's offset in its row hist[g * P + p]. The order of the workgroups' runs
 // inside a partition is the atomics' order: no counter depends on it (build3 places rows by rank,
 // the nested builds aggregate), and no scan over the P x G counts is needed.
-__global__ __launch_bounds__(kPBlock) void k_rp_hist(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+__global__ __launch_bounds__(kPBlock) void k_rp_hist(RelTiles rt, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                      uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist,
                                                      uint32_t* __restrict__ cur) {
   __shared__ uint32_t cnt[kMaxParts];
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
   __syncthreads();
   uint32_t key[kPRounds];
+  auto load = [&](uint32_t tile) __attribute__((always_inline)) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t b = rt.base(tile);
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
-    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    key[j] = i < r.n ? key_ld(r, i) : 0u;
-  }
+    for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
+      const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
+      key[j] = tile < ntiles && i < r.n ? key_ld(r, i) : 0u;
+    }
+  };
+  load(blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t b = rt.base(tile);
+    const uint32_t pofs = rt.pofs(tile);
     uint32_t bl[kPRounds];
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = uint64_t(tile) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
+      const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
       bl[j] = i < r.n ? fm.mod(murmur32(key[j])) - lo : nbl;
     }
-    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
-#pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      key[j] = i < r.n ? key_ld(r, i) : 0u;
-    }
+    load(tile + gridDim.x);  // next tile: loads in flight
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j)
-      if (bl[j] < nbl) atomicAdd(&cnt[fw.div(bl[j])], 1u);
+      if (bl[j] < nbl) atomicAdd(&cnt[pofs + fw.div(bl[j])], 1u);
   }
   __syncthreads();
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) {
@@ -138,7 +156,7 @@ __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
 // before the current tile's write-out, so the CU's reads and writes overlap.
 // Partition starts: an LDS scan of the P partition sizes (k_rp_hist's cursors) in every workgroup;
 // workgroup 0 writes them to ps[0..P] and clears the other cursor set for the next call.
-__global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+__global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
                                                         const uint32_t* __restrict__ cur, uint32_t* __restrict__ cur_next,
                                                         uint32_t* __restrict__ ps, uint2* __restrict__ out) {
@@ -148,14 +166,20 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
   __shared__ uint32_t wsum[kPBlock / kWave];
   // explicit row ids are loaded with the keys, a tile ahead (loading them at the stage write after
   // the ranking phase waited for every load separately: one round trip per tuple and round)
-  const bool explicit_rows = r.row_off != 0xFFFFFFFFu;
+  const bool explicit_rows = rt.r0.row_off != 0xFFFFFFFFu;  // (both relations alike)
   uint32_t h[kPRounds], rw[kPRounds];
+  auto load = [&](uint32_t tile) __attribute__((always_inline)) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t b = rt.base(tile);
 #pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    h[j] = i < r.n ? key_ld(r, i) : 0u;
-    rw[j] = explicit_rows && i < r.n ? r.row(i) : 0u;
-  }
+    for (int j = 0; j < kPRounds; ++j) {
+      const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
+      const bool ok = tile < ntiles && i < r.n;
+      h[j] = ok ? key_ld(r, i) : 0u;
+      rw[j] = explicit_rows && ok ? r.row(i) : 0u;
+    }
+  };
+  load(blockIdx.x);
   // this workgroup's write cursor per partition: partition start + its run's offset (k_rp_hist)
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) gb[p] = cur[p];
   __syncthreads();
@@ -170,7 +194,9 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
   }
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     for (uint32_t p = threadIdx.x; p < P; p += kPBlock) loc[p] = 0;
-    const uint64_t base = uint64_t(tile) * kPTile;
+    const RelView& r = rt.rel(tile);
+    const uint64_t base = rt.base(tile);
+    const uint32_t pofs = rt.pofs(tile);
     uint32_t rk[kPRounds];
     __syncthreads();
 #pragma unroll
@@ -179,7 +205,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
       h[j] = murmur32(h[j]);
       const uint32_t bl = fm.mod(h[j]) - lo;
       if (i < r.n && bl < nbl) {  // rk = partition << 14 | rank in the tile's run (kPTile = 2^14)
-        const uint32_t part = fw.div(bl);
+        const uint32_t part = pofs + fw.div(bl);
         rk[j] = (part << 14) | atomicAdd(&loc[part], 1u);
       } else {
         rk[j] = kInvalid;
@@ -194,16 +220,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelView r, FastMod fm, u
       stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], explicit_rows ? rw[j] : r.row(i));
     }
     __syncthreads();
-    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;  // next tile: loads in flight
-#pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      h[j] = i < r.n ? key_ld(r, i) : 0u;
-      rw[j] = explicit_rows && i < r.n ? r.row(i) : 0u;
-    }
+    load(tile + gridDim.x);  // next tile: loads in flight
     for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
       const uint2 e = stage[k];
-      const uint32_t p = fw.div(fm.mod(e.x) - lo);
+      const uint32_t p = pofs + fw.div(fm.mod(e.x) - lo);
       nt_st(out + gb[p] + (k - loc[p]), e);
     }
     __syncthreads();
@@ -238,7 +258,7 @@ struct WsGeom {
   static constexpr uint32_t kStage = PPT == 1 ? 17408u : 15360u;  // the half tile + carries (pairs)
 };
 template <int PPT, bool EXPL>
-__global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
+__global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelTiles rt, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                          uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
                                                          const uint32_t* __restrict__ cur, uint32_t* __restrict__ cur_next,
                                                          uint32_t* __restrict__ ps, uint2* __restrict__ out) {
@@ -277,7 +297,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, 
   for (uint32_t p = me; p < kPBlock * PPT; p += kPBlock) loc[p] = 0;
   __syncthreads();  // (the first half tile's rank atomics)
   uint32_t h[kWsRounds], rw[EXPL ? kWsRounds : 1];
-  auto load = [&](uint64_t base) __attribute__((always_inline)) {
+  // half `hf` of tile `tile`
+  auto load = [&](uint32_t tile, uint32_t hf) __attribute__((always_inline)) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t base = rt.base(tile) + uint64_t(hf) * kWsSub;
 #pragma unroll
     for (int j = 0; j < kWsRounds; ++j) {
       const uint64_t i = base + uint64_t(j) * kPBlock + me;
@@ -312,9 +335,12 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, 
     *tot = all;
     return base + pre;
   };
-  // one half tile; `next`: the next half tile's first tuple (its keys are loaded once this one is
-  // staged, so the loads overlap the write-out); ~0: none
-  auto process = [&](uint64_t base, uint64_t next) __attribute__((always_inline)) {
+  // half `hf` of tile `tile`; the next half tile's keys (ntile, nhf; ntile >= ntiles: none) are
+  // loaded once this one is staged, so the loads overlap the write-out
+  auto process = [&](uint32_t tile, uint32_t hf, uint32_t ntile, uint32_t nhf) __attribute__((always_inline)) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t base = rt.base(tile) + uint64_t(hf) * kWsSub;
+    const uint32_t pofs = rt.pofs(tile);
     uint32_t rk[kWsRounds];  // partition << 13 | rank in the half tile
 #pragma unroll
     for (int j = 0; j < kWsRounds; ++j) {
@@ -323,7 +349,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, 
       const uint32_t bl = fm.mod(h[j]) - lo;
       rk[j] = kInvalid;
       if (i < r.n && bl < nbl) {
-        const uint32_t p = fw.div(bl);
+        const uint32_t p = pofs + fw.div(bl);
         rk[j] = (p << 13) | atomicAdd(&loc[p], 1u);
       }
     }
@@ -375,7 +401,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, 
       else row = uint32_t(r.row_base + i);
       stage[sbase[rk[j] >> 13] + (rk[j] & (kWsSub - 1))] = make_uint2(h[j], row);
     }
-    if (next != ~0ull) load(next);
+    if (ntile < ntiles) load(ntile, nhf);
     __syncthreads();
     for (uint32_t kk = me; kk < nfull * SEG; kk += kPBlock) {
       const uint2 si = seginfo[kk / SEG];
@@ -399,11 +425,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelView r, FastMod fm, 
       at += L[k];
     }
   };
-  if (blockIdx.x < ntiles) load(uint64_t(blockIdx.x) * kPTile);
+  if (blockIdx.x < ntiles) load(blockIdx.x, 0);
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    const uint64_t base = uint64_t(tile) * kPTile;
-    process(base, base + kWsSub);
-    process(base + kWsSub, tile + gridDim.x < ntiles ? uint64_t(tile + gridDim.x) * kPTile : ~0ull);
+    process(tile, 0, tile, 1);
+    process(tile, 1, tile + gridDim.x, 0);
   }
   flush_carry();
 }
@@ -1395,12 +1420,19 @@ Plan plan_for(uint32_t nbl, uint32_t W, uint64_t n) {
 // k_rp_hist (sizes, runs claimed on the partition cursors) and k_rp_scatter (starts, pairs).
 // t_hist / t_scatter: timer phases of the two streaming kernels (-1: untimed).
 hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, const Plan& pl, uint2* out,
-                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1) {
+                           uint32_t* ps, hipStream_t s, int t_hist = -1, int t_scatter = -1,
+                           const hj3d_rel* r1 = nullptr) {
   hipError_t e;
-  if (r.n == 0) return hipMemsetAsync(ps, 0, (uint64_t(pl.P) + 1) * sizeof(uint32_t), s);
+  // r1: a second relation of the same table geometry, partitioned in the same two launches (its
+  // partitions follow at P .. 2P - 1, its pairs after r's)
+  const uint32_t PT = r1 ? 2 * pl.P : pl.P;
+  const uint32_t nt0 = pl.ntiles, nt1 = r1 ? uint32_t((r1->n + kPTile - 1) / kPTile) : 0u;
+  const uint32_t ntiles = nt0 + nt1;
+  if (ntiles == 0) return hipMemsetAsync(ps, 0, (uint64_t(PT) + 1) * sizeof(uint32_t), s);
+  if (PT > kMaxParts) return hipErrorNotSupported;
   // G persistent workgroups in both passes, one row of run offsets per workgroup
-  const uint32_t g = pl.ntiles < uint32_t(ctx->num_cus) ? pl.ntiles : uint32_t(ctx->num_cus);
-  if ((e = ctx->scratch[kScrPHist].ensure(uint64_t(pl.P) * g * sizeof(uint32_t))) != hipSuccess) return e;
+  const uint32_t g = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
+  if ((e = ctx->scratch[kScrPHist].ensure(uint64_t(PT) * g * sizeof(uint32_t))) != hipSuccess) return e;
   uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
   if (!ctx->part_cur.p) {
     if ((e = ctx->part_cur.ensure(2 * (kMaxParts + 1) * sizeof(uint32_t))) != hipSuccess) return e;
@@ -1409,24 +1441,28 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   uint32_t* cur = ctx->part_cur.as<uint32_t>() + (ctx->part_parity & 1u) * (kMaxParts + 1);
   uint32_t* cur_next = ctx->part_cur.as<uint32_t>() + ((ctx->part_parity + 1) & 1u) * (kMaxParts + 1);
   ctx->part_parity ^= 1u;
-  const RelView v = view_of(r);
+  RelTiles rt;
+  rt.r0 = view_of(r);
+  rt.r1 = r1 ? view_of(*r1) : rt.r0;
+  rt.nt0 = nt0;
+  rt.P = pl.P;
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
   {
     PhaseTimer tm(ctx, t_hist);
-    hipLaunchKernelGGL(k_rp_hist, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P, pl.ntiles,
-                       hist, cur);
+    hipLaunchKernelGGL(k_rp_hist, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles, hist,
+                       cur);
   }
   {
     PhaseTimer tm(ctx, t_scatter);
     const bool ex = r.row_off != HJ3D_ROW_IMPLICIT;
-#define HJ3D_WS_LAUNCH(PPT, EX)                                                                                  \
-  hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P, \
-                     pl.ntiles, hist, cur, cur_next, ps, out)
+#define HJ3D_WS_LAUNCH(PPT, EX)                                                                                   \
+  hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, \
+                     ntiles, hist, cur, cur_next, ps, out)
     // whole segments pay once a workgroup takes two or more tiles (its carries ride into a later
-    // tile); with one tile each (config E's 4.2 M tuples) every run is flushed partial anyway and
-    // the plain write-out is faster (0.303 vs 0.317 ms build, same box)
-    const bool ws = HJ3D_RP_WS && pl.ntiles >= 2 * g;
-    if (ws && pl.P <= kPBlock) {
+    // tile); with one tile each (config E's relations one at a time) every run is flushed partial
+    // anyway and the plain write-out is faster (0.303 vs 0.317 ms build, same box)
+    const bool ws = HJ3D_RP_WS && ntiles >= 2 * g;
+    if (ws && PT <= kPBlock) {
       if (ex) HJ3D_WS_LAUNCH(1, true);
       else HJ3D_WS_LAUNCH(1, false);
     } else if (ws) {
@@ -1434,8 +1470,8 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
       else HJ3D_WS_LAUNCH(2, false);
     } else
 #undef HJ3D_WS_LAUNCH
-      hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, t->nb_local, pl.fw, pl.P,
-                         pl.ntiles, hist, cur, cur_next, ps, out);
+      hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles,
+                         hist, cur, cur_next, ps, out);
   }
   return hipGetLastError();
 }
@@ -1475,11 +1511,11 @@ bool radix_probe_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n
 }
 
 hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
-                                 uint32_t* ps, uint32_t* nparts, hipStream_t s) {
+                                 uint32_t* ps, uint32_t* nparts, hipStream_t s, const hj3d_rel* r1) {
   const Plan pl = plan_for(t->nb_local, W, r.n);
-  if (pl.P > kMaxParts) return hipErrorNotSupported;
+  if (pl.P * (r1 ? 2u : 1u) > kMaxParts) return hipErrorNotSupported;
   *nparts = pl.P;
-  return partition_pairs(ctx, t, r, pl, out, ps, s);
+  return partition_pairs(ctx, t, r, pl, out, ps, s, -1, -1, r1);
 }
 
 hipError_t radix_partition_pairs_2l(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t Wf, uint2* out,
@@ -1517,11 +1553,15 @@ hipError_t radix_partition_pairs_2l(hj3d_ctx* ctx, const hj3d_table* t, const hj
   const FastDiv fwf = make_div(Wf), fw1 = make_div(W1);
   hipLaunchKernelGGL(k_rp_hist2, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, nbl, fwf, Pf, C, P1, ntiles, hist1, cur,
                      ftot);
+  RelTiles rt;
+  rt.r0 = rt.r1 = v;
+  rt.nt0 = ntiles;
+  rt.P = P1;
   if (r.row_off != HJ3D_ROW_IMPLICIT)
-    hipLaunchKernelGGL((k_rp_wscatter<1, true>), dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
+    hipLaunchKernelGGL((k_rp_wscatter<1, true>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
                        cur, cur_next, ps1, coarse);
   else
-    hipLaunchKernelGGL((k_rp_wscatter<1, false>), dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
+    hipLaunchKernelGGL((k_rp_wscatter<1, false>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
                        cur, cur_next, ps1, coarse);
   hipLaunchKernelGGL(k_rp_split2, dim3(ctx->num_cus * 4), dim3(kS2Block), 0, s, static_cast<const uint2*>(coarse),
                      static_cast<const uint32_t*>(ps1), P1, C, cbits, Pf, t->fm, lo, fwf,
