@@ -654,6 +654,10 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
 constexpr uint32_t kBuildSlice2 = 8192;
 constexpr uint32_t kBuildSlice2Max = 10240;  // wider slices keep the partition count <= 1024 (k_rp_wscatter<1>)
 constexpr uint32_t kBuildStage = 14400;
+#ifndef HJ3D_B3_HALF
+#define HJ3D_B3_HALF 0  // chaining build: half-width slices, two 512-thread k_rp_build3 workgroups per CU (A/B)
+#endif
+constexpr uint32_t kB3HalfW = 5120, kB3HalfStage = 6656;  // 72 KB of LDS: two workgroups per CU
 
 // The staged build as a persistent kernel (one 1024-thread workgroup per CU takes partitions
 // blockIdx.x, blockIdx.x + gridDim.x, ...): the next partition's pairs are loaded into registers
@@ -664,15 +668,18 @@ constexpr uint32_t kBuildStage = 14400;
 // rows (buckets of 2..kSortedMax entries come out sorted by row, with no sort pass; longer ones
 // stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) scatter
 // through HBM instead (sorting their small buckets there).
-constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12288 pairs
-__global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
-                                                       FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
-                                                       uint32_t* __restrict__ off, uint2* __restrict__ ent) {
-  __shared__ uint32_t cnt[kBuildSlice2Max + 1];
-  __shared__ uint2 stage[kBuildStage];
-  __shared__ uint32_t wsum[kJBlock / kWave];
-  constexpr uint32_t kCap = kB3Per * kJBlock;
-  static_assert(kCap <= kBuildStage, "a register-held partition must fit the stage");
+constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12 * BLOCK pairs
+// BLOCK = 1024: one workgroup per CU, slices up to kBuildSlice2Max buckets; BLOCK = 512
+// (HJ3D_B3_HALF): two per CU on half-width slices (WMAX, STAGE: its LDS share)
+template <int BLOCK, uint32_t WMAX, uint32_t STAGE>
+__global__ __launch_bounds__(BLOCK) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                     FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
+                                                     uint32_t* __restrict__ off, uint2* __restrict__ ent) {
+  __shared__ uint32_t cnt[WMAX + 1];
+  __shared__ uint2 stage[STAGE];
+  __shared__ uint32_t wsum[BLOCK / kWave];
+  constexpr uint32_t kCap = kB3Per * BLOCK;
+  static_assert(kCap <= STAGE, "a register-held partition must fit the stage");
   uint2 ea[kB3Per], eb[kB3Per];
   auto load = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
     if (p >= P) return;
@@ -680,7 +687,7 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
     if (s1 - s0 > kCap) return;
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
-      const uint32_t i = s0 + u * kJBlock + threadIdx.x;
+      const uint32_t i = s0 + u * BLOCK + threadIdx.x;
       e[u] = i < s1 ? nt_ld(pairs + i) : make_uint2(0, 0);
     }
   };
@@ -688,21 +695,21 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
     const uint32_t b0 = p * W;
     const uint32_t nbs = min(W, nbl - b0);
     const uint32_t s0 = ps[p], s1 = ps[p + 1], m = s1 - s0;
-    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) cnt[k] = 0;
+    for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) cnt[k] = 0;
     __syncthreads();
     if (m > kCap) {  // skewed partition: scatter through HBM, sort the small buckets there
-      for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) atomicAdd(&cnt[fm.mod(pairs[i].x) - lo - b0], 1u);
+      for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) atomicAdd(&cnt[fm.mod(pairs[i].x) - lo - b0], 1u);
       __syncthreads();
-      lds_excl_scan(cnt, nbs, wsum);
-      for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) off[b0 + k] = s0 + cnt[k];
+      lds_excl_scan<BLOCK>(cnt, nbs, wsum);
+      for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) off[b0 + k] = s0 + cnt[k];
       if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
       __syncthreads();
-      for (uint32_t i = s0 + threadIdx.x; i < s1; i += kJBlock) {
+      for (uint32_t i = s0 + threadIdx.x; i < s1; i += BLOCK) {
         const uint2 x = pairs[i];
         ent[s0 + atomicAdd(&cnt[fm.mod(x.x) - lo - b0], 1u)] = x;
       }
       __syncthreads();
-      for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) {
+      for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) {
         const uint32_t bs = k ? cnt[k - 1] : 0u, n = cnt[k] - bs;
         if (n < 2 || n > kSortedMax) continue;
         uint2* E = ent + s0 + bs;
@@ -722,21 +729,21 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build3(const uint2* __restrict__
     uint32_t rk[kB3Per];  // bucket << 16 | arrival rank (W <= 2^16, ranks < 2^16)
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
-      const bool v = u * kJBlock + threadIdx.x < m;
+      const bool v = u * BLOCK + threadIdx.x < m;
       const uint32_t b = v ? fm.mod(e[u].x) - lo - b0 : 0u;
       rk[u] = v ? (b << 16) | atomicAdd(&cnt[b], 1u) : kInvalid;
     }
     __syncthreads();
-    lds_excl_scan(cnt, nbs, wsum);
+    lds_excl_scan<BLOCK>(cnt, nbs, wsum);
     if (threadIdx.x == 0) cnt[nbs] = m;
-    for (uint32_t k = threadIdx.x; k < nbs; k += kJBlock) nt_st(off + b0 + k, s0 + cnt[k]);
+    for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) nt_st(off + b0 + k, s0 + cnt[k]);
     if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u)
       if (rk[u] != kInvalid) stage[cnt[rk[u] >> 16] + (rk[u] & 0xFFFFu)] = e[u];
     __syncthreads();
-    for (uint32_t q = threadIdx.x; q < m; q += kJBlock) {
+    for (uint32_t q = threadIdx.x; q < m; q += BLOCK) {
       const uint2 x = stage[q];
       const uint32_t b = fm.mod(x.x) - lo - b0;
       const uint32_t bs = cnt[b], n = cnt[b + 1] - bs;
@@ -1585,7 +1592,14 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   uint32_t W2 = kBuildSlice2;
   const uint32_t Wk = uint32_t((uint64_t(nbl) + kPBlock - 1) / kPBlock);
   if (HJ3D_RP_WS && Wk > W2 && Wk <= kBuildSlice2Max && fill * Wk * 1.25 <= kBuildStage) W2 = Wk;
-  const bool staged = fill * W2 * 1.25 <= kBuildStage && (uint64_t(nbl) + W2 - 1) / W2 <= kMaxParts;
+  bool staged = fill * W2 * 1.25 <= kBuildStage && (uint64_t(nbl) + W2 - 1) / W2 <= kMaxParts;
+  // HJ3D_B3_HALF: half-width slices (up to 2048 of them), two 512-thread build workgroups per CU
+  const uint32_t Wh = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
+  const bool half = HJ3D_B3_HALF && Wh <= kB3HalfW && fill * std::max(Wh, 1024u) * 1.25 <= kB3HalfStage;
+  if (half) {
+    W2 = std::max(Wh, 1024u);
+    staged = true;
+  }
   const Plan pl = plan_for(nbl, staged ? W2 : kBuildSlice, r.n);
   if (pl.P > kMaxParts) return hipErrorNotSupported;  // > 2048 x 16384 buckets: the direct build
   if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
@@ -1594,9 +1608,14 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   if (nbl && staged) {
-    const uint32_t g = pl.P < uint32_t(ctx->num_cus) ? pl.P : uint32_t(ctx->num_cus);
-    hipLaunchKernelGGL(k_rp_build3, dim3(g), dim3(kJBlock), 0, s, pairs, ps, t->fm,
-                       uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
+    const uint32_t cus = uint32_t(ctx->num_cus) * (half ? 2u : 1u);
+    const uint32_t g = pl.P < cus ? pl.P : cus;
+    if (half)
+      hipLaunchKernelGGL((k_rp_build3<512, kB3HalfW, kB3HalfStage>), dim3(g), dim3(512), 0, s, pairs, ps, t->fm,
+                         uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
+    else
+      hipLaunchKernelGGL((k_rp_build3<kJBlock, kBuildSlice2Max, kBuildStage>), dim3(g), dim3(kJBlock), 0, s, pairs, ps,
+                         t->fm, uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
     hipLaunchKernelGGL(k_rp_build, dim3(pl.P), dim3(kJBlock), 0, s, pairs, ps, t->fm, uint32_t(t->desc.bucket_lo), nbl,

@@ -40,8 +40,9 @@ EXP1 = [
     ("exp1_R1000000_S10000000_uni", [1000000, 10000000, 0, 1.0, 0, 1]),
     # config D (|R| = 1e8, |S| = 1e9): Csr, the 3D plan Nsr (unique build keys) and the non-unique
     # 3D plans Nrs / NrsNU (build on S.a, NB = #dv(S.a)); ~30 min per pair of plans, ~40 GB of host
-    # memory. Plans already in an existing fixture with the same inputs are kept, not recomputed.
-    ("exp1_R100000000_S1000000000_uni", [100000000, 1000000000, 0, 1.0, 0, 1, "nodump", "Csr,Nsr,Nrs,NrsNU"]),
+    # memory (Crs, the chaining table on S: ~45 GB). Plans already in an existing fixture with the same
+    # inputs are kept, not recomputed.
+    ("exp1_R100000000_S1000000000_uni", [100000000, 1000000000, 0, 1.0, 0, 1, "nodump", "Csr,Nsr,Nrs,NrsNU,CsrUU,Crs"]),
 ]
 EXP4 = [
     ("exp4_R3_a2_A2_b2_B1", [3, 2, 2, 2, 1, "dump"]),   # App. A print-relations case
