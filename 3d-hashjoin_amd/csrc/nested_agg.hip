@@ -874,7 +874,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     Pf = std::min<uint64_t>((Pf + G - 1) / G * G, 8192);
     const uint32_t Wf = uint32_t((uint64_t(nbl) + Pf - 1) / Pf);
     const uint32_t Pf2 = (nbl + Wf - 1) / Wf, C = (Pf2 + 1023) / 1024;
-    if (Wf >= 256 && C >= 2 && C <= 16) {
+    if (Wf >= 64 && C >= 2 && C <= 16) {
       two = true;
       W = Wf;
     }

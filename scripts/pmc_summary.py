@@ -7,8 +7,15 @@ pass) and writes a JSON summary (default profiles/<TAG>_pmc.json) that bench.py 
 
 Corrections (MI355X_MICROARCH.md, "HBM [CDNA4]"): rocprofv3 reports FETCH_SIZE / WRITE_SIZE in
 KiB; on gfx950 FETCH_SIZE counts half the bytes of a coalesced streaming read, so it is doubled.
-WRITE_SIZE is taken as reported (exact for 16-B/lane streaming stores; our 8-B/lane stores are
-uncalibrated, noted in the output). For each kernel only the launches of the largest grid are
+Calibrated in round 5 on known byte counts (micro/micro_fetch.hip, profiles/r05_fetch_calibration.json):
+every read the L2 sends to the fabric is a 128-B request (TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ) for
+16-, 8- and 4-B streaming loads, 4-B loads at a 12-B stride, and SPARSE 4-B gathers alike (one word per
+64-B sector moves the whole 128-B line: twice the sector bytes), while FETCH_SIZE counts 64 B per
+request. So 2 x FETCH_SIZE is the read traffic for every access pattern here, and sparse gathers
+really move 128 B per touched line. When the request-size passes are present the read bytes are
+taken from them directly: 128 RDREQ_128B + 64 RDREQ_64B + 32 RDREQ_32B. Writes: streaming 4- and 8-B
+stores go out as 64-B requests (WRITE_SIZE exact); partial lines leave as 32-B requests, so the write
+bytes are 64 WRREQ_64B + 32 (WRREQ - WRREQ_64B) when those passes are present. For each kernel only the launches of the largest grid are
 kept (the probe side S, not the build side R) and the median over those launches is reported.
 Of several template instantiations of one kernel the one LAUNCHED MOST OFTEN is reported under the
 plain name: that is the one the timed steps run (a checksum-folding verification launch runs
@@ -87,6 +94,16 @@ def main():
             d["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * 2
             d["write_bytes"] = d["WRITE_SIZE"] * 1024
             d["traffic_bytes_per_launch"] = d["fetch_bytes"] + d["write_bytes"]
+        if "TCC_EA0_RDREQ_sum" in d:  # read bytes by request size (calibrated, see the docstring)
+            n, n32 = d["TCC_EA0_RDREQ_sum"], d.get("TCC_EA0_RDREQ_32B_sum", 0.0)
+            n64, n128 = d.get("TCC_EA0_RDREQ_64B_sum", 0.0), d.get("TCC_EA0_RDREQ_128B_sum", 0.0)
+            d["read_bytes_req"] = 128 * n128 + 64 * n64 + 32 * n32 + 64 * max(n - n128 - n64 - n32, 0.0)
+        if "TCC_EA0_WRREQ_sum" in d:
+            n, n64 = d["TCC_EA0_WRREQ_sum"], d.get("TCC_EA0_WRREQ_64B_sum", 0.0)
+            d["write_bytes_req"] = 64 * n64 + 32 * (n - n64)
+            d["write_partial_frac"] = (n - n64) / n if n else 0.0
+        if "read_bytes_req" in d and "write_bytes_req" in d:
+            d["traffic_bytes_per_launch"] = d["read_bytes_req"] + d["write_bytes_req"]
         if "TCC_HIT_sum" in d and "TCC_MISS_sum" in d:
             d["l2_hit_rate"] = d["TCC_HIT_sum"] / max(d["TCC_HIT_sum"] + d["TCC_MISS_sum"], 1)
         if "SQ_INSTS_LDS" in d and "SQ_LDS_BANK_CONFLICT" in d:
@@ -100,8 +117,9 @@ def main():
         "tag": a.tag, "workload": a.workload, "nR": a.nR, "nS": a.nS, "emit": bool(a.emit),
         "command": "rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
                    + ("" if a.workload == "B" else f" --workload {a.workload}"),
-        "corrections": "FETCH_SIZE, WRITE_SIZE in KiB; FETCH_SIZE x2 (gfx950 streaming-read undercount); "
-                       "WRITE_SIZE as reported (8-B/lane stores uncalibrated)",
+        "corrections": "FETCH_SIZE, WRITE_SIZE in KiB; FETCH_SIZE x2 (every read request is 128 B, counted as "
+                       "64: calibrated for streaming loads and sparse gathers, profiles/r05_fetch_calibration.json); "
+                       "traffic from the request-size counters where present (128/64/32-B reads, 64/32-B writes)",
         "kernels": kern,
     }
     dst = a.out or os.path.join(ROOT, "profiles", f"{a.tag}_pmc.json")
