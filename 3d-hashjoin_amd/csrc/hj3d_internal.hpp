@@ -85,6 +85,7 @@ struct hj3d_ctx {
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
+  bool nested_2l = false;         // HJ3D_OPT_NESTED_2L: the exact two-level partition + register aggregation
   bool sync_build = false;        // HJ3D_OPT_SYNC_BUILD: nested builds resolved before hj3d_build returns
   bool pk_compact = false;        // HJ3D_OPT_PK_COMPACT: the packed probe's compact slice image where it applies
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup

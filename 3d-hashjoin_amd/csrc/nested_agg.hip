@@ -75,7 +75,11 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
 #endif
 #ifndef HJ3D_NAGG_2L
-#define HJ3D_NAGG_2L 1  // one-level partitions too large for k_nagg_reg: the exact two-level partition (0: A/B)
+// one-level partitions too large for k_nagg_reg: the exact two-level partition + k_nagg_reg. Off by
+// default: at config C it measured 2.93 against 2.25 ms for the one-level partition + k_nagg (the
+// narrow partitions' fixed costs outweigh the saved pair traffic); HJ3D_OPT_NESTED_2L
+// turns it on per context (tests, A/B)
+#define HJ3D_NAGG_2L 0
 #endif
 #ifndef HJ3D_NAGG_WAVES
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
@@ -869,7 +873,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // two-level partition into up to 8192 narrow ones (radix_partition_pairs_2l; skew-safe, unlike the
   // slices' fixed regions), rounded to whole waves of the aggregation's workgroups
   bool two = false;
-  if (!pk && nt == 1 && HJ3D_NAGG_2L && double(n) * W / nbl > 0.85 * kRegCap) {
+  if (!pk && nt == 1 && (HJ3D_NAGG_2L || ctx->nested_2l) && double(n) * W / nbl > 0.85 * kRegCap) {
     uint64_t Pf = std::max<uint64_t>((uint64_t(nbl) + 8191) / 8192, uint64_t(double(n) / (0.6 * kRegCap)));
     Pf = std::min<uint64_t>((Pf + G - 1) / G * G, 8192);
     const uint32_t Wf = uint32_t((uint64_t(nbl) + Pf - 1) / Pf);

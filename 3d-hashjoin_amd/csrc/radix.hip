@@ -250,6 +250,9 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
 #ifndef HJ3D_RP_WS
 #define HJ3D_RP_WS 1  // the build-side partition writes whole segments (k_rp_wscatter; 0: k_rp_scatter, A/B)
 #endif
+#ifndef HJ3D_RP_WS_MIN
+#define HJ3D_RP_WS_MIN 4  // ... from this many tiles per partitioning workgroup on
+#endif
 constexpr int kWsRounds = 8;
 constexpr int kWsSub = kPBlock * kWsRounds;  // 8192 tuples per half tile
 template <int PPT>
@@ -1465,10 +1468,11 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
 #define HJ3D_WS_LAUNCH(PPT, EX)                                                                                   \
   hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, \
                      ntiles, hist, cur, cur_next, ps, out)
-    // whole segments pay once a workgroup takes two or more tiles (its carries ride into a later
-    // tile); with one tile each (config E's relations one at a time) every run is flushed partial
-    // anyway and the plain write-out is faster (0.303 vs 0.317 ms build, same box)
-    const bool ws = HJ3D_RP_WS && ntiles >= 2 * g;
+    // whole segments pay once a workgroup takes several tiles (its carries ride into later tiles):
+    // config C (24 tiles per workgroup) 0.735 -> 0.543 ms; with 1-2.4 tiles each (configs E and B)
+    // most runs are flushed partial anyway and the plain write-out measured faster (E, both tables
+    // in one pass: 51.8 against 2 x 20 us; B: 70.4 against 67.4 us)
+    const bool ws = HJ3D_RP_WS && ntiles >= HJ3D_RP_WS_MIN * g;
     if (ws && PT <= kPBlock) {
       if (ex) HJ3D_WS_LAUNCH(1, true);
       else HJ3D_WS_LAUNCH(1, false);

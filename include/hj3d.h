@@ -194,7 +194,12 @@ enum {
    * they return (they wait for its counts and run the sort build there if the LDS aggregation build
    * gave up), so the build relation's device memory may be released as soon as the call returns.
    * Default: the table finishes at its next use (see hj3d_build). */
-  HJ3D_OPT_SYNC_BUILD = 13
+  HJ3D_OPT_SYNC_BUILD = 13,
+  /* HJ3D_OPT_NESTED_2L (0/1, default 0): a nested build whose one-level partitions are too large for
+   * the register aggregation takes the exact two-level partition into narrow partitions (up to 8192,
+   * skew-safe) and aggregates them in registers. Measured slower at config C (2.93 against 2.25 ms),
+   * so off by default; kept for A/B measurements and its parity test. */
+  HJ3D_OPT_NESTED_2L = 14
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

@@ -637,12 +637,16 @@ def test_nested_build_two_level_partition(ctx, zipf):
     R = O.tuples3(Rk, np.zeros_like(Rk))
     S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
     e = O.nested_plan(S, 1, R, 0, nb, True)
-    t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
-    got = hj3d.exp1_plan(ctx, "Nrs", dev(R), dev(S), nb, table=t)
-    path = t.build_path()
-    st = t.stats()
-    t.close()
-    assert path == "nested_agg_2l_reg" or path == "nested_sort", path
+    ctx.nested_2l(True)
+    try:
+        t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+        got = hj3d.exp1_plan(ctx, "Nrs", dev(R), dev(S), nb, table=t)
+        path = t.build_path()
+        st = t.stats()
+        t.close()
+    finally:
+        ctx.nested_2l(False)
+    assert path == "nested_agg_2l_reg", path
     assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_unnest, e.c_top)
     assert got["out"] == e.out
     assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
