@@ -12,6 +12,14 @@
 
 #include "hj3d_internal.hpp"
 
+#include <atomic>
+
+namespace hj3d {
+static std::atomic<uint64_t> g_launches{0};
+void note_launch() { g_launches.fetch_add(1, std::memory_order_relaxed); }
+uint64_t launch_total() { return g_launches.load(std::memory_order_relaxed); }
+}  // namespace hj3d
+
 using namespace hj3d;
 
 namespace {
@@ -462,6 +470,8 @@ const char* hj3d_table_build_path(const hj3d_table* t) {
   std::snprintf(w->path_buf, sizeof(w->path_buf), "%s?", t->path);
   return w->path_buf;
 }
+
+uint64_t hj3d_launch_count(void) { return hj3d::launch_total(); }
 
 hj3d_status hj3d_table_finish(hj3d_ctx* ctx, hj3d_table* t) {
   if (!ctx || !t) return HJ3D_EINVAL;

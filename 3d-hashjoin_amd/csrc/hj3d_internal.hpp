@@ -13,6 +13,19 @@
 #include "hj3d_device.hpp"
 
 namespace hj3d {
+// Kernel launches of this library, process-wide (hj3d_launch_count: the bench reports launches per
+// step). Every launch site goes through hipLaunchKernelGGL (redefined below) or KernelSpan::launch.
+void note_launch();
+uint64_t launch_total();
+}  // namespace hj3d
+#undef hipLaunchKernelGGL
+#define hipLaunchKernelGGL(kernelName, ...)                   \
+  do {                                                        \
+    ::hj3d::note_launch();                                    \
+    hipLaunchKernelGGLInternal((kernelName), __VA_ARGS__);    \
+  } while (0)
+
+namespace hj3d {
 
 constexpr int kBlock = 256;           // 4 waves; the default workgroup of every streaming kernel
 constexpr uint32_t kInvalid = 0xFFFFFFFFu;
@@ -471,6 +484,7 @@ struct KernelSpan {
   }
   template <typename F, typename... Args>
   void launch(F kernel, dim3 grid, dim3 block, hipStream_t s, Args... args) {
+    if (a) note_launch();
     if (a) hipExtLaunchKernelGGL(kernel, grid, block, 0, s, a, b, 0, args...);
     else hipLaunchKernelGGL(kernel, grid, block, 0, s, args...);
   }

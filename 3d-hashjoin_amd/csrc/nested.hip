@@ -256,6 +256,9 @@ constexpr uint32_t kHeavyOut = 8192;
 #define HJ3D_EXP_U 4  // k_expand_light: outputs per thread and step (1: one at a time, A/B)
 #endif
 constexpr int kExpU = HJ3D_EXP_U;
+#ifndef HJ3D_EXP_XCD
+#define HJ3D_EXP_XCD 0  // k_expand_light: slot blocks XCD-ordered (1: A/B; config D probe 6.19 -> 6.15 ms, C 0.791 -> 0.795 ms: off)
+#endif
 #ifndef HJ3D_RN_XCD
 #define HJ3D_RN_XCD 1  // nested probe on slices wider than LDS: shared slices, XCD-ordered blocks (0: A/B)
 #endif
@@ -301,7 +304,15 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t n
   __shared__ uint64_t lpos[kBlock];
   __shared__ uint32_t wsum[kBlock / kWave];
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  const uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  // XCD-ordered blocks (HJ3D_EXP_XCD): workgroup b runs on XCD b % 8, so consecutive slot blocks
+  // (probe tuples of one slice: their keys' sub rows lie in one window of `sub`) would read that
+  // window into eight L2s; XCD x takes the x-th eighth of the blocks instead
+  uint32_t bid = blockIdx.x;
+  if (HJ3D_EXP_XCD) {
+    const uint32_t per = gridDim.x / 8;
+    if (bid < per * 8) bid = (bid % 8) * per + bid / 8;
+  }
+  const uint64_t i = uint64_t(bid) * kBlock + threadIdx.x;
   uint32_t c = 0, z = 0, pr = 0;
   uint64_t pos = 0;
   if (i < nslots) {
@@ -378,7 +389,7 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t n
     }
   }
   // the output checksums only (the counts are the probe's): no partials without HJ3D_PROBE_CHECKSUM
-  if (CK) block_store<kProbeFields, 1>(acc, partials + uint64_t(blockIdx.x) * kProbeFields);
+  if (CK) block_store<kProbeFields, 1>(acc, partials + uint64_t(bid) * kProbeFields);
 }
 
 // hoff[q] = first flattened output of heavy slot q (exclusive scan of their counts, one workgroup;

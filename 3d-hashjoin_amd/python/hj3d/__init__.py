@@ -117,6 +117,7 @@ def lib():
         "hj3d_build_many": (st, [p, C.POINTER(p), R, u32]),
         "hj3d_table_build_path": (C.c_char_p, [p]),
         "hj3d_table_finish": (st, [p, p]),
+        "hj3d_launch_count": (u64, []),
         "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
         "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe": (st, [p, p, R, u32, p, u64]),

@@ -827,6 +827,7 @@ def main_single_config(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     ctx = hj3d.Context(0)
+    launches = []  # (build, probe) kernel launches of each step
     ctx.timing(True)
     if args.nested_build == "radix":
         ctx.nested_radix(True)
@@ -847,11 +848,14 @@ def main_single_config(args):
         fx = fixture(f"exp1_R{nR}_S{nS}_zipf{str(args.theta).replace('.', '').rstrip('0') or '0'}")
 
         def step(ev):
+            l0 = hj3d.lib().hj3d_launch_count()
             ev[0].record()
             table.build(relS)
             ev[1].record()
+            l1 = hj3d.lib().hj3d_launch_count()
             ctx.probe(table, relR, unnest=True, out=out, fetch=False, checksum=state["ck"])
             ev[2].record()
+            launches.append((l1 - l0, hj3d.lib().hj3d_launch_count() - l1))
 
     else:
         log2R, a, A, b, B = args.log2R, 3, 4, 2, 2
@@ -865,17 +869,21 @@ def main_single_config(args):
         fx = fixture(f"exp4_R{log2R}_a{a}_A{A}_b{b}_B{B}")
 
         def step(ev):
+            l0 = hj3d.lib().hj3d_launch_count()
             ev[0].record()
             ctx.build_many([ts, tt], [relS, relT])  # one launch sequence for both tables
             ev[1].record()
+            l1 = hj3d.lib().hj3d_launch_count()
             ctx.probe2(ts, tt, relR, fetch=False)
             ev[2].record()
+            launches.append((l1 - l0, hj3d.lib().hj3d_launch_count() - l1))
 
     torch.cuda.synchronize()
     for _ in range(args.warmup):
         step(_events(torch, 3))
     torch.cuda.synchronize()
     evs = [_events(torch, 3) for _ in range(args.steps)]
+    del launches[:]  # the timed steps' kernel launches (build, probe), from the library's own counter
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for e in evs:
@@ -884,6 +892,7 @@ def main_single_config(args):
     wall_ms = (time.perf_counter() - t0) * 1e3 / args.steps
     build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    timed_launches = launches[-1] if launches else (None, None)
 
     verify = {}
     if args.workload == "C":
@@ -946,6 +955,8 @@ def main_single_config(args):
         "ms_per_step": wall_ms, "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
         "data": data, "config": {"workload": workload, "config": args.workload, "parallelism": "single GPU"},
         "build_ms": build_ms, "probe_ms": probe_ms,
+        "launches_per_step": {"build": timed_launches[0], "probe": timed_launches[1],
+                              "note": "kernel launches of libhj3d per timed step (hj3d_launch_count)"},
         "roofline": {"bound": "hbm", "kernel": "phase (build / probe)", "unit": "GB/s", "peak": PEAK_HBM_GBS,
                      "achieved": probe_bytes / (probe_ms * 1e-3) / 1e9,
                      "frac": probe_bytes / (probe_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,

@@ -215,6 +215,9 @@ enum {
                              * of more than 1024 slices: its second partition level (k_pk_split) */
   HJ3D_T_NTIMERS = 6
 };
+/* Kernel launches issued by this library so far, all contexts of the process (diagnostic: the bench
+ * reports launches per step). */
+uint64_t hj3d_launch_count(void);
 hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
 hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count);
 hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx);

@@ -631,7 +631,7 @@ def test_nested_build_two_level_partition(ctx, zipf):
     ~12K pairs. Counters, output checksums and statistics equal the oracle's."""
     import hj3d
     rng = np.random.default_rng(53 + zipf)
-    nb, nS, dom = 300_000, 12_000_000, 600_000
+    nb, nS, dom = 300_000, 12_000_000, 300_000  # ~1 key per bucket (NB = #dv, as the plans size it)
     Sa = (np.minimum(rng.zipf(1.4, nS) - 1, dom - 1) if zipf else rng.integers(0, dom, nS)).astype(np.uint32)
     Rk = rng.permutation(dom).astype(np.uint32)[:400_000]
     R = O.tuples3(Rk, np.zeros_like(Rk))
