@@ -74,6 +74,9 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_REG
 #define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
 #endif
+#ifndef HJ3D_NAGG_REG_FILL
+#define HJ3D_NAGG_REG_FILL 0.85  // largest mean partition (fraction of the register capacity) for k_nagg_reg
+#endif
 #ifndef HJ3D_NAGG_2L
 // one-level partitions too large for k_nagg_reg: the exact two-level partition + k_nagg_reg. Off by
 // default: at config C it measured 2.93 against 2.25 ms for the one-level partition + k_nagg (the
@@ -972,7 +975,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)
   const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
-  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= 0.85 * kRegCap && capr <= 4 * kRegBlock &&
+  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= HJ3D_NAGG_REG_FILL * kRegCap && capr <= 4 * kRegBlock &&
                    reg_lds_words(capr, W) * 4 <= 160 * 1024;
   if (reg) {
     const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);

@@ -89,12 +89,13 @@ inline FastDiv make_div(uint32_t d) {
 // (nt0 of them), its partitions follow at P + p and its pairs after relation 0's.
 struct RelTiles {
   RelView r0, r1;
-  uint32_t nt0;  // kPTile-tiles of r0
+  uint32_t nt0;  // tiles of r0
   uint32_t P;    // partitions per relation
+  uint32_t tsz = kPTile;  // tuples per tile
   __device__ __forceinline__ bool second(uint32_t tile) const { return tile >= nt0; }
   __device__ __forceinline__ const RelView& rel(uint32_t tile) const { return tile >= nt0 ? r1 : r0; }
   __device__ __forceinline__ uint64_t base(uint32_t tile) const {
-    return uint64_t(tile >= nt0 ? tile - nt0 : tile) * kPTile;
+    return uint64_t(tile >= nt0 ? tile - nt0 : tile) * tsz;
   }
   __device__ __forceinline__ uint32_t pofs(uint32_t tile) const { return tile >= nt0 ? P : 0u; }
 };
@@ -105,18 +106,19 @@ struct RelTiles {
 // size) and keeps the run's offset in its row hist[g * P + p]. The order of the workgroups' runs
 // inside a partition is the atomics' order: no counter depends on it (build3 places rows by rank,
 // the nested builds aggregate), and no scan over the P x G counts is needed.
+template <int ROUNDS>
 __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelTiles rt, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                      uint32_t P, uint32_t ntiles, uint32_t* __restrict__ hist,
                                                      uint32_t* __restrict__ cur) {
   __shared__ uint32_t cnt[kMaxParts];
   for (uint32_t p = threadIdx.x; p < P; p += kPBlock) cnt[p] = 0;
   __syncthreads();
-  uint32_t key[kPRounds];
+  uint32_t key[ROUNDS];
   auto load = [&](uint32_t tile) __attribute__((always_inline)) {
     const RelView& r = rt.rel(tile);
     const uint64_t b = rt.base(tile);
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {  // all loads of the tile in flight together
+    for (int j = 0; j < ROUNDS; ++j) {  // all loads of the tile in flight together
       const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
       key[j] = tile < ntiles && i < r.n ? key_ld(r, i) : 0u;
     }
@@ -126,15 +128,15 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelTiles rt, FastMod fm, ui
     const RelView& r = rt.rel(tile);
     const uint64_t b = rt.base(tile);
     const uint32_t pofs = rt.pofs(tile);
-    uint32_t bl[kPRounds];
+    uint32_t bl[ROUNDS];
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
+    for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
       bl[j] = i < r.n ? fm.mod(murmur32(key[j])) - lo : nbl;
     }
     load(tile + gridDim.x);  // next tile: loads in flight
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j)
+    for (int j = 0; j < ROUNDS; ++j)
       if (bl[j] < nbl) atomicAdd(&cnt[pofs + fw.div(bl[j])], 1u);
   }
   __syncthreads();
@@ -156,23 +158,27 @@ __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum);
 // before the current tile's write-out, so the CU's reads and writes overlap.
 // Partition starts: an LDS scan of the P partition sizes (k_rp_hist's cursors) in every workgroup;
 // workgroup 0 writes them to ps[0..P] and clears the other cursor set for the next call.
+template <int ROUNDS>
 __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fw,
                                                         uint32_t P, uint32_t ntiles, const uint32_t* __restrict__ offs,
                                                         const uint32_t* __restrict__ cur, uint32_t* __restrict__ cur_next,
                                                         uint32_t* __restrict__ ps, uint2* __restrict__ out) {
-  __shared__ uint2 stage[kPTile];
+  constexpr int kTile = kPBlock * ROUNDS;
+  __shared__ uint2 stage[kTile];
   __shared__ uint32_t loc[kMaxParts];   // local counts, then local run starts
   __shared__ uint32_t gb[kMaxParts];    // global run start of each partition for this tile
-  __shared__ uint32_t wsum[kPBlock / kWave];
+  // the scans' wave sums live in the stage: every scan runs while the stage holds nothing (before
+  // the tile is staged; the previous tile's write-out ended at a barrier)
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(stage);
   // explicit row ids are loaded with the keys, a tile ahead (loading them at the stage write after
   // the ranking phase waited for every load separately: one round trip per tuple and round)
   const bool explicit_rows = rt.r0.row_off != 0xFFFFFFFFu;  // (both relations alike)
-  uint32_t h[kPRounds], rw[kPRounds];
+  uint32_t h[ROUNDS], rw[ROUNDS];
   auto load = [&](uint32_t tile) __attribute__((always_inline)) {
     const RelView& r = rt.rel(tile);
     const uint64_t b = rt.base(tile);
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
+    for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
       const bool ok = tile < ntiles && i < r.n;
       h[j] = ok ? key_ld(r, i) : 0u;
@@ -197,10 +203,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
     const RelView& r = rt.rel(tile);
     const uint64_t base = rt.base(tile);
     const uint32_t pofs = rt.pofs(tile);
-    uint32_t rk[kPRounds];
+    uint32_t rk[ROUNDS];
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
+    for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
       h[j] = murmur32(h[j]);
       const uint32_t bl = fm.mod(h[j]) - lo;
@@ -214,10 +220,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
     __syncthreads();
     const uint32_t m = lds_excl_scan(loc, P, wsum);  // staged tuples of this tile
 #pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
+    for (int j = 0; j < ROUNDS; ++j) {
       if (rk[j] == kInvalid) continue;
       const uint64_t i = base + uint64_t(j) * kPBlock + threadIdx.x;
-      stage[loc[rk[j] >> 14] + (rk[j] & (kPTile - 1))] = make_uint2(h[j], explicit_rows ? rw[j] : r.row(i));
+      stage[loc[rk[j] >> 14] + (rk[j] & (kTile - 1))] = make_uint2(h[j], explicit_rows ? rw[j] : r.row(i));
     }
     __syncthreads();
     load(tile + gridDim.x);  // next tile: loads in flight
@@ -252,6 +258,12 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
 #endif
 #ifndef HJ3D_RP_WS_MIN
 #define HJ3D_RP_WS_MIN 4  // ... from this many tiles per partitioning workgroup on
+#endif
+#ifndef HJ3D_RP_SMALL_ROUNDS
+#define HJ3D_RP_SMALL_ROUNDS 8  // below that: the plain scatter on tiles of this many x 1024 tuples (16: A/B)
+#endif
+#ifndef HJ3D_RP_SMALL_WGS
+#define HJ3D_RP_SMALL_WGS 1  // ... with this many workgroups per CU (its ~100 VGPRs leave room for one)
 #endif
 constexpr int kWsRounds = 8;
 constexpr int kWsSub = kPBlock * kWsRounds;  // 8192 tuples per half tile
@@ -1436,12 +1448,25 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   // r1: a second relation of the same table geometry, partitioned in the same two launches (its
   // partitions follow at P .. 2P - 1, its pairs after r's)
   const uint32_t PT = r1 ? 2 * pl.P : pl.P;
-  const uint32_t nt0 = pl.ntiles, nt1 = r1 ? uint32_t((r1->n + kPTile - 1) / kPTile) : 0u;
+  const uint32_t cus = uint32_t(ctx->num_cus);
+  // whole segments (16384-tuple tiles, k_rp_wscatter) once a workgroup takes several tiles (their
+  // carries ride into later tiles): config C (24 tiles per workgroup) 0.735 -> 0.543 ms; with 1-2.4
+  // tiles each (configs E and B) most runs are flushed partial anyway and the plain write-out
+  // measured faster (E, both tables in one pass: 51.8 against 2 x 20 us; B: 70.4 against 67.4 us).
+  // Small inputs take the plain scatter on HJ3D_RP_SMALL_ROUNDS x 1024-tuple tiles instead (more,
+  // evenly spread tiles: config B's 611 tiles of 16384 gave 157 workgroups 2 and 99 of them 3),
+  // one workgroup per CU.
+  const uint32_t nt16 = uint32_t((r.n + kPTile - 1) / kPTile) + (r1 ? uint32_t((r1->n + kPTile - 1) / kPTile) : 0u);
+  const bool ws = HJ3D_RP_WS && nt16 >= HJ3D_RP_WS_MIN * (nt16 < cus ? nt16 : cus);
+  const uint32_t rounds = ws ? uint32_t(kPRounds) : uint32_t(HJ3D_RP_SMALL_ROUNDS);
+  const uint32_t tsz = kPBlock * rounds;
+  const uint32_t nt0 = uint32_t((r.n + tsz - 1) / tsz), nt1 = r1 ? uint32_t((r1->n + tsz - 1) / tsz) : 0u;
   const uint32_t ntiles = nt0 + nt1;
   if (ntiles == 0) return hipMemsetAsync(ps, 0, (uint64_t(PT) + 1) * sizeof(uint32_t), s);
   if (PT > kMaxParts) return hipErrorNotSupported;
   // G persistent workgroups in both passes, one row of run offsets per workgroup
-  const uint32_t g = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
+  const uint32_t gmax = ws ? cus : cus * HJ3D_RP_SMALL_WGS;
+  const uint32_t g = ntiles < gmax ? ntiles : gmax;
   if ((e = ctx->scratch[kScrPHist].ensure(uint64_t(PT) * g * sizeof(uint32_t))) != hipSuccess) return e;
   uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
   if (!ctx->part_cur.p) {
@@ -1456,11 +1481,16 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   rt.r1 = r1 ? view_of(*r1) : rt.r0;
   rt.nt0 = nt0;
   rt.P = pl.P;
+  rt.tsz = tsz;
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
   {
     PhaseTimer tm(ctx, t_hist);
-    hipLaunchKernelGGL(k_rp_hist, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles, hist,
-                       cur);
+    if (rounds == kPRounds)
+      hipLaunchKernelGGL(k_rp_hist<kPRounds>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles,
+                         hist, cur);
+    else
+      hipLaunchKernelGGL(k_rp_hist<HJ3D_RP_SMALL_ROUNDS>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw,
+                         PT, ntiles, hist, cur);
   }
   {
     PhaseTimer tm(ctx, t_scatter);
@@ -1468,11 +1498,6 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
 #define HJ3D_WS_LAUNCH(PPT, EX)                                                                                   \
   hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, \
                      ntiles, hist, cur, cur_next, ps, out)
-    // whole segments pay once a workgroup takes several tiles (its carries ride into later tiles):
-    // config C (24 tiles per workgroup) 0.735 -> 0.543 ms; with 1-2.4 tiles each (configs E and B)
-    // most runs are flushed partial anyway and the plain write-out measured faster (E, both tables
-    // in one pass: 51.8 against 2 x 20 us; B: 70.4 against 67.4 us)
-    const bool ws = HJ3D_RP_WS && ntiles >= HJ3D_RP_WS_MIN * g;
     if (ws && PT <= kPBlock) {
       if (ex) HJ3D_WS_LAUNCH(1, true);
       else HJ3D_WS_LAUNCH(1, false);
@@ -1481,8 +1506,8 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
       else HJ3D_WS_LAUNCH(2, false);
     } else
 #undef HJ3D_WS_LAUNCH
-      hipLaunchKernelGGL(k_rp_scatter, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles,
-                         hist, cur, cur_next, ps, out);
+      hipLaunchKernelGGL(k_rp_scatter<HJ3D_RP_SMALL_ROUNDS>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local,
+                         pl.fw, PT, ntiles, hist, cur, cur_next, ps, out);
   }
   return hipGetLastError();
 }
