@@ -53,7 +53,7 @@ bool rel_ok(const hj3d_rel* r) {
   return true;
 }
 
-constexpr int kResFields = 16;
+// (kResFields: hj3d_device.hpp)
 // result-slot words beyond the counters: n_out before the current probe call, and a sticky flag
 // set when a call's non-dense output exceeded its own buffer (accumulated strands included)
 constexpr int kResOutMark = 14, kResOvf = 15;
@@ -179,9 +179,9 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
   }
 }
 
-hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable) {
-  if (!ctx) return HJ3D_EINVAL;
-  ctx->timing = enable != 0;
+hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int mode) {
+  if (!ctx || mode < 0 || mode > 2) return HJ3D_EINVAL;
+  ctx->timing = mode;
   return HJ3D_OK;
 }
 
@@ -308,13 +308,21 @@ hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
 // (word 1 = main records; word 3 = the aggregation build's give-up flag) travel to pinned host
 // memory behind the build and are read at the table's next use (table_resolve), so consecutive
 // builds (experiment 4's two tables) do not wait for each other.
-static hipError_t nested_pending(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& build, bool agg) {
+// The aggregation builds write the host copy from their last kernel (k_nagg_mains), so their pinned
+// mirror must exist before the build (nested_host_counts); the other nested builds copy it.
+static hipError_t nested_host_counts(hj3d_table* t) {
   hipError_t e = hipSuccess;
   if (!t->hc) {
     e = hipHostMalloc(reinterpret_cast<void**>(&t->hc), 4 * sizeof(uint64_t), hipHostMallocDefault);
     if (e == hipSuccess) e = hipEventCreateWithFlags(&t->hc_ev, hipEventDisableTiming);
   }
-  if (e == hipSuccess) e = hipMemcpyAsync(t->hc, t->counts.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
+  return e;
+}
+static hipError_t nested_pending(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& build, bool agg) {
+  hipError_t e = nested_host_counts(t);
+  // (agg: k_nagg_mains wrote the mirror)
+  if (e == hipSuccess && !agg)
+    e = hipMemcpyAsync(t->hc, t->counts.p, 4 * sizeof(uint64_t), hipMemcpyDeviceToHost, ctx->stream);
   if (e == hipSuccess) e = hipEventRecord(t->hc_ev, ctx->stream);
   t->pending = e == hipSuccess;
   t->pending_agg = agg;
@@ -341,7 +349,9 @@ hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d
     {
       PhaseTimer tm(ctx, HJ3D_T_BUILD);
       for (uint32_t k = 0; k < 2; ++k) tables[k]->pending = false;
-      e = nested_build_agg_many(ctx, tables, builds, 2, ctx->stream, &path);
+      e = nested_host_counts(tables[0]);
+      if (e == hipSuccess) e = nested_host_counts(tables[1]);
+      if (e == hipSuccess) e = nested_build_agg_many(ctx, tables, builds, 2, ctx->stream, &path);
     }
     if (e == hipErrorOutOfMemory) {
       (void)hipGetLastError();
@@ -400,7 +410,8 @@ static hipError_t build_one(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build)
                                                   : hipErrorNotSupported;
     bool agg = false;
     if (e == hipErrorNotSupported && !ctx->nested_sort) {
-      e = nested_build_agg(ctx, t, *build, ctx->stream, &t->path);
+      e = nested_host_counts(t);
+      if (e == hipSuccess) e = nested_build_agg(ctx, t, *build, ctx->stream, &t->path);
       if (e == hipErrorOutOfMemory) {  // partition / slice scratch did not fit: the sort build
         (void)hipGetLastError();
         e = hipErrorNotSupported;
@@ -435,7 +446,11 @@ namespace hj3d {
 hipError_t table_resolve(hj3d_ctx* ctx, hj3d_table* t) {
   if (!t->pending) return hipSuccess;
   t->pending = false;
-  hipError_t e = hipEventSynchronize(t->hc_ev);
+  // polled, not waited for: the build is short (config E: ~0.3 ms) and the probe's launches follow
+  // as soon as it lands (a blocking wait's wake-up left the GPU idle for ~20 us)
+  hipError_t e;
+  while ((e = hipEventQuery(t->hc_ev)) == hipErrorNotReady) {
+  }
   if (e != hipSuccess) {
     t->built = false;
     return e;
@@ -656,10 +671,10 @@ hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* t
   if (hipError_t re = resolve(ctx, tt); re != hipSuccess) return from_hip(ctx, re, "hj3d_probe2");
   PhaseTimer tm(ctx, HJ3D_T_PROBE);
   uint64_t* res = ctx->res.as<uint64_t>();
-  hipError_t e = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
-  if (e == hipSuccess) {
+  hipError_t e;
+  {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
-    e = probe2(ctx, ts, tt, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    e = probe2(ctx, ts, tt, *probe, flags, out_dev, out_cap, res, ctx->stream);  // (clears res itself)
   }
   return from_hip(ctx, e, "hj3d_probe2");
 }

@@ -17,6 +17,9 @@
 namespace hj3d {
 namespace {
 
+#ifndef HJ3D_NDU_DIAG
+#define HJ3D_NDU_DIAG 0  // diagnostic variant (checksums wrong): 1 light matches skip their sub-row reads
+#endif
 constexpr int kItems = 2;
 constexpr uint64_t kInline2 = 64;
 constexpr int kF = 12;  // c_probe_rs, cmp_rs, c_probe_rt, cmp_rt, unnest_1, unnest_2, top, sum_a, sum_b, sum_c, sum_h, xor_h
@@ -118,7 +121,7 @@ __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const N
   a[5] += prod;
   a[6] += prod;
   if (prod <= kInline2) {
-    light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w);
+    if (!HJ3D_NDU_DIAG) light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w);
   } else {
     const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
     heavy[slot] = Heavy2{pr, ms, mt, 0};
@@ -292,12 +295,16 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
   (void)out;
   (void)out_cap;
   if (flags & HJ3D_PROBE_EMIT) return hipErrorNotSupported;
-  if (r.n == 0) return hipSuccess;
+  // the result slot and the heavy-item counter start at zero: one launch clears both (with the
+  // partitioner's own counters on the partitioned path)
+  ZeroList z;
+  z.add(res, kResFields);
+  if (r.n == 0) return zero_words(z, s);
   hipError_t e = ctx->scratch[kScrC].ensure(r.n * sizeof(Heavy2) + 16);
   if (e != hipSuccess) return e;
   uint64_t* nheavy = ctx->scratch[kScrC].as<uint64_t>();
   Heavy2* heavy = reinterpret_cast<Heavy2*>(nheavy + 2);
-  if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint64_t), s)) != hipSuccess) return e;
+  z.add(nheavy, 1);
   const RelView v = view_of(r);
   const unsigned g = grid_for(ctx, r.n, kBlock * kItems);
   if (ts->desc.kind == HJ3D_NESTED) {
@@ -314,7 +321,7 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
       ProbeParts pp;
       // no output: the regions' output slots are not needed
       e = radix_partition_probe(ctx, ts, r, uint32_t(0.8 * kProbeLdsWords / (2.0 + 4.0 * fill)), &pp, s, nullptr,
-                                nullptr, false);
+                                nullptr, false, &z);
       if (e == hipSuccess) {
         const uint32_t nblocks = pp.P * pp.splits;
         hipLaunchKernelGGL(k_ndu_seg<true>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,
@@ -325,12 +332,15 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
                            res);
       }
     }
-    if (e == hipErrorNotSupported)
+    if (e == hipErrorNotSupported) {
+      if ((e = zero_words(z, s)) != hipSuccess) return e;
       hipLaunchKernelGGL(k_ndu, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res);
-    else if (e != hipSuccess)
+    } else if (e != hipSuccess) {
       return e;
+    }
     hipLaunchKernelGGL(k_ndu_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res);
   } else {
+    if ((e = zero_words(z, s)) != hipSuccess) return e;
     CTab S{ts->off.as<const uint32_t>(), ts->ent.as<const uint2>(), ts->fm, uint32_t(ts->desc.bucket_lo),
            ts->nb_local};
     CTab T{tt->off.as<const uint32_t>(), tt->ent.as<const uint2>(), tt->fm, uint32_t(tt->desc.bucket_lo),

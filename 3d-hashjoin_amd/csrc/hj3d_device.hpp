@@ -112,6 +112,7 @@ struct RelView {
 struct ProbeAcc {
   uint64_t n_probe, n_matched, n_out, n_cmps, sum_a, sum_b, sum_c, sum_h, xor_h;
 };
+constexpr int kResFields = 16;   // u64 words of the context's result slot (hj3d_probe_result + marks)
 constexpr int kProbeFields = 9;  // xor_h is the last field (reduced with xor)
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {

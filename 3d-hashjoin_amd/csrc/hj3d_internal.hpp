@@ -85,7 +85,7 @@ struct hj3d_ctx {
   bool res_overflow = false;  // a dense-output probe of the strand had fewer slots than tuples
   bool res_accumulated = false;
   // phase timers
-  bool timing = false;
+  int timing = 0;  // hj3d_ctx_timing: 0 off, 1 every timer, 2 dispatch-carried kernel spans only
   bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
   uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
   bool nested_radix = false;      // HJ3D_OPT_NESTED_RADIX
@@ -251,6 +251,22 @@ __device__ __forceinline__ uint32_t lb_exclusive(const uint64_t* status, uint32_
 // scan.hip: exclusive prefix sum of n values into out[0..n], out[n] = total. in may alias out.
 hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, uint64_t n, hipStream_t s);
 hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s);
+// scan.hip: up to four arrays of u64 words zeroed by one launch (instead of a runtime fill each,
+// ~5 us apiece between the kernels of a short strand)
+struct ZeroList {
+  uint64_t* p[4] = {nullptr, nullptr, nullptr, nullptr};
+  uint32_t n[4] = {0, 0, 0, 0};
+  bool add(uint64_t* q, uint32_t words) {  // false: the list is full
+    for (int k = 0; k < 4; ++k)
+      if (!p[k]) {
+        p[k] = q;
+        n[k] = words;
+        return true;
+      }
+    return false;
+  }
+};
+hipError_t zero_words(const ZeroList& z, hipStream_t s);
 // sort.hip: stable LSD radix sort of (key,val) u32 pairs on key bits [0, bits). Result lands in
 // (k0,v0); (k1,v1) is a same-size scratch double buffer. With in_alt, an odd number of passes
 // leaves the result in (k1,v1) and sets *in_alt instead of copying it back.
@@ -296,9 +312,11 @@ struct ProbeParts {
 };
 // slots = false: the caller never writes output (the dense output slots of the regions, a
 // transpose + scan of the region counts, are not computed; pp->seg is then undefined)
+// also (optional): words the caller needs zeroed before the strand, cleared by the same launch as
+// the partitioner's overflow counters (only on success: on hipErrorNotSupported nothing was launched)
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
                                  hipStream_t s, const SelArgs* sel = nullptr, unsigned long long** npass = nullptr,
-                                 bool slots = true);
+                                 bool slots = true, const ZeroList* also = nullptr);
 // chain_pk.hip: the unique chaining probe on packed pairs (partitioner + probe, two launches; the
 // result slot is set, or added to with HJ3D_PROBE_ACCUMULATE, by the probe kernel itself: no fill
 // before it). hipErrorNotSupported when the geometry does not pack (use radix_probe).
@@ -446,7 +464,7 @@ struct PhaseTimer {
   int phase;
   hipEvent_t a = nullptr;
   PhaseTimer(hj3d_ctx* c, int p) : ctx(c), phase(p) {
-    if (ctx->timing && p >= 0 && (a = take_event(ctx))) (void)hipEventRecord(a, ctx->stream);
+    if (ctx->timing == 1 && p >= 0 && (a = take_event(ctx))) (void)hipEventRecord(a, ctx->stream);
   }
   ~PhaseTimer() {
     if (!a) return;

@@ -88,6 +88,23 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
 
+#ifndef HJ3D_NAGG_CLK
+#define HJ3D_NAGG_CLK 0  // diagnostic: per-workgroup phase clocks of k_nagg (read by hj3d_diag_nagg_clk)
+#endif
+[[maybe_unused]] constexpr uint32_t kClkParts = 16384, kClkPts = 8;
+#if HJ3D_NAGG_CLK
+__device__ uint64_t g_nagg_clk[kClkParts * kClkPts];
+#endif
+// point k of partition gp's timeline: 100 MHz wall clock (point 7: the workgroup's dispatch index)
+__device__ __forceinline__ void nagg_clk(uint32_t gp, int k) {
+#if HJ3D_NAGG_CLK
+  if (threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + k] = k == 7 ? blockIdx.x : wall_clock64();
+#else
+  (void)gp;
+  (void)k;
+#endif
+}
+
 __device__ __forceinline__ uint32_t slot_of(uint32_t h, uint32_t cap) { return __umulhi(h * 0x9E3779B1u, cap); }
 // per-key probe step in [1, cap) (double hashing: no primary clusters, so the longest probe
 // sequence among a wave's 64 lanes, which the whole wave waits for, stays short)
@@ -200,6 +217,7 @@ struct NaggTabs {
   uint32_t* sub[2] = {nullptr, nullptr};
   uint4* main[2] = {nullptr, nullptr};
   uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
+  uint64_t* hc[2] = {nullptr, nullptr};      // the tables' pinned host mirrors of the counts words (or none)
   uint32_t* sink = nullptr;  // pass B's stores of items without a row (the context's store-sink words)
 };
 // one partition (global index gp) of k_nagg
@@ -226,6 +244,8 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
   // (table ti's sub rows are numbered from its first pair: ps[ti * P])
   const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = ps[ti * tabs.P];
+  nagg_clk(gp, 0);
+  nagg_clk(gp, 7);
   const int lane = threadIdx.x & 63;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   if constexpr (PK) {
@@ -302,6 +322,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       ovf = 0;
     }
     __syncthreads();
+    nagg_clk(gp, 1);
     // ---- pass A: count and min row per key ----
     uint2 v[kAggU], nv[kAggU];
     restart();
@@ -370,6 +391,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
     }
     __syncthreads();
+    nagg_clk(gp, 2);
     if (ovf) {  // too many distinct keys for one round: retry the first half of the range
       if (c1 - c0 <= kAggMinSpan) {  // > ~24 keys per bucket: the sort-based build instead
         if (threadIdx.x == 0) atomicOr(fail, 1u);
@@ -413,6 +435,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     }
     for (uint32_t k = threadIdx.x; k < c1 - c0; k += BLOCK) off[b0 + c0 + k] = mrun + bcnt[k];
     __syncthreads();
+    nagg_clk(gp, 3);
     // ---- pass B: rows into their keys' sub ranges ----
     restart();
     if (HJ3D_NAGG_STATIC) {
@@ -470,11 +493,13 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
     }
+    nagg_clk(gp, 4);
     mrun += nk;
     srun += nrows;
     c0 = c1;
     __syncthreads();
   }
+  nagg_clk(gp, 5);
   if (threadIdx.x == 0) dcount[gp] = mrun;
   const uint64_t wm = wave_max(uint64_t(mxlen));
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
@@ -800,11 +825,22 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
   if (gp == 0 && threadIdx.x < tabs.nt) {  // every table's counts (entries, main records, off[nbl])
     const uint32_t tj = threadIdx.x;
     uint64_t* counts = tabs.counts[tj];
+    uint64_t c0 = 0, c1 = 0;
     if (!reinterpret_cast<const uint32_t*>(counts + 3)[0]) {
       const uint32_t a = tj * tabs.P, b = (tj + 1) * tabs.P;
-      counts[0] = ps[b] - ps[a];
-      counts[1] = mbase[b] - mbase[a];
-      tabs.off[tj][nbl] = mbase[b] - mbase[a];
+      c0 = ps[b] - ps[a];
+      c1 = mbase[b] - mbase[a];
+      counts[0] = c0;
+      counts[1] = c1;
+      tabs.off[tj][nbl] = uint32_t(c1);
+    }
+    // the host's copy, written here instead of by a device-to-host copy behind the build (words 2
+    // and 3 were final when k_nagg ended); the host reads it after the build's event
+    if (uint64_t* h = tabs.hc[tj]) {
+      h[0] = c0;
+      h[1] = c1;
+      h[2] = counts[2];
+      h[3] = counts[3];
     }
   }
   if (reinterpret_cast<const uint32_t*>(tabs.counts[ti] + 3)[0]) return;  // fail flag
@@ -911,6 +947,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     tabs.sub[k] = tt[k]->sub.as<uint32_t>();
     tabs.main[k] = tt[k]->main.as<uint4>();
     tabs.counts[k] = tt[k]->counts.as<uint64_t>();
+    tabs.hc[k] = tt[k]->hc;  // (allocated by the caller: nested_host_counts)
   }
   const uint2* pairs = nullptr;
   const uint32_t* ps = nullptr;
@@ -1020,3 +1057,20 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
 }
 
 }  // namespace hj3d
+
+// Diagnostic (builds with HJ3D_NAGG_CLK only; else HJ3D_EUNSUPPORTED): the last k_nagg launch's
+// per-partition phase clocks, 8 words per partition (0 entry, 1 table cleared, 2 pass A done, 3 main
+// records written, 4 pass B done, 5 exit: 100 MHz wall clock; 7 the workgroup's dispatch index).
+extern "C" hj3d_status hj3d_diag_nagg_clk(uint64_t* host, uint32_t parts) {
+#if HJ3D_NAGG_CLK
+  if (!host || parts > hj3d::kClkParts) return HJ3D_EINVAL;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(hj3d::g_nagg_clk), uint64_t(parts) * hj3d::kClkPts * sizeof(uint64_t)) ==
+                 hipSuccess
+             ? HJ3D_OK
+             : HJ3D_EDEVICE;
+#else
+  (void)host;
+  (void)parts;
+  return HJ3D_EUNSUPPORTED;
+#endif
+}

@@ -1729,7 +1729,8 @@ hipError_t pk_probe_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
 }
 
 hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, ProbeParts* pp,
-                                 hipStream_t s, const SelArgs* sel, unsigned long long** npass, bool slots) {
+                                 hipStream_t s, const SelArgs* sel, unsigned long long** npass, bool slots,
+                                 const ZeroList* also) {
   hipError_t e;
   const uint32_t nbl = t->nb_local;
   if (W < 64) W = 64;
@@ -1774,7 +1775,13 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   uint32_t* seg = counts + nreg;  // nreg + 1 (transposed counts, scanned in place)
   unsigned long long* novf = ctx->scratch[kScrSortV].as<unsigned long long>();
   uint2* ovf = reinterpret_cast<uint2*>(ctx->scratch[kScrSortV].as<char>() + 64);
-  if ((e = hipMemsetAsync(novf, 0, 2 * sizeof(unsigned long long), s)) != hipSuccess) return e;  // novf, npass
+  if (also) {  // novf, npass and the caller's words in one launch
+    ZeroList z = *also;
+    if (!z.add(reinterpret_cast<uint64_t*>(novf), 2)) return hipErrorInvalidValue;
+    if ((e = zero_words(z, s)) != hipSuccess) return e;
+  } else if ((e = hipMemsetAsync(novf, 0, 2 * sizeof(unsigned long long), s)) != hipSuccess) {  // novf, npass
+    return e;
+  }
   if (npass) *npass = novf + 1;
   const RelView v = view_of(r);
   {

@@ -390,4 +390,17 @@ hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, 
   return hipGetLastError();
 }
 
+namespace {
+__global__ __launch_bounds__(256) void k_zero_words(ZeroList z) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    for (uint32_t i = threadIdx.x; i < z.n[k]; i += 256) z.p[k][i] = 0;
+}
+}  // namespace
+
+hipError_t zero_words(const ZeroList& z, hipStream_t s) {
+  hipLaunchKernelGGL(k_zero_words, dim3(1), dim3(256), 0, s, z);
+  return hipGetLastError();
+}
+
 }  // namespace hj3d

@@ -277,8 +277,10 @@ class Context:
         """Smallest probe side (tuples) that takes the radix-partitioned chaining kernels."""
         self.set_option(OPT_RADIX_MIN, int(n))
 
-    def timing(self, enable: bool = True):
-        self._check(lib().hj3d_ctx_timing(self.h, int(enable)), "timing")
+    def timing(self, mode: int = 1):
+        """0 / False: off; 1 / True: every timer; 2: only the kernel spans carried by a dispatch
+        (no marker packets between kernels; see hj3d_ctx_timing)."""
+        self._check(lib().hj3d_ctx_timing(self.h, int(mode)), "timing")
 
     def timer(self, phase: int):
         ms, cnt = C.c_double(), C.c_uint64()

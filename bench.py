@@ -97,6 +97,13 @@ def parse():
                    help="3D build: bucket-range partition + LDS aggregation (default), the same on the packed "
                         "partitioner's slices (HJ3D_OPT_NESTED_PK, the form of tables above 2048 partitions), LSD "
                         "key sort (HJ3D_OPT_NESTED_SORT), radix bucket CSR + per-bucket grouping (HJ3D_OPT_NESTED_RADIX)")
+    p.add_argument("--chain-build", default="auto", choices=["auto", "slices"],
+                   help="chaining build: the library's choice (default), or the two-level slice build (pk_build, "
+                        "HJ3D_OPT_PK_BUILD) wherever it applies (A/B)")
+    p.add_argument("--lib-timing", default="auto", choices=["auto", "0", "1", "2"],
+                   help="library timers (hj3d_ctx_timing): auto = 2 (dispatch-carried kernel spans only, no marker "
+                        "packets between kernels) where the line's per-kernel figures come from those spans (the "
+                        "packed probe), 1 (every timer) for the other B/D probe paths, 0 for C/E (no timer read)")
     p.add_argument("--log2R", type=int, default=22, help="config E: |R| = 2^log2R")
     a = p.parse_args()
     if a.workload is None:
@@ -343,7 +350,9 @@ def main():
     plan = args.plan
     emit = not args.no_emit
     ctx = hj3d.Context(local)
-    ctx.timing(True)
+    lib_timing = (2 if (args.probe_path == "packed" and args.plan == "Csr") else 1) if args.lib_timing == "auto" \
+        else int(args.lib_timing)
+    ctx.timing(lib_timing)
     if sharded and not args.rehearse:
         # the data path (counts, pairs, counter merges) on libhj3d's own RCCL communicator;
         # torch.distributed only hands over its id and times (barriers, max over ranks). World
@@ -365,6 +374,8 @@ def main():
         ctx.nested_pk(True)
     elif args.nested_build == "sort":
         ctx.nested_sort(True)
+    if args.chain_build == "slices":
+        ctx.pk_build(True)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
     fx_plan = (fx or {}).get("plans", {}).get(plan)
 
@@ -828,7 +839,7 @@ def main_single_config(args):
     torch.cuda.set_device(0)
     ctx = hj3d.Context(0)
     launches = []  # (build, probe) kernel launches of each step
-    ctx.timing(True)
+    ctx.timing(0 if args.lib_timing == "auto" else int(args.lib_timing))  # (no timer is read here)
     if args.nested_build == "radix":
         ctx.nested_radix(True)
     elif args.nested_build == "sort":

@@ -204,7 +204,10 @@ enum {
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
  * (phase ids below). hj3d_ctx_timer reads (synchronously) the summed milliseconds and the
- * number of recorded intervals since the last reset. */
+ * number of recorded intervals since the last reset. hj3d_ctx_timing(ctx, mode): 0 off; 1 every
+ * timer (whole-call phases are marker events between the kernels on the stream); 2 only the timers
+ * whose events travel with a kernel's dispatch (the packed probe's k_pk_part / k_pk_split /
+ * k_pk_probe), so timing puts no packet between the kernels. */
 enum {
   HJ3D_T_BUILD = 0,         /* hj3d_build, whole call */
   HJ3D_T_PROBE = 1,         /* hj3d_probe / hj3d_probe2, whole call */
@@ -218,7 +221,12 @@ enum {
 /* Kernel launches issued by this library so far, all contexts of the process (diagnostic: the bench
  * reports launches per step). */
 uint64_t hj3d_launch_count(void);
-hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int enable);
+/* Diagnostic: per-partition phase clocks of the last k_nagg launch (library built with
+ * -DHJ3D_NAGG_CLK=1; otherwise HJ3D_EUNSUPPORTED). 8 u64 words per partition: 0 entry, 1 table
+ * cleared, 2 pass A done, 3 main records written, 4 pass B done, 5 exit (100 MHz wall clock), 7 the
+ * workgroup's dispatch index. parts <= 16384. */
+hj3d_status hj3d_diag_nagg_clk(uint64_t* host, uint32_t parts);
+hj3d_status hj3d_ctx_timing(hj3d_ctx* ctx, int mode);
 hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t* count);
 hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx);
 

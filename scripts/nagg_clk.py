@@ -1,0 +1,82 @@
+#!/usr/bin/env python3
+"""Per-partition phase clocks of the nested aggregation kernel (k_nagg), from a library built with
+-DHJ3D_NAGG_CLK=1 (HJ3D_LIB=.../variants/clk/libhj3d.so): where a workgroup's time goes (table
+clear, pass A, main records, pass B) and how the partitions' start times spread over the launch.
+
+--workload E: config E's two tables in one build_many (1024 partitions of 3072 buckets);
+--workload C: one table over 1e8 Zipf-0.8 keys (config C's build). Prints one JSON object: the
+median / p90 microseconds of every phase over the partitions, the launch span, and the workgroups'
+start-time deciles."""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="E", choices=["C", "E"])
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import hj3d
+
+    dev = torch.device("cuda", 0)
+    ctx = hj3d.Context(0)
+    if a.workload == "E":
+        log2R = 22
+        nR = 1 << log2R
+        R, S, T = hj3d.exp4_relations_ref(log2R, 3, 4, 2, 2, device=dev)
+        nb = (nR >> 3) + (nR >> 2)
+        ts, tt = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb), hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+        ts.reserve(S.shape[0])
+        tt.reserve(T.shape[0])
+        relS, relT = hj3d.Rel(S, key_word=1), hj3d.Rel(T, key_word=1)
+
+        def build():
+            ctx.build_many([ts, tt], [relS, relT])
+            return ts
+    else:
+        R, S = hj3d.exp1_relations_ref(10_000_000, 100_000_000, True, 0.8, 0, device=dev)
+        relS = hj3d.Rel(S, key_word=1)
+        dv = ctx.num_distinct(relS, 10_000_000)
+        t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, dv)
+        t.reserve(S.shape[0])
+
+        def build():
+            ctx.build(t, relS)
+            return t
+    for _ in range(a.reps):
+        tb = build()
+    torch.cuda.synchronize()
+    path = tb.build_path()
+    parts = 16384
+    buf = (C.c_uint64 * (parts * 8))()
+    st = hj3d.lib().hj3d_diag_nagg_clk(buf, parts)
+    if st != 0:
+        raise SystemExit(f"hj3d_diag_nagg_clk: status {st} (library without HJ3D_NAGG_CLK?)")
+    x = np.frombuffer(buf, dtype=np.uint64).reshape(parts, 8).astype(np.int64)
+    x = x[x[:, 0] > 0]
+    t0 = x[:, 0].min()
+    us = lambda v: v * 0.01  # 100 MHz ticks -> microseconds
+    out = {"workload": a.workload, "path": path, "partitions": int(len(x)), "span_us": round(us(x[:, 5].max() - t0), 1)}
+    names = ["clear", "pass_A", "mains", "pass_B", "tail"]
+    for k, nm in enumerate(names):
+        d = us(x[:, k + 1] - x[:, k])
+        out[nm] = {"median": round(float(np.median(d)), 2), "p90": round(float(np.percentile(d, 90)), 2),
+                   "max": round(float(d.max()), 2)}
+    tot = us(x[:, 5] - x[:, 0])
+    out["workgroup_total"] = {"median": round(float(np.median(tot)), 2), "p90": round(float(np.percentile(tot, 90)), 2),
+                              "max": round(float(tot.max()), 2)}
+    starts = us(x[:, 0] - t0)
+    out["start_deciles_us"] = [round(float(np.percentile(starts, q)), 1) for q in range(0, 101, 10)]
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
