@@ -556,6 +556,24 @@ __device__ __forceinline__ void nested_bucket(uint32_t h, uint32_t pr, const MT*
   }
 }
 
+// The probe's small fills in one launch (they were three runtime fills / copies, and the count slots'
+// fill wrote all |probe| + 1 words: 0.8 GB, 106 us at config D): the partials' atomic row, base0 =
+// *src (n_probe before this call), and in the materialised unnest the count slots past the used
+// ones (seg_tot region slots + *novf overflow slots; every used slot is written by the probe kernels).
+__global__ __launch_bounds__(kBlock) void k_rn_prep(uint64_t* __restrict__ prow, uint64_t* __restrict__ base0,
+                                                    const uint64_t* __restrict__ src, uint64_t* __restrict__ cnt,
+                                                    const uint32_t* __restrict__ seg_tot,
+                                                    const unsigned long long* __restrict__ novf, uint64_t n) {
+  if (blockIdx.x == 0) {
+    if (threadIdx.x < kProbeFields) prow[threadIdx.x] = 0;
+    if (threadIdx.x == 0) *base0 = *src;
+  }
+  if (!cnt) return;
+  const uint64_t start = uint64_t(*seg_tot) + *novf;
+  for (uint64_t i = start + uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += uint64_t(gridDim.x) * kBlock)
+    cnt[i] = 0;
+}
+
 // PKD: the regions hold packed pairs {v, row} of pk_probe_slices (bucket in the slice v >> qbits, hash
 // pk.hash_of(v, p): no modulo per pair), else {hash, row}.
 template <int MODE, bool FITS, bool PKD>
@@ -871,13 +889,8 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
     return e;
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
-  if ((e = hipMemsetAsync(partials + uint64_t(nblocks) * kProbeFields, 0, kProbeFields * sizeof(uint64_t), s)) !=
-      hipSuccess)
-    return e;
   uint64_t* base0 = partials + uint64_t(nblocks + 1) * kProbeFields;
-  if ((e = hipMemcpyAsync(base0, sel ? static_cast<void*>(npass) : static_cast<void*>(res), sizeof(uint64_t),
-                          hipMemcpyDeviceToDevice, s)) != hipSuccess)
-    return e;
+  const uint64_t* base_src = sel ? reinterpret_cast<const uint64_t*>(npass) : res;
   const bool unnest = flags & HJ3D_PROBE_UNNEST;
   const bool emit = (flags & HJ3D_PROBE_EMIT) && out;
   const uint32_t* off = t->off.as<const uint32_t>();
@@ -895,7 +908,6 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
     cnt = ctx->scratch[kScrA].as<uint64_t>();
     zo = ctx->scratch[kScrC].as<uint32_t>() + 16;
     po = zo + r.n;
-    if ((e = hipMemsetAsync(cnt, 0, (r.n + 1) * sizeof(uint64_t), s)) != hipSuccess) return e;
   } else if (mode == kAggUN) {
     if ((e = ctx->scratch[kScrC].ensure(r.n * sizeof(Heavy) + 16)) != hipSuccess) return e;
     nhq = ctx->scratch[kScrC].as<uint64_t>();
@@ -904,6 +916,9 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   }
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   uint64_t* sink = ctx->ctl.as<uint64_t>() + 64;  // ctl words [64, 128): store sink
+  hipLaunchKernelGGL(k_rn_prep, dim3(cnt ? ctx->num_cus * 4 : 1), dim3(kBlock), 0, s,
+                     partials + uint64_t(nblocks) * kProbeFields, base0, base_src, cnt, pp.seg + uint64_t(pp.G) * pp.P,
+                     pp.novf, r.n);
   {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
     auto launch = [&](auto mode_c) {

@@ -49,7 +49,7 @@ def main():
         t.reserve(S.shape[0])
 
         def build():
-            ctx.build(t, relS)
+            t.build(relS)
             return t
     for _ in range(a.reps):
         tb = build()
