@@ -257,7 +257,7 @@ constexpr uint32_t kHeavyOut = 8192;
 #endif
 constexpr int kExpU = HJ3D_EXP_U;
 #ifndef HJ3D_EXP_XCD
-#define HJ3D_EXP_XCD 0  // k_expand_light: slot blocks XCD-ordered (1: A/B; config D probe 6.19 -> 6.15 ms, C 0.791 -> 0.795 ms: off)
+#define HJ3D_EXP_XCD 1  // k_expand_light: slot blocks XCD-ordered (0: A/B; config D Nrs probe 6.14 -> 5.64 ms, C unchanged)
 #endif
 #ifndef HJ3D_RN_XCD
 #define HJ3D_RN_XCD 1  // nested probe on slices wider than LDS: shared slices, XCD-ordered blocks (0: A/B)
