@@ -124,6 +124,7 @@ void hj3d_ctx_destroy(hj3d_ctx* ctx) {
   ctx->ctl.release();
   ctx->scan_status.release();
   ctx->part_cur.release();
+  ctx->gbar.release();
   for (auto ev : ctx->event_pool) (void)hipEventDestroy(ev);
   if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -171,6 +172,7 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_PK_COMPACT: ctx->pk_compact = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SYNC_BUILD: ctx->sync_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_2L: ctx->nested_2l = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_RP_UNFUSED: ctx->rp_unfused = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);

@@ -99,6 +99,7 @@ struct hj3d_ctx {
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
   bool nested_2l = false;         // HJ3D_OPT_NESTED_2L: the exact two-level partition + register aggregation
+  bool rp_unfused = false;        // HJ3D_OPT_RP_UNFUSED: small build partitions as histogram + scatter launches
   bool sync_build = false;        // HJ3D_OPT_SYNC_BUILD: nested builds resolved before hj3d_build returns
   bool pk_compact = false;        // HJ3D_OPT_PK_COMPACT: the packed probe's compact slice image where it applies
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
@@ -110,6 +111,10 @@ struct hj3d_ctx {
   // call k counts into set k & 1 and clears set (k + 1) & 1 for the next call; zeroed once here
   hj3d::DevBuf part_cur;
   uint32_t part_parity = 0;
+  // grid barrier of the fused partition (radix.hip k_rp_fused): word 0 a monotonic arrival counter
+  // (each launch waits for the running sum of the grids launched on it), word 1 the timeout flag
+  hj3d::DevBuf gbar;
+  uint64_t gbar_target = 0;
   hipError_t ensure_ctl() {
     if (ctl.p) return hipSuccess;
     hipError_t e = ctl.ensure(128 * sizeof(uint64_t));  // 8 control words; [64, 128): store sink

@@ -239,6 +239,163 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
   }
 }
 
+// One launch for both passes of small inputs (k_rp_hist + k_rp_scatter fused; implicit rows): every
+// workgroup takes at most TMAX tiles (g, g + G, ...), issues all their key loads at once, keeps the
+// hashes in registers while it counts them per partition and claims its runs on the partition
+// cursors, then waits at a grid barrier for every workgroup's claims (the partition sizes), scans
+// the sizes in LDS and scatters the tiles from its registers as k_rp_scatter does. R is read once,
+// not twice, and one launch boundary goes. The G workgroups are persistent (one per CU, the host
+// checks the occupancy); the barrier is a monotonic arrival counter (target = the running sum of
+// the grids launched on it), so it is never reset. A barrier that does not complete in ~0.2 s sets
+// the timeout word and lets the workgroup go on (results wrong, flagged) instead of hanging.
+// Phase 2 stages kFzGroup tiles per pass. One relation only (hj3d_build; hj3d_build_many's two
+// relations keep the two launches: at config E, 4 tiles per workgroup, the fused form measured
+// 66.9 against 19.4 + 43.8 us, at config B, 5 tiles, 87.0 against 26.4 + 67.5 us).
+#ifndef HJ3D_RP_FUSED
+#define HJ3D_RP_FUSED 1  // small implicit-row inputs: the fused one-launch partition (0: hist + scatter, A/B)
+#endif
+#ifndef HJ3D_RP_FZ_GROUP
+#define HJ3D_RP_FZ_GROUP 2  // fused partition: tiles staged per pass of phase 2 (1: one pass per tile, A/B)
+#endif
+constexpr int kFzRounds = 8;
+constexpr int kFzGroup = HJ3D_RP_FZ_GROUP;
+constexpr int kFzTMax = 6;  // tiles per workgroup held in registers (48 hashes per thread)
+__device__ __forceinline__ void grid_barrier(uint64_t* __restrict__ bar, uint64_t target) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > 20000000ull) {  // 0.2 s at 100 MHz
+        __hip_atomic_store(bar + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// 32-bit index math and branch-free 32-bit divisions (FastDiv32) keep the held hashes in registers:
+// the bucket is h - (h / NB) NB - lo, the partition bucket / W.
+struct FzGeom {
+  FastDiv32 dnb, dw;
+  uint32_t nb, lo, nbl, P;
+  __device__ __forceinline__ uint32_t bucket(uint32_t h) const { return h - dnb.div(h) * nb - lo; }
+};
+template <int TMAX>
+__global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, uint32_t ntiles, uint32_t* __restrict__ cur,
+                                                      uint32_t* __restrict__ cur_next, uint32_t* __restrict__ ps,
+                                                      uint2* __restrict__ out, uint64_t* __restrict__ bar,
+                                                      uint64_t target) {
+  constexpr int R = kFzRounds;
+  constexpr int kTile = kPBlock * R;
+  __shared__ uint2 stage[kTile * kFzGroup];
+  __shared__ uint32_t loc[kMaxParts];  // phase 1: counts; then the partition starts; per tile: local runs
+  __shared__ uint32_t gb[kMaxParts];   // this workgroup's write cursor per partition
+  uint32_t* wsum = reinterpret_cast<uint32_t*>(stage);
+  const uint32_t G = gridDim.x, P = fz.P, me = threadIdx.x;
+  uint32_t hv[TMAX][R];
+  for (uint32_t p = me; p < P; p += kPBlock) loc[p] = 0;
+  // tuples of tile t left to this thread's item j: i = tile base + j * 1024 + me < n (32-bit counts)
+  const auto nleft = [&](uint32_t tile) __attribute__((always_inline)) {
+    const RelView& r = rt.rel(tile);
+    const uint64_t b = rt.base(tile);
+    return tile < ntiles && r.n > b ? uint32_t(min(r.n - b, uint64_t(kTile))) : 0u;
+  };
+  // every key load of the workgroup's tiles in flight together
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    const uint32_t tile = blockIdx.x + uint32_t(t) * G;
+    const RelView& r = rt.rel(tile);
+    const uint32_t nl = nleft(tile);
+    const char* tb = r.base + rt.base(tile) * r.stride + r.key_off;
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      const uint32_t li = uint32_t(j) * kPBlock + me;
+      hv[t][j] = li < nl ? (HJ3D_NT_BUILD ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(tb + li * r.stride))
+                                          : *reinterpret_cast<const uint32_t*>(tb + li * r.stride))
+                         : 0u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < TMAX; ++t) {
+    const uint32_t tile = blockIdx.x + uint32_t(t) * G;
+    const uint32_t nl = nleft(tile), pofs = rt.pofs(tile);
+#pragma unroll
+    for (int j = 0; j < R; ++j) {
+      hv[t][j] = murmur32(hv[t][j]);
+      const uint32_t bl = fz.bucket(hv[t][j]);
+      if (uint32_t(j) * kPBlock + me < nl && bl < fz.nbl) atomicAdd(&loc[pofs + fz.dw.div(bl)], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t p = me; p < P; p += kPBlock) {
+    const uint32_t c = loc[p];
+    gb[p] = c ? atomicAdd(&cur[p], c) : 0u;  // this workgroup's run inside partition p
+  }
+  grid_barrier(bar, target);
+  // partition sizes are final: starts by an LDS scan (the cursors read at L2, past this CU's cache)
+  for (uint32_t p = me; p < P; p += kPBlock) loc[p] = __hip_atomic_load(cur + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const uint32_t total = lds_excl_scan<kPBlock>(loc, P, wsum);
+  for (uint32_t p = me; p < P; p += kPBlock) {
+    if (blockIdx.x == 0) ps[p] = loc[p];
+    gb[p] += loc[p];
+  }
+  if (blockIdx.x == 0) {
+    if (me == 0) ps[P] = total;
+    for (uint32_t p = me; p <= kMaxParts; p += kPBlock) cur_next[p] = 0;
+  }
+  // phase 2: kFzGroup tiles per staging pass (fewer barriers and scans than one pass per tile)
+#pragma unroll
+  for (int t0 = 0; t0 < TMAX; t0 += kFzGroup) {
+    if (blockIdx.x + uint32_t(t0) * G >= ntiles) break;
+    __syncthreads();  // (the starts / the previous pass's cursor advance are read below)
+    for (uint32_t p = me; p < P; p += kPBlock) loc[p] = 0;
+    uint32_t rk[kFzGroup][R];
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kFzGroup; ++u) {
+      const int t = t0 + u < TMAX ? t0 + u : TMAX - 1;
+      const uint32_t nl = t0 + u < TMAX ? nleft(blockIdx.x + uint32_t(t) * G) : 0u;
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        // (opaque to the compiler: phase 1's buckets are not kept live across the barrier for reuse
+        // here, which would hold a second register per item)
+        asm volatile("" : "+v"(hv[t][j]));
+        const uint32_t bl = fz.bucket(hv[t][j]);
+        rk[u][j] = kInvalid;
+        if (uint32_t(j) * kPBlock + me < nl && bl < fz.nbl) {
+          const uint32_t part = fz.dw.div(bl);
+          rk[u][j] = (part << 15) | atomicAdd(&loc[part], 1u);
+        }
+      }
+    }
+    __syncthreads();
+    const uint32_t m = lds_excl_scan<kPBlock>(loc, P, wsum);
+#pragma unroll
+    for (int u = 0; u < kFzGroup; ++u) {
+      const int t = t0 + u < TMAX ? t0 + u : TMAX - 1;
+      const uint32_t rb = uint32_t(rt.r0.row_base + rt.base(blockIdx.x + uint32_t(t) * G));  // implicit rows
+#pragma unroll
+      for (int j = 0; j < R; ++j) {
+        if (rk[u][j] == kInvalid) continue;
+        stage[loc[rk[u][j] >> 15] + (rk[u][j] & 0x7FFFu)] = make_uint2(hv[t][j], rb + uint32_t(j) * kPBlock + me);
+      }
+    }
+    __syncthreads();
+    for (uint32_t k = me; k < m; k += kPBlock) {
+      const uint2 e = stage[k];
+      const uint32_t p = fz.dw.div(fz.bucket(e.x));
+      nt_st(out + gb[p] + (k - loc[p]), e);
+    }
+    __syncthreads();
+    for (uint32_t p = me; p < P; p += kPBlock) gb[p] += (p + 1 < P ? loc[p + 1] : m) - loc[p];
+  }
+}
+
 // The same scatter with WHOLE-SEGMENT write-out into the exact runs k_rp_hist claimed.
 // k_rp_scatter writes each tile's run of a partition as it comes: at ~8 pairs per partition and
 // tile nearly every run starts and ends inside a 64/128-B segment, and the two halves of such a
@@ -1483,6 +1640,48 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   rt.P = pl.P;
   rt.tsz = tsz;
   const uint32_t lo = uint32_t(t->desc.bucket_lo);
+  // small implicit-row inputs: one fused launch (k_rp_fused) when every workgroup's tiles fit its
+  // registers and the G workgroups are co-resident (the grid barrier needs all of them at once)
+  const bool implicit = r.row_off == HJ3D_ROW_IMPLICIT && (!r1 || r1->row_off == HJ3D_ROW_IMPLICIT);
+  const uint32_t tpw = (ntiles + g - 1) / g;
+  if (HJ3D_RP_FUSED && !ctx->rp_unfused && !r1 && !ws && rounds == uint32_t(kFzRounds) && implicit && tpw <= uint32_t(kFzTMax) &&
+      t->desc.num_buckets >= 2 && t->desc.num_buckets < (1ull << 32) && pl.W >= 2) {
+    const void* kf = tpw <= 2   ? reinterpret_cast<const void*>(&k_rp_fused<2>)
+                     : tpw == 3 ? reinterpret_cast<const void*>(&k_rp_fused<3>)
+                     : tpw == 4 ? reinterpret_cast<const void*>(&k_rp_fused<4>)
+                     : tpw == 5 ? reinterpret_cast<const void*>(&k_rp_fused<5>)
+                                : reinterpret_cast<const void*>(&k_rp_fused<6>);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kf, kPBlock, 0) == hipSuccess &&
+        uint64_t(per_cu) * cus >= g) {
+      if (!ctx->gbar.p) {
+        if ((e = ctx->gbar.ensure(2 * sizeof(uint64_t))) != hipSuccess) return e;
+        if ((e = hipMemsetAsync(ctx->gbar.p, 0, ctx->gbar.bytes, s)) != hipSuccess) return e;
+      }
+      ctx->gbar_target += g;
+      PhaseTimer tm(ctx, t_scatter);
+      uint64_t* bar = ctx->gbar.as<uint64_t>();
+      FzGeom fz;
+      fz.dnb = FastDiv32::make(uint32_t(t->desc.num_buckets));
+      fz.dw = FastDiv32::make(pl.W);
+      fz.nb = uint32_t(t->desc.num_buckets);
+      fz.lo = lo;
+      fz.nbl = t->nb_local;
+      fz.P = PT;
+#define HJ3D_FZ_LAUNCH(T)                                                                                             \
+  hipLaunchKernelGGL(k_rp_fused<T>, dim3(g), dim3(kPBlock), 0, s, rt, fz, ntiles, cur, cur_next, ps, out, bar, \
+                     ctx->gbar_target)
+      switch (tpw <= 2 ? 2 : tpw) {
+        case 2: HJ3D_FZ_LAUNCH(2); break;
+        case 3: HJ3D_FZ_LAUNCH(3); break;
+        case 4: HJ3D_FZ_LAUNCH(4); break;
+        case 5: HJ3D_FZ_LAUNCH(5); break;
+        default: HJ3D_FZ_LAUNCH(6); break;
+      }
+#undef HJ3D_FZ_LAUNCH
+      return hipGetLastError();
+    }
+  }
   {
     PhaseTimer tm(ctx, t_hist);
     if (rounds == kPRounds)

@@ -28,6 +28,7 @@ T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
 OPT_PROBE_ITEMS = 7
 OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_PK_COMPACT, OPT_SYNC_BUILD, OPT_NESTED_2L = 8, 9, 10, 11, 12, 13, 14
+OPT_RP_UNFUSED = 15
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -406,6 +407,11 @@ class Context:
         """Nested builds too coarse for the register aggregation take the exact two-level partition
         (HJ3D_OPT_NESTED_2L; off by default, tests and A/B)."""
         self.set_option(OPT_NESTED_2L, int(on))
+
+    def rp_unfused(self, on: bool = True):
+        """Small build partitions as two launches (histogram, scatter) instead of the fused
+        one-launch partition (HJ3D_OPT_RP_UNFUSED; tests and A/B)."""
+        self.set_option(OPT_RP_UNFUSED, int(on))
 
     def sync_build(self, on: bool = True):
         """Nested builds finished inside hj3d_build (HJ3D_OPT_SYNC_BUILD): the build relation may

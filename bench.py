@@ -100,6 +100,9 @@ def parse():
     p.add_argument("--chain-build", default="auto", choices=["auto", "slices"],
                    help="chaining build: the library's choice (default), or the two-level slice build (pk_build, "
                         "HJ3D_OPT_PK_BUILD) wherever it applies (A/B)")
+    p.add_argument("--rp-unfused", action="store_true",
+                   help="small build partitions as two launches (histogram, scatter) instead of the fused "
+                        "one-launch partition (HJ3D_OPT_RP_UNFUSED, A/B)")
     p.add_argument("--lib-timing", default="auto", choices=["auto", "0", "1", "2"],
                    help="library timers (hj3d_ctx_timing): auto = 2 (dispatch-carried kernel spans only, no marker "
                         "packets between kernels) where the line's per-kernel figures come from those spans (the "
@@ -350,9 +353,14 @@ def main():
     plan = args.plan
     emit = not args.no_emit
     ctx = hj3d.Context(local)
+    # per-kernel HIP events: dispatch-carried spans (2) for the packed probe, every timer (1) otherwise.
+    # With --lib-timing auto the K timed steps run uninstrumented (0) and K further steps carry the
+    # kernel events (the line's per-kernel figures): an event riding on a dispatch costs ~10 us of
+    # idle GPU before the next kernel (profiles/r05x_*), ~2 % of config B's probe phase.
     lib_timing = (2 if (args.probe_path == "packed" and args.plan == "Csr") else 1) if args.lib_timing == "auto" \
         else int(args.lib_timing)
-    ctx.timing(lib_timing)
+    timed_timing = 0 if args.lib_timing == "auto" else lib_timing
+    ctx.timing(timed_timing)
     if sharded and not args.rehearse:
         # the data path (counts, pairs, counter merges) on libhj3d's own RCCL communicator;
         # torch.distributed only hands over its id and times (barriers, max over ranks). World
@@ -376,6 +384,8 @@ def main():
         ctx.nested_sort(True)
     if args.chain_build == "slices":
         ctx.pk_build(True)
+    if args.rp_unfused:
+        ctx.rp_unfused(True)
     fx = fixture(f"exp1_R{nR_tot}_S{nS_tot}_uni") if (args.inputs == "reference" and args.b == 1) else None
     fx_plan = (fx or {}).get("plans", {}).get(plan)
 
@@ -539,7 +549,24 @@ def main():
 
     build_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     probe_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    # per-kernel averages over the timed steps (HIP events on the engine's stream)
+    instrumented = None
+    if timed_timing != lib_timing:
+        # K kernel-timing steps: the same step with the per-kernel events (HIP events on the engine's
+        # stream, riding on the timed kernels' dispatches)
+        ctx.timing(lib_timing)
+        ctx.timer_reset()
+        kevs = [_events(torch, 3) for _ in range(args.steps)]
+        barrier()
+        torch.cuda.synchronize()
+        for e in kevs:
+            step(e)
+        torch.cuda.synchronize()
+        barrier()
+        instrumented = {"steps": args.steps, "lib_timing": lib_timing,
+                        "build_ms": sum(e[0].elapsed_time(e[1]) for e in kevs) / args.steps,
+                        "probe_ms": sum(e[1].elapsed_time(e[2]) for e in kevs) / args.steps}
+    # per-kernel averages (HIP events on the engine's stream): over the timed steps, or over the
+    # kernel-timing steps when the timed steps ran uninstrumented
     kern_avg = {}
     kprobe = "k_pk_probe" if packed else ("k_rp_probe_seg" if unique else "k_rn_probe_seg")
     kpart = "k_pk_part" if packed else "k_rp_part1"
@@ -547,6 +574,7 @@ def main():
             ((("k_pk_split", hj3d.T_HIST),) if packed else ()):
         ms, cnt = ctx.timer(ph)
         kern_avg[name] = ms / cnt if cnt else None
+    ctx.timing(timed_timing)
     # verification step (outside the timed region): the same step once more with the
     # order-independent output checksums folded in
     state["ck"] = True
@@ -731,6 +759,10 @@ def main():
             "frac": kernels[dom]["frac"], "traffic": traffic,
             "kernel": dom, "kernel_avg_ms": kernels[dom]["avg_ms"], "alg_bytes_per_launch": kernels[dom]["alg_bytes"],
             "kernels": kernels,
+            "kernel_timing": ("HIP events riding on the kernels' dispatches over K kernel-timing steps after the "
+                              "(uninstrumented) timed steps" if instrumented else
+                              "HIP events on the engine's stream over the timed steps"),
+            "instrumented_steps": instrumented,
             "probe_phase": {"ms": probe_ms, "alg_bytes": phase_alg,
                             "achieved_GBs": phase_alg / (probe_ms * 1e-3) / 1e9,
                             "frac": phase_alg / (probe_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
@@ -840,6 +872,8 @@ def main_single_config(args):
     ctx = hj3d.Context(0)
     launches = []  # (build, probe) kernel launches of each step
     ctx.timing(0 if args.lib_timing == "auto" else int(args.lib_timing))  # (no timer is read here)
+    if args.rp_unfused:
+        ctx.rp_unfused(True)
     if args.nested_build == "radix":
         ctx.nested_radix(True)
     elif args.nested_build == "sort":

@@ -199,7 +199,11 @@ enum {
    * the register aggregation takes the exact two-level partition into narrow partitions (up to 8192,
    * skew-safe) and aggregates them in registers. Measured slower at config C (2.93 against 2.25 ms),
    * so off by default; kept for A/B measurements and its parity test. */
-  HJ3D_OPT_NESTED_2L = 14
+  HJ3D_OPT_NESTED_2L = 14,
+  /* HJ3D_OPT_RP_UNFUSED (0/1, default 0): small implicit-row build partitions run as two launches
+   * (histogram, then scatter) instead of the fused one-launch partition with its grid barrier
+   * (A/B measurements and the parity test of both forms). */
+  HJ3D_OPT_RP_UNFUSED = 15
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase

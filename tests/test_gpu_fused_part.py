@@ -1,0 +1,88 @@
+"""GPU parity of the fused one-launch build partition (radix.hip k_rp_fused: histogram held in
+registers, grid barrier, scatter) against the oracle, and against the two-launch form
+(HJ3D_OPT_RP_UNFUSED) it replaces. Sizes cover every register-tile count the kernel is instantiated
+for (1 to 6 tiles of 8192 tuples per workgroup), ragged last tiles and Zipf-skewed keys; the
+chaining table's statistics, the unique and non-unique probes' counters and output checksums must
+equal the oracle's (HtChaining1::insert order, ht_chaining.hh:181-196)."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_sum", "cc0_cnt",
+             "cc1_min", "cc1_max", "cc1_sum", "cc1_cnt")
+
+
+def dev(a):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).cuda()
+
+
+def _check(ctx, B, P, nb, unfused):
+    import hj3d
+    lib = hj3d.lib()
+    ctx.rp_unfused(unfused)
+    try:
+        for unique in (True, False):
+            e = O.chain_plan(B, 0, P, 1, nb, unique)
+            t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, nb)
+            l0 = lib.hj3d_launch_count()
+            t.build(hj3d.Rel(dev(B), 0))
+            launches = lib.hj3d_launch_count() - l0
+            r = ctx.probe(t, hj3d.Rel(dev(P), 1), unique=unique)
+            assert (r.n_out, r.n_cmps) == (e.c_probe, e.c_cmp), (unique, unfused)
+            assert {"n": r.n_out, "sum_a": r.sum_a, "sum_b": r.sum_b, "sum_c": 0, "sum_h": r.sum_h,
+                    "xor_h": r.xor_h} == e.out, (unique, unfused)
+            st = t.stats()
+            assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, (unique, unfused)
+            t.close()
+    finally:
+        ctx.rp_unfused(False)
+    return launches
+
+
+@pytest.mark.parametrize("n", [1_000_003, 2_500_017, 6_000_005, 9_437_184, 12_500_000])
+@pytest.mark.parametrize("unfused", [False, True], ids=["fused", "two_launch"])
+def test_fused_partition_chaining_build(ctx, n, unfused):
+    """Key/FK tables at fill 1 (the headline's shape) from 1 to 6 tiles per workgroup; the fused
+    form builds in two launches (partition + build), the two-launch form in three."""
+    rng = np.random.default_rng(n % 1000)
+    Bk = rng.permutation(n).astype(np.uint32)
+    Pk = rng.integers(0, n, n // 2).astype(np.uint32)
+    B = O.tuples3(Bk, np.zeros(n, np.uint32))
+    P = O.tuples3(np.arange(len(Pk), dtype=np.uint32), Pk)
+    launches = _check(ctx, B, P, n, unfused)
+    assert launches == (3 if unfused else 2), launches
+
+
+@pytest.mark.parametrize("theta", [0.6, 1.0])
+def test_fused_partition_skewed_keys(ctx, theta):
+    """Zipf build keys: hot buckets make partitions of very different sizes (one exceeds the staged
+    build's registers and takes its HBM fallback); the fused partition's runs stay exact."""
+    rng = np.random.default_rng(int(theta * 100))
+    n = 4_000_000
+    Bk = (np.minimum(rng.zipf(1.0 + theta, n), 5_000_000) - 1).astype(np.uint32)
+    Pk = rng.integers(0, 4_000_000, n).astype(np.uint32)
+    B = O.tuples3(Bk, np.zeros(n, np.uint32))
+    P = O.tuples3(np.arange(n, dtype=np.uint32), Pk)
+    assert _check(ctx, B, P, n, False) == 2
+
+
+def test_fused_partition_repeated_builds(ctx):
+    """The grid barrier's arrival counter is monotonic across launches (never reset): many builds
+    on one context, alternating table sizes (grids of 122 and 256 workgroups), stay exact."""
+    import hj3d
+    rng = np.random.default_rng(5)
+    for k in range(12):
+        n = 1_000_000 if k % 2 else 3_000_000
+        Bk = rng.permutation(n).astype(np.uint32)
+        B = O.tuples3(Bk, np.zeros(n, np.uint32))
+        P = O.tuples3(np.arange(n // 4, dtype=np.uint32), rng.integers(0, n, n // 4).astype(np.uint32))
+        e = O.chain_plan(B, 0, P, 1, n, True)
+        t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, n)
+        t.build(hj3d.Rel(dev(B), 0))
+        r = ctx.probe(t, hj3d.Rel(dev(P), 1), unique=True)
+        assert (r.n_out, r.n_cmps, r.sum_h, r.xor_h) == (e.c_probe, e.c_cmp, e.out["sum_h"], e.out["xor_h"]), k
+        t.close()
