@@ -1012,7 +1012,8 @@ def main_single_config(args):
     # scripts/pmc_summary.py --workload C|E): bytes per step of each phase's kernels
     pm = _load_pmc(args.pmc_json, args.workload)
     if pm:
-        ph_build = ("k_rp_hist", "k_rp_scatter", "k_nagg", "k_nagg_mains", "k_rs_scatter", "k_rs_hist")
+        ph_build = ("k_rp_hist", "k_rp_scatter", "k_rp_wscatter", "k_rp_fused", "k_nagg", "k_nagg_mains", "k_rs_scatter",
+                    "k_rs_hist")
         ph_probe = ("k_rp_part1", "k_rn_probe_seg", "k_expand_light", "k_expand_heavy_flat", "k_ndu_seg", "k_ndu",
                     "k_ndu_heavy")
         tr = {k: d.get("traffic_bytes_per_launch") for k, d in pm["kernels"].items()

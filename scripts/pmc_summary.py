@@ -34,7 +34,7 @@ import statistics
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # longer names first: a name is matched as a substring of the mangled kernel name
 KERNELS = ("k_pk_probe", "k_pk_part", "k_pk_build", "k_rp_probe_seg", "k_rp_part1", "k_probe_ovf", "k_rp_probe",
-           "k_rp_scatter", "k_rp_hist", "k_rp_build3", "k_rp_build2", "k_rp_build", "k_sort_small_buckets",
+           "k_rp_scatter", "k_rp_hist", "k_rp_fused", "k_rp_wscatter", "k_rp_build3", "k_rp_build2", "k_rp_build", "k_sort_small_buckets",
            "k_scan_tiles",
            # nested (config C) and experiment-4 (config E) kernels
            "k_nagg_mains", "k_nagg_order", "k_nagg_rebase", "k_nagg_counts", "k_nagg_ps_shift", "k_nagg_pk_ovf",
