@@ -70,6 +70,8 @@ bool dense_output(const hj3d_table* t, uint32_t flags) {
 // kernels drop pairs past out_cap. Mark n_out before the call and compare after it, on the stream.
 hipError_t out_mark(hj3d_ctx* ctx, const hj3d_table* t, uint32_t flags) {
   if (!(flags & HJ3D_PROBE_EMIT) || dense_output(t, flags)) return hipSuccess;
+  // a fresh strand's result slot was just zeroed: its mark (word 14) equals n_out (word 2) = 0
+  if (!(flags & HJ3D_PROBE_ACCUMULATE)) return hipSuccess;
   uint64_t* res = ctx->res.as<uint64_t>();
   return hipMemcpyAsync(res + kResOutMark, res + 2, sizeof(uint64_t), hipMemcpyDeviceToDevice, ctx->stream);
 }
@@ -575,14 +577,23 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
       return from_hip(ctx, e, "hj3d_probe");
     }
   }
-  hipError_t e = acc ? hipSuccess : hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+  // the partitioned nested probe zeroes a fresh strand's result slot in the launch that clears its
+  // partitioner's counters (no runtime fill); the other paths with a fill here
+  const bool nested_radix = t->desc.kind == HJ3D_NESTED && radix_nested_applicable(ctx, t, probe->n);
+  ZeroList zres;
+  zres.add(res, kResFields);
+  hipError_t e = acc || nested_radix ? hipSuccess : hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
   if (e == hipSuccess) e = out_mark(ctx, t, flags);
   if (e == hipSuccess) {
     e = hipErrorNotSupported;
     if (t->desc.kind == HJ3D_CHAIN && radix_probe_applicable(ctx, t, probe->n))
       e = radix_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);  // times its own kernels
-    else if (radix_nested_applicable(ctx, t, probe->n))
-      e = radix_nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream);
+    else if (nested_radix)
+      e = radix_nested_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream, nullptr, acc ? nullptr : &zres);
+    if (e == hipErrorNotSupported && nested_radix && !acc) {  // (nothing was launched: the slot is still to clear)
+      const hipError_t z = hipMemsetAsync(res, 0, kResFields * sizeof(uint64_t), ctx->stream);
+      if (z != hipSuccess) e = z;
+    }
     if (e == hipErrorNotSupported) {
       PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
       e = (t->desc.kind == HJ3D_CHAIN) ? chain_probe(ctx, t, *probe, flags, out_dev, out_cap, res, ctx->stream)

@@ -399,8 +399,11 @@ hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, u
                         uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // partitioned nested probe (every mode of nested_probe); needs t->n_mains
 bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n_probe);
+// also (optional): words to zero before the strand (a fresh result slot), in the partitioner's
+// counter-clearing launch; on hipErrorNotSupported nothing was launched
 hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                              uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr);
+                              uint64_t out_cap, uint64_t* res_dev, hipStream_t s, const SelArgs* sel = nullptr,
+                              const ZeroList* also = nullptr);
 // exp4.hip
 hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel& r, uint32_t flags,
                   void* out, uint64_t out_cap, uint64_t* res_dev, hipStream_t s);

@@ -563,10 +563,12 @@ __device__ __forceinline__ void nested_bucket(uint32_t h, uint32_t pr, const MT*
 __global__ __launch_bounds__(kBlock) void k_rn_prep(uint64_t* __restrict__ prow, uint64_t* __restrict__ base0,
                                                     const uint64_t* __restrict__ src, uint64_t* __restrict__ cnt,
                                                     const uint32_t* __restrict__ seg_tot,
-                                                    const unsigned long long* __restrict__ novf, uint64_t n) {
+                                                    const unsigned long long* __restrict__ novf, uint64_t n,
+                                                    uint32_t* __restrict__ zero32) {
   if (blockIdx.x == 0) {
     if (threadIdx.x < kProbeFields) prow[threadIdx.x] = 0;
     if (threadIdx.x == 0) *base0 = *src;
+    if (threadIdx.x == 64 && zero32) *zero32 = 0;  // the expansion's heavy-slot counter
   }
   if (!cnt) return;
   const uint64_t start = uint64_t(*seg_tot) + *novf;
@@ -851,7 +853,7 @@ bool radix_nested_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t 
 }
 
 hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
-                              uint64_t out_cap, uint64_t* res, hipStream_t s, const SelArgs* sel) {
+                              uint64_t out_cap, uint64_t* res, hipStream_t s, const SelArgs* sel, const ZeroList* also) {
   hipError_t e;
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbl = t->nb_local;
   // slice width: 80% of the LDS budget at the mean number of main records per bucket (a
@@ -875,9 +877,11 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
       e = pk_probe_slices(ctx, t, r, W1 >= 64 ? W1 : w_fit, &pp, &pk, s);
       if (e == hipSuccess) pkd = true;
       else if (e != hipErrorNotSupported) return e;
+      if (pkd && also && (e = zero_words(*also, s)) != hipSuccess) return e;
     }
   }
-  if (!pkd && (e = radix_partition_probe(ctx, t, r, w_fit, &pp, s, sel, sel ? &npass : nullptr)) != hipSuccess) return e;
+  if (!pkd && (e = radix_partition_probe(ctx, t, r, w_fit, &pp, s, sel, sel ? &npass : nullptr, true, also)) != hipSuccess)
+    return e;
   // slices wider than LDS (more than the partitioner's 2048 slices at the fitting width: config D's
   // 1e8-bucket table) are probed through the cache. Then kHbmSplits workgroups share each slice and
   // the blocks are ordered so that an XCD's workgroups take consecutive (slice, share) pairs: the
@@ -916,9 +920,16 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   }
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   uint64_t* sink = ctx->ctl.as<uint64_t>() + 64;  // ctl words [64, 128): store sink
+  // the materialised expansion's heavy-slot counter (scratch kScrSortK, word 0) is zeroed by the prep
+  // launch (no runtime fill behind the probe)
+  uint32_t* nheavy = nullptr;
+  if (mode == kCountUN) {
+    if ((e = ctx->scratch[kScrSortK].ensure((r.n + 64) * sizeof(uint32_t))) != hipSuccess) return e;
+    nheavy = ctx->scratch[kScrSortK].as<uint32_t>();
+  }
   hipLaunchKernelGGL(k_rn_prep, dim3(cnt ? ctx->num_cus * 4 : 1), dim3(kBlock), 0, s,
                      partials + uint64_t(nblocks) * kProbeFields, base0, base_src, cnt, pp.seg + uint64_t(pp.G) * pp.P,
-                     pp.novf, r.n);
+                     pp.novf, r.n, nheavy);
   {
     PhaseTimer tk(ctx, HJ3D_T_PROBE_KERNEL);
     auto launch = [&](auto mode_c) {
@@ -958,14 +969,11 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   // expansion over the slots: regions' then overflow pairs' (unused slots have count 0)
   if ((e = exclusive_scan_u64(ctx, cnt, cnt, r.n, s)) != hipSuccess) return e;
   const uint32_t nblk = uint32_t((r.n + kBlock - 1) / kBlock);
-  // heavy slots: at most one per slot (many probe tuples may match one hot key)
-  if ((e = ctx->scratch[kScrSortK].ensure((r.n + 64) * sizeof(uint32_t))) != hipSuccess) return e;
+  // heavy slots: at most one per slot (many probe tuples may match one hot key); nheavy zeroed above
   if ((e = ctx->scratch[kScrD].ensure((r.n + 2) * sizeof(uint64_t))) != hipSuccess) return e;  // hoff
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblk) * kProbeFields * sizeof(uint64_t))) != hipSuccess) return e;
-  uint32_t* nheavy = ctx->scratch[kScrSortK].as<uint32_t>();
   uint32_t* heavy = nheavy + 64;
   partials = ctx->scratch[kScrPartial].as<uint64_t>();
-  if ((e = hipMemsetAsync(nheavy, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
   SlotSrc src{view_of(r), nullptr, mains, zo, po};
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   if ((e = expand(ctx, src, true, ck, r.n, cnt, sub, o, out_cap, heavy, nheavy, partials, res, s)) != hipSuccess)
