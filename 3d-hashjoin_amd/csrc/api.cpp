@@ -204,6 +204,30 @@ hj3d_status hj3d_ctx_timer(hj3d_ctx* ctx, int phase, double* ms_total, uint64_t*
   return HJ3D_OK;
 }
 
+hj3d_status hj3d_tevent_create(hj3d_ctx* ctx, void** ev) {
+  if (!ctx || !ev) return HJ3D_EINVAL;
+  hipEvent_t e = nullptr;
+  const hipError_t r = hipEventCreateWithFlags(&e, HJ3D_TIMER_EVENT_FLAGS);
+  *ev = r == hipSuccess ? e : nullptr;
+  return from_hip(ctx, r, "hj3d_tevent_create");
+}
+
+hj3d_status hj3d_tevent_record(hj3d_ctx* ctx, void* ev) {
+  if (!ctx || !ev) return HJ3D_EINVAL;
+  return from_hip(ctx, hipEventRecord(static_cast<hipEvent_t>(ev), ctx->stream), "hj3d_tevent_record");
+}
+
+hj3d_status hj3d_tevent_elapsed(void* a, void* b, float* ms) {
+  if (!a || !b || !ms) return HJ3D_EINVAL;
+  if (hipEventSynchronize(static_cast<hipEvent_t>(b)) != hipSuccess) return HJ3D_EDEVICE;
+  return hipEventElapsedTime(ms, static_cast<hipEvent_t>(a), static_cast<hipEvent_t>(b)) == hipSuccess ? HJ3D_OK
+                                                                                                      : HJ3D_EDEVICE;
+}
+
+void hj3d_tevent_destroy(void* ev) {
+  if (ev) (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
+}
+
 hj3d_status hj3d_ctx_timer_reset(hj3d_ctx* ctx) {
   if (!ctx) return HJ3D_EINVAL;
   (void)hipStreamSynchronize(ctx->stream);

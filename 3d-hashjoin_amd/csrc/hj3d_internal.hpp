@@ -456,12 +456,17 @@ enum ScratchSlot {
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
                            uint64_t set0 = ~0ull, const uint64_t* base0 = nullptr);
 
+#ifndef HJ3D_TIMER_EVENT_FLAGS
+#define HJ3D_TIMER_EVENT_FLAGS hipEventDisableSystemFence  // timer events (hipEventDefault: A/B)
+#endif
 // Event spans on the context stream when timing is enabled (hj3d_ctx_timer): a PhaseTimer
 // brackets whatever is enqueued during its lifetime.
 inline hipEvent_t take_event(hj3d_ctx* ctx) {
   if (ctx->pool_used == ctx->event_pool.size()) {
     hipEvent_t ev;
-    if (hipEventCreate(&ev) != hipSuccess) return nullptr;
+    // timing only: no system-scope fence when the event is recorded (a fence writes the L2 back
+    // and leaves the GPU idle ~10 us between the kernels around the event)
+    if (hipEventCreateWithFlags(&ev, HJ3D_TIMER_EVENT_FLAGS) != hipSuccess) return nullptr;
     ctx->event_pool.push_back(ev);
   }
   return ctx->event_pool[ctx->pool_used++];

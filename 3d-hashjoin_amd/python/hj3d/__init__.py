@@ -106,6 +106,10 @@ def lib():
         "hj3d_ctx_set_option": (st, [p, i32, C.c_int64]),
         "hj3d_ctx_timer": (st, [p, i32, C.POINTER(C.c_double), C.POINTER(u64)]),
         "hj3d_ctx_timer_reset": (st, [p]),
+        "hj3d_tevent_create": (st, [p, C.POINTER(p)]),
+        "hj3d_tevent_record": (st, [p, p]),
+        "hj3d_tevent_elapsed": (st, [p, p, C.POINTER(C.c_float)]),
+        "hj3d_tevent_destroy": (None, [p]),
         "hj3d_dev_alloc": (st, [p, u64, C.POINTER(p)]),
         "hj3d_dev_free": (st, [p, p]),
         "hj3d_upload": (st, [p, p, p, u64]),
@@ -221,6 +225,34 @@ class ProbeResult:
     sum_h: int
     xor_h: int
     overflow: bool = False
+
+
+class TimingEvent:
+    """A timing event on a context's stream (hj3d_tevent_*: a HIP event without the system-scope
+    fence, so recording it does not stall the kernels around it). Same use as
+    torch.cuda.Event(enable_timing=True): record(), then a.elapsed_time(b) in ms."""
+
+    def __init__(self, ctx: "Context"):
+        self.ctx = ctx
+        h = C.c_void_p()
+        ctx._check(lib().hj3d_tevent_create(ctx.h, C.byref(h)), "hj3d_tevent_create")
+        self.h = h
+
+    def record(self):
+        self.ctx._check(lib().hj3d_tevent_record(self.ctx.h, self.h), "hj3d_tevent_record")
+
+    def elapsed_time(self, other: "TimingEvent") -> float:
+        ms = C.c_float()
+        st = lib().hj3d_tevent_elapsed(self.h, other.h, C.byref(ms))
+        if st != 0:
+            raise Hj3dError(st, "hj3d_tevent_elapsed")
+        return float(ms.value)
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _lib is not None:
+            _lib.hj3d_tevent_destroy(h)
+            self.h = None
 
 
 class Context:

@@ -100,6 +100,9 @@ def parse():
     p.add_argument("--chain-build", default="auto", choices=["auto", "slices"],
                    help="chaining build: the library's choice (default), or the two-level slice build (pk_build, "
                         "HJ3D_OPT_PK_BUILD) wherever it applies (A/B)")
+    p.add_argument("--torch-events", action="store_true",
+                   help="phase boundaries timed with torch.cuda.Event (default hipEvents; A/B) instead of the "
+                        "library's fence-free timing events")
     p.add_argument("--rp-unfused", action="store_true",
                    help="small build partitions as two launches (histogram, scatter) instead of the fused "
                         "one-launch partition (HJ3D_OPT_RP_UNFUSED, A/B)")
@@ -298,7 +301,16 @@ def _with_copy_peak(roof, cp, keys=("achieved",)):
             roof[f"{k}_frac_of_copy_peak" if k != "achieved" else "frac_of_copy_peak"] = roof[k] / cp["copy_peak_GBs"]
 
 
+_EVENT_CTX = None  # the workload's hj3d context: phase events on its stream (hj3d.TimingEvent)
+
+
 def _events(torch, n):
+    """Phase-boundary events of one step. With a context: HIP events on the engine's stream created
+    without the system-scope fence (hj3d_tevent_*): a default event writes the L2 back when it is
+    recorded and leaves the GPU idle ~10 us at each phase boundary."""
+    if _EVENT_CTX is not None:
+        import hj3d
+        return [hj3d.TimingEvent(_EVENT_CTX) for _ in range(n)]
     return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
 
@@ -353,6 +365,8 @@ def main():
     plan = args.plan
     emit = not args.no_emit
     ctx = hj3d.Context(local)
+    global _EVENT_CTX
+    _EVENT_CTX = None if args.torch_events else ctx
     # per-kernel HIP events: dispatch-carried spans (2) for the packed probe, every timer (1) otherwise.
     # With --lib-timing auto the K timed steps run uninstrumented (0) and K further steps carry the
     # kernel events (the line's per-kernel figures): an event riding on a dispatch costs ~10 us of
@@ -870,6 +884,8 @@ def main_single_config(args):
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(0)
     ctx = hj3d.Context(0)
+    global _EVENT_CTX
+    _EVENT_CTX = None if args.torch_events else ctx
     launches = []  # (build, probe) kernel launches of each step
     ctx.timing(0 if args.lib_timing == "auto" else int(args.lib_timing))  # (no timer is read here)
     if args.rp_unfused:

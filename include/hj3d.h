@@ -206,6 +206,14 @@ enum {
   HJ3D_OPT_RP_UNFUSED = 15
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
+/* Timing events for a host's own phase timers (the bench's build / probe boundaries): HIP events
+ * created without the system-scope fence (hipEventDisableSystemFence), recorded on the context
+ * stream. A default event writes the L2 back when it is recorded, which leaves the GPU idle
+ * ~10 us between the kernels around it. hj3d_tevent_elapsed waits for b, then gives b - a in ms. */
+hj3d_status hj3d_tevent_create(hj3d_ctx* ctx, void** ev);
+hj3d_status hj3d_tevent_record(hj3d_ctx* ctx, void* ev);
+hj3d_status hj3d_tevent_elapsed(void* a, void* b, float* ms);
+void hj3d_tevent_destroy(void* ev);
 /* Kernel-phase timers: HIP events recorded on the context stream around every phase
  * (phase ids below). hj3d_ctx_timer reads (synchronously) the summed milliseconds and the
  * number of recorded intervals since the last reset. hj3d_ctx_timing(ctx, mode): 0 off; 1 every
