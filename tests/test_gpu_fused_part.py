@@ -86,3 +86,33 @@ def test_fused_partition_repeated_builds(ctx):
         r = ctx.probe(t, hj3d.Rel(dev(P), 1), unique=True)
         assert (r.n_out, r.n_cmps, r.sum_h, r.xor_h) == (e.c_probe, e.c_cmp, e.out["sum_h"], e.out["xor_h"]), k
         t.close()
+
+
+def test_timing_events_measure_the_stream(ctx):
+    """hj3d_tevent_* (fence-free HIP events on the context stream, the bench's phase boundaries):
+    the span around a build equals the span torch.cuda.Event measures around the same work within
+    the events' jitter, and spans are ordered."""
+    import torch
+    import hj3d
+    n = 4_000_000
+    B = O.tuples3(np.random.default_rng(3).permutation(n).astype(np.uint32), np.zeros(n, np.uint32))
+    dB = dev(B)
+    t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, n)
+    t.build(hj3d.Rel(dB, 0))
+    torch.cuda.synchronize()
+    ev = [hj3d.TimingEvent(ctx) for _ in range(3)]
+    te = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    te[0].record()
+    ev[0].record()
+    for _ in range(5):
+        t.build(hj3d.Rel(dB, 0))
+    ev[1].record()
+    t.build(hj3d.Rel(dB, 0))
+    ev[2].record()
+    te[1].record()
+    torch.cuda.synchronize()
+    a, b = ev[0].elapsed_time(ev[1]), ev[1].elapsed_time(ev[2])
+    total = te[0].elapsed_time(te[1])
+    assert 0 < b < a and a + b <= total * 1.05 + 0.05, (a, b, total)
+    assert a + b >= 0.5 * total, (a, b, total)
+    t.close()
