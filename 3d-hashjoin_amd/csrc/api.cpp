@@ -82,6 +82,21 @@ hipError_t out_check(hj3d_ctx* ctx, const hj3d_table* t, uint32_t flags, uint64_
   return hipGetLastError();
 }
 
+// The fused build partition's grid barrier (radix.hip k_rp_fused) sets word 1 of ctx->gbar when a
+// barrier did not complete in time (its workgroups then went on, so the build is not valid). Result
+// reads copy the word with the result slot and report it.
+hipError_t gbar_copy(hj3d_ctx* ctx, uint64_t* word) {
+  *word = 0;
+  return ctx->gbar.p ? hipMemcpyAsync(word, ctx->gbar.as<uint64_t>() + 1, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                      ctx->stream)
+                     : hipSuccess;
+}
+hj3d_status gbar_check(hj3d_ctx* ctx, uint64_t word) {
+  if (!word) return HJ3D_OK;
+  (void)hipMemsetAsync(ctx->gbar.as<uint64_t>() + 1, 0, sizeof(uint64_t), ctx->stream);
+  return fail(ctx, HJ3D_EDEVICE, "fused build partition: a grid barrier timed out, a build since the last result is invalid");
+}
+
 }  // namespace
 
 extern "C" {
@@ -680,10 +695,12 @@ hj3d_status hj3d_probe_sel(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* p
 
 hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out) {
   if (!ctx || !out) return HJ3D_EINVAL;
-  uint64_t h[kResFields];
+  uint64_t h[kResFields], gw = 0;
   hipError_t e = hipMemcpyAsync(h, ctx->res.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = gbar_copy(ctx, &gw);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe_result");
+  if (const hj3d_status gs = gbar_check(ctx, gw); gs != HJ3D_OK) return gs;
   out->n_probe = h[0];
   out->n_matched = h[1];
   out->n_out = h[2];
@@ -718,10 +735,12 @@ hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* t
 
 hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out) {
   if (!ctx || !out) return HJ3D_EINVAL;
-  uint64_t h[kResFields];
+  uint64_t h[kResFields], gw = 0;
   hipError_t e = hipMemcpyAsync(h, ctx->res.p, sizeof(h), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = gbar_copy(ctx, &gw);
   if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
   if (e != hipSuccess) return from_hip(ctx, e, "hj3d_probe2_result");
+  if (const hj3d_status gs = gbar_check(ctx, gw); gs != HJ3D_OK) return gs;
   static_assert(sizeof(hj3d_probe2_res) == 12 * sizeof(uint64_t), "probe2 result layout");
   std::memcpy(out, h, sizeof(hj3d_probe2_res));
   return HJ3D_OK;

@@ -202,7 +202,9 @@ enum {
   HJ3D_OPT_NESTED_2L = 14,
   /* HJ3D_OPT_RP_UNFUSED (0/1, default 0): small implicit-row build partitions run as two launches
    * (histogram, then scatter) instead of the fused one-launch partition with its grid barrier
-   * (A/B measurements and the parity test of both forms). */
+   * (A/B measurements and the parity test of both forms). The fused form runs only when the
+   * occupancy API confirms all its workgroups are resident; should a barrier still not complete
+   * within 0.2 s, the next hj3d_probe_result / hj3d_probe2_result returns HJ3D_EDEVICE. */
   HJ3D_OPT_RP_UNFUSED = 15
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
