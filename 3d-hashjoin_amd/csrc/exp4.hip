@@ -31,13 +31,18 @@ struct Heavy2 {
   uint32_t pad;
 };
 
-__device__ __forceinline__ void add_triple(uint64_t (&a)[kF], uint32_t r, uint32_t s, uint32_t t) {
+// One output triple: its row sums always (the unnest reads every sub row, as AlgUnnestHt::step,
+// algebra.hh:510-541, produces every tuple), its hash only with HJ3D_PROBE_CHECKSUM (ck; the
+// verification checksums, which the reference does not compute; two mix64 per triple).
+__device__ __forceinline__ void add_triple(uint64_t (&a)[kF], uint32_t r, uint32_t s, uint32_t t, bool ck) {
   a[7] += r;
   a[8] += s;
   a[9] += t;
-  const uint64_t h = triple_hash(r, s, t);
-  a[10] += h;
-  a[11] ^= h;
+  if (ck) {
+    const uint64_t h = triple_hash(r, s, t);
+    a[10] += h;
+    a[11] ^= h;
+  }
 }
 
 struct NTab {  // nested table view
@@ -90,7 +95,7 @@ struct CTab {  // chaining table view
 // of 8 into registers before they are combined, so a match costs one or two memory latencies
 // instead of one per sub row.
 __device__ __forceinline__ void light_triples(uint64_t (&a)[kF], uint32_t pr, const NTab& S, const NTab& T, uint32_t zs,
-                                              uint32_t ws, uint32_t zt, uint32_t wt) {
+                                              uint32_t ws, uint32_t zt, uint32_t wt, bool ck) {
   constexpr uint32_t kB = 8;
   for (uint32_t qb = 0; qb < wt; qb += kB) {
     uint32_t tv[kB];
@@ -105,7 +110,7 @@ __device__ __forceinline__ void light_triples(uint64_t (&a)[kF], uint32_t pr, co
         if (qb + qu >= wt) break;
 #pragma unroll
         for (uint32_t pu = 0; pu < kB; ++pu)
-          if (pb + pu < ws) add_triple(a, pr, sv[pu], tv[qu]);
+          if (pb + pu < ws) add_triple(a, pr, sv[pu], tv[qu], ck);
       }
     }
   }
@@ -114,14 +119,14 @@ __device__ __forceinline__ void light_triples(uint64_t (&a)[kF], uint32_t pr, co
 // Ndu for one probe tuple after its two lookups (ms / mt: global main indices or kInvalid).
 __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const NTab& S, const NTab& T, uint32_t ms,
                                          const uint4& MS, uint32_t mt, const uint4& MT, Heavy2* __restrict__ heavy,
-                                         uint64_t* __restrict__ nheavy) {
+                                         uint64_t* __restrict__ nheavy, bool ck) {
   a[2] += 1;
   a[4] += MT.w;
   const uint64_t prod = uint64_t(MS.w) * MT.w;
   a[5] += prod;
   a[6] += prod;
   if (prod <= kInline2) {
-    if (!HJ3D_NDU_DIAG) light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w);
+    if (!HJ3D_NDU_DIAG) light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w, ck);
   } else {
     const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
     heavy[slot] = Heavy2{pr, ms, mt, 0};
@@ -130,21 +135,21 @@ __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const N
 
 // AlgNestJoinProbe(S) -> AlgNestJoinProbe(T) -> unnest both, for one probe tuple (HBM tables).
 __device__ __forceinline__ void ndu_probe(uint64_t (&a)[kF], uint32_t h, uint32_t pr, const NTab& S, const NTab& T,
-                                          Heavy2* __restrict__ heavy, uint64_t* __restrict__ nheavy) {
+                                          Heavy2* __restrict__ heavy, uint64_t* __restrict__ nheavy, bool ck) {
   uint4 MS, MT;
   const uint32_t ms = S.find(h, &a[1], &MS);
   if (ms == kInvalid) return;
   a[0] += 1;
   const uint32_t mt = T.find(h, &a[3], &MT);
   if (mt == kInvalid) return;
-  ndu_tail(a, pr, S, T, ms, MS, mt, MT, heavy, nheavy);
+  ndu_tail(a, pr, S, T, ms, MS, mt, MT, heavy, nheavy, ck);
 }
 
 __global__ __launch_bounds__(kBlock) void k_ndu(RelView r, NTab S, NTab T, Heavy2* __restrict__ heavy,
-                                                uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+                                                uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res, bool ck) {
   uint64_t a[kF] = {0};
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock)
-    ndu_probe(a, murmur32(r.key(i)), r.row(i), S, T, heavy, nheavy);
+    ndu_probe(a, murmur32(r.key(i)), r.row(i), S, T, heavy, nheavy, ck);
   block_flush<kF, 1>(a, res);
 }
 
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(kJBlock) void k_ndu_seg(const uint2* __restrict__ r
                                                      const uint32_t* __restrict__ seg, uint32_t G, uint32_t cap, NTab S,
                                                      NTab T, uint32_t W, uint32_t P, uint32_t splits, bool flat,
                                                      Heavy2* __restrict__ heavy, uint64_t* __restrict__ nheavy,
-                                                     uint64_t* __restrict__ res) {
+                                                     uint64_t* __restrict__ res, bool ck) {
   __shared__ uint32_t lds[kProbeLdsWords];
   const uint32_t p = blockIdx.x / splits, sp = blockIdx.x % splits;
   const uint32_t b0 = p * W;
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(kJBlock) void k_ndu_seg(const uint2* __restrict__ r
            },
            [&](uint32_t h, uint32_t pr, uint64_t) {
              if (!FITS) {
-               ndu_probe(a, h, pr, S, T, heavy, nheavy);
+               ndu_probe(a, h, pr, S, T, heavy, nheavy, ck);
                return;
              }
              const uint32_t bl = S.fm.mod(h) - S.lo - b0;
@@ -193,7 +198,7 @@ __global__ __launch_bounds__(kJBlock) void k_ndu_seg(const uint2* __restrict__ r
              const uint32_t dt = ldT[bl];
              const uint32_t mt = nfind(h, lmT, dt >> 16, dt & 0xFFFFu, &a[3], &MT);
              if (mt == kInvalid) return;
-             ndu_tail(a, pr, S, T, s0 + ms, MS, t0 + mt, MT, heavy, nheavy);
+             ndu_tail(a, pr, S, T, s0 + ms, MS, t0 + mt, MT, heavy, nheavy, ck);
            });
   block_flush<kF, 1>(a, res);
 }
@@ -201,16 +206,17 @@ __global__ __launch_bounds__(kJBlock) void k_ndu_seg(const uint2* __restrict__ r
 // Overflow pairs of the partition (runs that did not fit their region), against the HBM tables.
 __global__ __launch_bounds__(kBlock) void k_ndu_ovf(const uint2* __restrict__ ovf, const unsigned long long* __restrict__ novf,
                                                     NTab S, NTab T, Heavy2* __restrict__ heavy,
-                                                    uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+                                                    uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res, bool ck) {
   uint64_t a[kF] = {0};
   const uint64_t n = *novf;
   for (uint64_t j = uint64_t(blockIdx.x) * kBlock + threadIdx.x; j < n; j += uint64_t(gridDim.x) * kBlock)
-    ndu_probe(a, ovf[j].x, ovf[j].y, S, T, heavy, nheavy);
+    ndu_probe(a, ovf[j].x, ovf[j].y, S, T, heavy, nheavy, ck);
   block_flush<kF, 1>(a, res);
 }
 
 __global__ __launch_bounds__(kBlock) void k_ndu_heavy(NTab S, NTab T, const Heavy2* __restrict__ heavy,
-                                                      const uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+                                                      const uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res,
+                                                      bool ck) {
   uint64_t a[kF] = {0};
   const uint64_t nh = *nheavy;
   for (uint64_t q = blockIdx.x; q < nh; q += gridDim.x) {
@@ -219,14 +225,14 @@ __global__ __launch_bounds__(kBlock) void k_ndu_heavy(NTab S, NTab T, const Heav
     const uint64_t prod = uint64_t(MS.w) * MT.w;
     for (uint64_t k = threadIdx.x; k < prod; k += kBlock) {
       const uint32_t tq = uint32_t(k / MS.w), sq = uint32_t(k % MS.w);
-      add_triple(a, hv.r, S.sub[MS.z + sq], T.sub[MT.z + tq]);
+      add_triple(a, hv.r, S.sub[MS.z + sq], T.sub[MT.z + tq], ck);
     }
   }
   block_flush<kF, 1>(a, res);
 }
 
 __global__ __launch_bounds__(kBlock) void k_chj(RelView r, CTab S, CTab T, Heavy2* __restrict__ heavy,
-                                                uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+                                                uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res, bool ck) {
   uint64_t a[kF] = {0};
   for (uint64_t i = uint64_t(blockIdx.x) * kBlock + threadIdx.x; i < r.n; i += uint64_t(gridDim.x) * kBlock) {
     const uint32_t h = murmur32(r.key(i));
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(kBlock) void k_chj(RelView r, CTab S, CTab T, Heavy
         if (es.x != h) continue;
         for (uint32_t kt = t0; kt < t1; ++kt) {
           const uint2 et = T.ent[kt];
-          if (et.x == h) add_triple(a, pr, es.y, et.y);
+          if (et.x == h) add_triple(a, pr, es.y, et.y, ck);
         }
       }
     } else {
@@ -267,7 +273,8 @@ __global__ __launch_bounds__(kBlock) void k_chj(RelView r, CTab S, CTab T, Heavy
 
 // Heavy chaining products: the block walks the S bucket; its threads stride over the T bucket.
 __global__ __launch_bounds__(kBlock) void k_chj_heavy(CTab S, CTab T, const Heavy2* __restrict__ heavy,
-                                                      const uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res) {
+                                                      const uint64_t* __restrict__ nheavy, uint64_t* __restrict__ res,
+                                                      bool ck) {
   uint64_t a[kF] = {0};
   const uint64_t nh = *nheavy;
   for (uint64_t q = blockIdx.x; q < nh; q += gridDim.x) {
@@ -281,7 +288,7 @@ __global__ __launch_bounds__(kBlock) void k_chj_heavy(CTab S, CTab T, const Heav
       if (es.x != h) continue;
       for (uint32_t kt = t0 + threadIdx.x; kt < t1; kt += kBlock) {
         const uint2 et = T.ent[kt];
-        if (et.x == h) add_triple(a, hv.r, es.y, et.y);
+        if (et.x == h) add_triple(a, hv.r, es.y, et.y, ck);
       }
     }
   }
@@ -295,6 +302,7 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
   (void)out;
   (void)out_cap;
   if (flags & HJ3D_PROBE_EMIT) return hipErrorNotSupported;
+  const bool ck = flags & HJ3D_PROBE_CHECKSUM;  // triple hashes (sum_h, xor_h); row sums always
   // the result slot and the heavy-item counter start at zero: one launch clears both (with the
   // partitioner's own counters on the partitioned path)
   ZeroList z;
@@ -325,28 +333,28 @@ hipError_t probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, con
       if (e == hipSuccess) {
         const uint32_t nblocks = pp.P * pp.splits;
         hipLaunchKernelGGL(k_ndu_seg<true>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,
-                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res);
+                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res, ck);
         hipLaunchKernelGGL(k_ndu_seg<false>, dim3(nblocks), dim3(kJBlock), 0, s, pp.region, pp.counts, pp.seg, pp.G,
-                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res);
+                           pp.cap, S, T, pp.W, pp.P, pp.splits, pp.flat, heavy, nheavy, res, ck);
         hipLaunchKernelGGL(k_ndu_ovf, dim3(ctx->num_cus), dim3(kBlock), 0, s, pp.ovf, pp.novf, S, T, heavy, nheavy,
-                           res);
+                           res, ck);
       }
     }
     if (e == hipErrorNotSupported) {
       if ((e = zero_words(z, s)) != hipSuccess) return e;
-      hipLaunchKernelGGL(k_ndu, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res);
+      hipLaunchKernelGGL(k_ndu, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res, ck);
     } else if (e != hipSuccess) {
       return e;
     }
-    hipLaunchKernelGGL(k_ndu_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res);
+    hipLaunchKernelGGL(k_ndu_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res, ck);
   } else {
     if ((e = zero_words(z, s)) != hipSuccess) return e;
     CTab S{ts->off.as<const uint32_t>(), ts->ent.as<const uint2>(), ts->fm, uint32_t(ts->desc.bucket_lo),
            ts->nb_local};
     CTab T{tt->off.as<const uint32_t>(), tt->ent.as<const uint2>(), tt->fm, uint32_t(tt->desc.bucket_lo),
            tt->nb_local};
-    hipLaunchKernelGGL(k_chj, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res);
-    hipLaunchKernelGGL(k_chj_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res);
+    hipLaunchKernelGGL(k_chj, dim3(g), dim3(kBlock), 0, s, v, S, T, heavy, nheavy, res, ck);
+    hipLaunchKernelGGL(k_chj_heavy, dim3(ctx->num_cus * 4), dim3(kBlock), 0, s, S, T, heavy, nheavy, res, ck);
   }
   return hipGetLastError();
 }

@@ -353,8 +353,11 @@ class Context:
             self._check(st, "hj3d_probe_result")
         return ProbeResult(*(getattr(r, f) for f, _ in _ProbeRes._fields_), overflow=st == HJ3D_EOVERFLOW)
 
-    def probe2(self, ts: "Table", tt: "Table", rel: Rel, fetch: bool = True) -> Optional[dict]:
-        self._check(lib().hj3d_probe2(self.h, ts.h, tt.h, C.byref(rel.c), 0, None, 0), "hj3d_probe2")
+    def probe2(self, ts: "Table", tt: "Table", rel: Rel, fetch: bool = True, checksum: bool = True) -> Optional[dict]:
+        """The experiment-4 strand. checksum=False leaves out the triple hashes (sum_h, xor_h: a
+        verification aid the reference does not compute); counters and row sums stay exact."""
+        flags = PROBE_CHECKSUM if checksum else 0
+        self._check(lib().hj3d_probe2(self.h, ts.h, tt.h, C.byref(rel.c), flags, None, 0), "hj3d_probe2")
         return self.probe2_result() if fetch else None
 
     def probe2_result(self) -> dict:

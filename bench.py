@@ -928,6 +928,7 @@ def main_single_config(args):
         tt.reserve(T.shape[0])
         relR, relS, relT = hj3d.Rel(R, key_word=0), hj3d.Rel(S, key_word=1), hj3d.Rel(T, key_word=1)
         fx = fixture(f"exp4_R{log2R}_a{a}_A{A}_b{b}_B{B}")
+        state = {"ck": False}
 
         def step(ev):
             l0 = hj3d.lib().hj3d_launch_count()
@@ -935,7 +936,8 @@ def main_single_config(args):
             ctx.build_many([ts, tt], [relS, relT])  # one launch sequence for both tables
             ev[1].record()
             l1 = hj3d.lib().hj3d_launch_count()
-            ctx.probe2(ts, tt, relR, fetch=False)
+            # (the triple hashes only in the verification step, as the other workloads' checksums)
+            ctx.probe2(ts, tt, relR, fetch=False, checksum=state["ck"])
             ev[2].record()
             launches.append((l1 - l0, hj3d.lib().hj3d_launch_count() - l1))
 
@@ -986,6 +988,9 @@ def main_single_config(args):
                                n_out / (probe_ms * 1e-3))
         n_build = nS
     else:
+        state["ck"] = True  # verification step: the same step with the triple checksums folded in
+        step(_events(torch, 3))
+        torch.cuda.synchronize()
         r = ctx.probe2_result()
         counters = {k: r[k] for k in ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp", "c_unnest_1",
                                       "c_unnest_2", "c_top")}
@@ -996,6 +1001,8 @@ def main_single_config(args):
                 ("c_probe_rs", "c_probe_RS"), ("c_probe_rs_cmp", "c_probe_RS_cmp"), ("c_probe_rt", "c_probe_RT"),
                 ("c_probe_rt_cmp", "c_probe_RT_cmp"), ("c_unnest_1", "c_unnest_1"), ("c_unnest_2", "c_unnest_2"),
                 ("c_top", "c_top")))
+            if "out" in ref:
+                verify["out"] = all(r[k] == ref["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h"))
         else:
             nc, A = nR >> 3, 4
             verify["against"] = "analytic counters of experiment 4"

@@ -312,7 +312,9 @@ hj3d_status hj3d_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel* probe
 hj3d_status hj3d_probe_result(hj3d_ctx* ctx, hj3d_probe_res* out);
 
 /* Experiment-4 probe strand over two tables built on S and T (both HJ3D_NESTED: Ndu with deferred
- * unnesting; both HJ3D_CHAIN: Chj). With HJ3D_PROBE_EMIT, triples {u32 r, s, t} go to out_dev. */
+ * unnesting; both HJ3D_CHAIN: Chj). With HJ3D_PROBE_EMIT, triples {u32 r, s, t} go to out_dev.
+ * The row sums sum_a / sum_b / sum_c are always folded (the unnest reads every output triple's
+ * rows); the triple hashes sum_h / xor_h only with HJ3D_PROBE_CHECKSUM (else 0). */
 hj3d_status hj3d_probe2(hj3d_ctx* ctx, const hj3d_table* ts, const hj3d_table* tt, const hj3d_rel* probe,
                         uint32_t flags, void* out_dev, uint64_t out_cap);
 hj3d_status hj3d_probe2_result(hj3d_ctx* ctx, hj3d_probe2_res* out);
