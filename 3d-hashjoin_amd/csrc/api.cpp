@@ -13,6 +13,8 @@
 #include "hj3d_internal.hpp"
 
 #include <atomic>
+#include <chrono>
+#include <sched.h>
 
 namespace hj3d {
 static std::atomic<uint64_t> g_launches{0};
@@ -95,6 +97,18 @@ hj3d_status gbar_check(hj3d_ctx* ctx, uint64_t word) {
   if (!word) return HJ3D_OK;
   (void)hipMemsetAsync(ctx->gbar.as<uint64_t>() + 1, 0, sizeof(uint64_t), ctx->stream);
   return fail(ctx, HJ3D_EDEVICE, "fused build partition: a grid barrier timed out, a build since the last result is invalid");
+}
+// The same for one table, in every getter that hands out its content: a chaining table built by the
+// fused partition carries its launch tag (gbar_tag), and a timed-out barrier wrote that tag into the
+// table's counts word 3 (synchronous; tables of other builds skip the read).
+hj3d_status table_gbar_check(hj3d_ctx* ctx, const hj3d_table* t) {
+  if (!t->gbar_tag) return HJ3D_OK;
+  uint64_t w = 0;
+  hipError_t e = hipMemcpyAsync(&w, t->counts.as<const uint64_t>() + 3, sizeof(w), hipMemcpyDeviceToHost, ctx->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+  if (e != hipSuccess) return from_hip(ctx, e, "fused build partition flag");
+  if (w != t->gbar_tag) return HJ3D_OK;
+  return fail(ctx, HJ3D_EDEVICE, "fused build partition: a grid barrier timed out, the table is invalid (rebuild it)");
 }
 
 }  // namespace
@@ -190,6 +204,10 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_SYNC_BUILD: ctx->sync_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_2L: ctx->nested_2l = value != 0; return HJ3D_OK;
     case HJ3D_OPT_RP_UNFUSED: ctx->rp_unfused = value != 0; return HJ3D_OK;
+    case HJ3D_OPT_DIAG_GBAR:
+      if (value < 0) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_DIAG_GBAR: >= 0");
+      ctx->diag_gbar = uint64_t(value);
+      return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);
@@ -340,6 +358,7 @@ hj3d_status hj3d_table_reserve(hj3d_ctx* ctx, hj3d_table* t, uint64_t max_build)
 hj3d_status hj3d_table_clear(hj3d_ctx* ctx, hj3d_table* t) {
   if (!ctx || !t) return HJ3D_EINVAL;
   t->pending = false;
+  t->gbar_tag = 0;
   hipError_t e = hipMemsetAsync(t->off.p, 0, (uint64_t(t->nb_local) + 1) * sizeof(uint32_t), ctx->stream);
   if (e == hipSuccess) e = hipMemsetAsync(t->counts.p, 0, 4 * sizeof(uint64_t), ctx->stream);
   t->n_build = 0;
@@ -423,6 +442,7 @@ static hipError_t build_one(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build)
   PhaseTimer tm(ctx, HJ3D_T_BUILD);
   hipError_t e;
   t->pending = false;  // a build in flight for the old content is replaced (its copy stays stream-ordered)
+  t->gbar_tag = 0;     // (set again by a fused build partition)
   // the build's row range (implicit rows: row_base + [0, n)); explicit rows: unknown
   t->row_lo = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base < (1ull << 32) ? uint32_t(build->row_base) : 0u;
   t->row_rr = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base + build->n <= (1ull << 32) ? build->n : 0u;
@@ -491,8 +511,17 @@ hipError_t table_resolve(hj3d_ctx* ctx, hj3d_table* t) {
   t->pending = false;
   // polled, not waited for: the build is short (config E: ~0.3 ms) and the probe's launches follow
   // as soon as it lands (a blocking wait's wake-up left the GPU idle for ~20 us)
+  // A short build lands within the spin; past 50 us the loop yields its core to other host threads
+  // (an RCCL proxy, other ranks), and past 20 ms it blocks.
   hipError_t e;
+  const auto t0 = std::chrono::steady_clock::now();
   while ((e = hipEventQuery(t->hc_ev)) == hipErrorNotReady) {
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    if (us > 20000) {
+      e = hipEventSynchronize(t->hc_ev);
+      break;
+    }
+    if (us > 50) sched_yield();
   }
   if (e != hipSuccess) {
     t->built = false;
@@ -533,6 +562,7 @@ uint64_t hj3d_launch_count(void) { return hj3d::launch_total(); }
 
 hj3d_status hj3d_table_finish(hj3d_ctx* ctx, hj3d_table* t) {
   if (!ctx || !t) return HJ3D_EINVAL;
+  if (const hj3d_status gs = table_gbar_check(ctx, t); gs != HJ3D_OK) return gs;
   return from_hip(ctx, table_resolve(ctx, t), "hj3d_table_finish");
 }
 
@@ -541,6 +571,7 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
   if (!ctx || !t || !n_payload || !n_sub) return HJ3D_EINVAL;
   const uint64_t nbl = t->nb_local;
   uint32_t last = 0;  // off[nb_local] = the payload count
+  if (const hj3d_status gs = table_gbar_check(ctx, t); gs != HJ3D_OK) return gs;
   hipError_t e = resolve(ctx, t);
   if (e != hipSuccess) return from_hip(ctx, e, "hj3d_table_export");
   e = hipMemcpyAsync(&last, t->off.as<uint32_t>() + nbl, sizeof(last), hipMemcpyDeviceToHost, ctx->stream);
@@ -563,6 +594,7 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
 hj3d_status hj3d_table_stats(hj3d_ctx* ctx, const hj3d_table* t, hj3d_stats* out) {
   if (!ctx || !t || !out) return HJ3D_EINVAL;
   std::memset(out, 0, sizeof(*out));
+  if (const hj3d_status gs = table_gbar_check(ctx, t); gs != HJ3D_OK) return gs;
   hipError_t e = resolve(ctx, t);
   if (e == hipSuccess) e = table_stats(ctx, t, out, ctx->stream);
   return from_hip(ctx, e, "hj3d_table_stats");

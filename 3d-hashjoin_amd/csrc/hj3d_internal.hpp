@@ -113,8 +113,12 @@ struct hj3d_ctx {
   uint32_t part_parity = 0;
   // grid barrier of the fused partition (radix.hip k_rp_fused): word 0 a monotonic arrival counter
   // (each launch waits for the running sum of the grids launched on it), word 1 the timeout flag
+  // (the timeout flag is also written into the built table's counts word 3, tagged with the launch's
+  // sequence number gbar_seq, and checked by the table's getters)
   hj3d::DevBuf gbar;
   uint64_t gbar_target = 0;
+  uint64_t gbar_seq = 0;
+  uint64_t diag_gbar = 0;  // HJ3D_OPT_DIAG_GBAR: barrier timeout in 100 MHz ticks, workgroup 0 never arrives
   hipError_t ensure_ctl() {
     if (ctl.p) return hipSuccess;
     hipError_t e = ctl.ensure(128 * sizeof(uint64_t));  // 8 control words; [64, 128): store sink
@@ -152,7 +156,9 @@ struct hj3d_table {
   // nested:   off[nb_local+1] over mains, main[d] = {hash, first_row, sub_off, sub_len},
   //           sub[n] = build rows grouped per key (first occurrence first, then row order)
   hj3d::DevBuf off, ent, main, sub;
-  hj3d::DevBuf counts;    // device u64[4]: {entries, distinct, max_sub_len, reserved}
+  hj3d::DevBuf counts;    // device u64[4]: {entries, distinct, max_sub_len, give-up flag (nested) /
+                          // fused-partition barrier timeout tag (chaining)}
+  uint64_t gbar_tag = 0;  // chaining tables built by the fused partition: its launch tag (0: none)
 };
 
 namespace hj3d {

@@ -868,6 +868,16 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   // slice its LDS width (pk_probe_slices); before, such tables were probed in ~1 MB slices through L2
   PkGeom pk{};
   bool pkd = false;
+  // once the packed partitioner has run, its control words (overflow count, n_probe) go back to zero
+  // on every exit, early returns included: the probes that share them rely on that
+  struct CtlReset {
+    hj3d_ctx* c;
+    hipStream_t st;
+    bool armed = false;
+    ~CtlReset() {
+      if (armed) (void)pk_ctl_reset(c, st);
+    }
+  } ctl_reset{ctx, s};
   {
     const uint64_t P0 = (uint64_t(nbl) + w_fit - 1) / w_fit;
     if (HJ3D_RN_PK && !sel && w_fit >= 64 && P0 > 2048 && P0 <= 65536) {
@@ -875,7 +885,7 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
       const uint64_t P1 = (P0 + G - 1) / G * G;  // whole waves of probe workgroups
       const uint32_t W1 = uint32_t((uint64_t(nbl) + P1 - 1) / P1);
       e = pk_probe_slices(ctx, t, r, W1 >= 64 ? W1 : w_fit, &pp, &pk, s);
-      if (e == hipSuccess) pkd = true;
+      if (e == hipSuccess) pkd = ctl_reset.armed = true;
       else if (e != hipErrorNotSupported) return e;
       if (pkd && also && (e = zero_words(*also, s)) != hipSuccess) return e;
     }
@@ -961,7 +971,10 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   if ((e = hipGetLastError()) != hipSuccess) return e;
   // the packed partitioner's control words (overflow count, n_probe) back to zero, the invariant of
   // the probes that share them
-  if (pkd && (e = pk_ctl_reset(ctx, s)) != hipSuccess) return e;
+  if (pkd) {
+    ctl_reset.armed = false;
+    if ((e = pk_ctl_reset(ctx, s)) != hipSuccess) return e;
+  }
   // n_probe counts every scanned tuple, also those of unowned buckets (dropped by the partition)
   if ((e = reduce_partials(partials, nblocks + 1, kProbeFields, 1, res, s, sel ? 0ull : r.n, base0)) != hipSuccess)
     return e;

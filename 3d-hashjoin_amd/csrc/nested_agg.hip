@@ -88,6 +88,10 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
 
+#ifndef HJ3D_NAGG_ENDBAR
+#define HJ3D_NAGG_ENDBAR 0  // a barrier after the last round of a partition too (1: A/B)
+#endif
+
 #ifndef HJ3D_NAGG_CLK
 #define HJ3D_NAGG_CLK 0  // diagnostic: per-workgroup phase clocks of k_nagg (read by hj3d_diag_nagg_clk)
 #endif
@@ -497,7 +501,10 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     mrun += nk;
     srun += nrows;
     c0 = c1;
-    __syncthreads();
+    // the barrier orders this round's LDS reads before the next round's table clear; after the last
+    // round there is none to wait for (a barrier there also waits for pass B's scattered stores to
+    // drain before the workgroup can end)
+    if (HJ3D_NAGG_ENDBAR || c0 < nbs) __syncthreads();
   }
   nagg_clk(gp, 5);
   if (threadIdx.x == 0) dcount[gp] = mrun;

@@ -172,7 +172,9 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
   uint32_t* wsum = reinterpret_cast<uint32_t*>(stage);
   // explicit row ids are loaded with the keys, a tile ahead (loading them at the stage write after
   // the ranking phase waited for every load separately: one round trip per tuple and round)
-  const bool explicit_rows = rt.r0.row_off != 0xFFFFFFFFu;  // (both relations alike)
+  // (relation 0's mode; a relation 1 of the other mode is still right: its rows come from r.row(i)
+  // at the stage write when relation 0 is implicit, and r.row(i) resolves implicit rows otherwise)
+  const bool explicit_rows = rt.r0.row_off != 0xFFFFFFFFu;
   uint32_t h[ROUNDS], rw[ROUNDS];
   auto load = [&](uint32_t tile) __attribute__((always_inline)) {
     const RelView& r = rt.rel(tile);
@@ -260,15 +262,30 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
 constexpr int kFzRounds = 8;
 constexpr int kFzGroup = HJ3D_RP_FZ_GROUP;
 constexpr int kFzTMax = 6;  // tiles per workgroup held in registers (48 hashes per thread)
-__device__ __forceinline__ void grid_barrier(uint64_t* __restrict__ bar, uint64_t target) {
+// On a timeout the workgroup sets the context's word bar[1] (read with the probe results) and writes
+// the launch's tag (the context's fused-launch sequence number) into the table's flag word `tflag`
+// (its counts word 3, unused by chaining tables): the table getters compare that word with the tag
+// the table was built under, so a later build's timeout never marks this table and this one's is
+// never lost. `ticks`: the timeout in 100 MHz ticks; `skip0`: workgroup 0 does not arrive
+// (diagnostic HJ3D_OPT_DIAG_GBAR: the barrier cannot complete, every workgroup times out).
+struct FzBar {
+  uint64_t* bar;
+  uint64_t target;
+  uint64_t* tflag;
+  uint64_t tag;
+  uint64_t ticks;
+  uint32_t skip0;
+};
+__device__ __forceinline__ void grid_barrier(const FzBar& b) {
   __syncthreads();
   if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    if (!(b.skip0 && blockIdx.x == 0)) __hip_atomic_fetch_add(b.bar, 1ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t0 = wall_clock64();
-    while (__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < target) {
+    while (__hip_atomic_load(b.bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < b.target) {
       __builtin_amdgcn_s_sleep(2);
-      if (wall_clock64() - t0 > 20000000ull) {  // 0.2 s at 100 MHz
-        __hip_atomic_store(bar + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (wall_clock64() - t0 > b.ticks) {  // default 0.2 s at 100 MHz
+        __hip_atomic_store(b.bar + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(b.tflag, b.tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         break;
       }
     }
@@ -286,8 +303,7 @@ struct FzGeom {
 template <int TMAX>
 __global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, uint32_t ntiles, uint32_t* __restrict__ cur,
                                                       uint32_t* __restrict__ cur_next, uint32_t* __restrict__ ps,
-                                                      uint2* __restrict__ out, uint64_t* __restrict__ bar,
-                                                      uint64_t target) {
+                                                      uint2* __restrict__ out, FzBar fb) {
   constexpr int R = kFzRounds;
   constexpr int kTile = kPBlock * R;
   __shared__ uint2 stage[kTile * kFzGroup];
@@ -335,7 +351,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, ui
     const uint32_t c = loc[p];
     gb[p] = c ? atomicAdd(&cur[p], c) : 0u;  // this workgroup's run inside partition p
   }
-  grid_barrier(bar, target);
+  grid_barrier(fb);
   // partition sizes are final: starts by an LDS scan (the cursors read at L2, past this CU's cache)
   for (uint32_t p = me; p < P; p += kPBlock) loc[p] = __hip_atomic_load(cur + p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
@@ -1658,9 +1674,16 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
         if ((e = ctx->gbar.ensure(2 * sizeof(uint64_t))) != hipSuccess) return e;
         if ((e = hipMemsetAsync(ctx->gbar.p, 0, ctx->gbar.bytes, s)) != hipSuccess) return e;
       }
-      ctx->gbar_target += g;
+      // the target counts this launch's arrivals; the context's running sum moves only once the
+      // launch is accepted (a failed launch adds no arrivals, so every later barrier would time out)
+      FzBar fb;
+      fb.bar = ctx->gbar.as<uint64_t>();
+      fb.skip0 = ctx->diag_gbar ? 1u : 0u;
+      fb.target = ctx->gbar_target + g;
+      fb.tflag = const_cast<hj3d_table*>(t)->counts.as<uint64_t>() + 3;
+      fb.tag = ctx->gbar_seq + 1;
+      fb.ticks = ctx->diag_gbar ? ctx->diag_gbar : 20000000ull;
       PhaseTimer tm(ctx, t_scatter);
-      uint64_t* bar = ctx->gbar.as<uint64_t>();
       FzGeom fz;
       fz.dnb = FastDiv32::make(uint32_t(t->desc.num_buckets));
       fz.dw = FastDiv32::make(pl.W);
@@ -1669,8 +1692,7 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
       fz.nbl = t->nb_local;
       fz.P = PT;
 #define HJ3D_FZ_LAUNCH(T)                                                                                             \
-  hipLaunchKernelGGL(k_rp_fused<T>, dim3(g), dim3(kPBlock), 0, s, rt, fz, ntiles, cur, cur_next, ps, out, bar, \
-                     ctx->gbar_target)
+  hipLaunchKernelGGL(k_rp_fused<T>, dim3(g), dim3(kPBlock), 0, s, rt, fz, ntiles, cur, cur_next, ps, out, fb)
       switch (tpw <= 2 ? 2 : tpw) {
         case 2: HJ3D_FZ_LAUNCH(2); break;
         case 3: HJ3D_FZ_LAUNCH(3); break;
@@ -1679,7 +1701,11 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
         default: HJ3D_FZ_LAUNCH(6); break;
       }
 #undef HJ3D_FZ_LAUNCH
-      return hipGetLastError();
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      ctx->gbar_target += g - fb.skip0;  // the arrivals this launch makes
+      ctx->gbar_seq = fb.tag;
+      const_cast<hj3d_table*>(t)->gbar_tag = fb.tag;  // the table's getters check its flag word
+      return hipSuccess;
     }
   }
   {
@@ -1693,7 +1719,9 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   }
   {
     PhaseTimer tm(ctx, t_scatter);
-    const bool ex = r.row_off != HJ3D_ROW_IMPLICIT;
+    // explicit rows when either relation has them (RelView::row resolves implicit rows too): the
+    // row mode of relation 0 alone would give relation 1's explicit rows as row_base + i
+    const bool ex = r.row_off != HJ3D_ROW_IMPLICIT || (r1 && r1->row_off != HJ3D_ROW_IMPLICIT);
 #define HJ3D_WS_LAUNCH(PPT, EX)                                                                                   \
   hipLaunchKernelGGL((k_rp_wscatter<PPT, EX>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, \
                      ntiles, hist, cur, cur_next, ps, out)

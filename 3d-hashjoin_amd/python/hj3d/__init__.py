@@ -29,6 +29,7 @@ OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFU
 OPT_PROBE_ITEMS = 7
 OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_PK_COMPACT, OPT_SYNC_BUILD, OPT_NESTED_2L = 8, 9, 10, 11, 12, 13, 14
 OPT_RP_UNFUSED = 15
+OPT_DIAG_GBAR = 16
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -125,6 +126,7 @@ def lib():
         "hj3d_launch_count": (u64, []),
         "hj3d_table_stats": (st, [p, p, C.POINTER(_Stats)]),
         "hj3d_table_size": (st, [p, p, C.POINTER(u64), C.POINTER(u64)]),
+        "hj3d_table_export": (st, [p, p, p, p, p, C.POINTER(u64), C.POINTER(u64)]),
         "hj3d_probe": (st, [p, p, R, u32, p, u64]),
         "hj3d_probe_result": (st, [p, C.POINTER(_ProbeRes)]),
         "hj3d_probe2": (st, [p, p, p, R, u32, p, u64]),
@@ -448,6 +450,12 @@ class Context:
         one-launch partition (HJ3D_OPT_RP_UNFUSED; tests and A/B)."""
         self.set_option(OPT_RP_UNFUSED, int(on))
 
+    def diag_gbar(self, ticks: int = 0):
+        """Diagnostic (HJ3D_OPT_DIAG_GBAR): the fused build partition's grid barrier times out after
+        `ticks` of the 100 MHz clock and its workgroup 0 never arrives, so the barrier fails (tests
+        of the failure path; 0 = off)."""
+        self.set_option(OPT_DIAG_GBAR, int(ticks))
+
     def sync_build(self, on: bool = True):
         """Nested builds finished inside hj3d_build (HJ3D_OPT_SYNC_BUILD): the build relation may
         be released when the call returns."""
@@ -761,4 +769,5 @@ class Table:
 
 
 from .plans import (EXP1_PLANS, exp1_plan, exp1_plan_sharded, exp1_relations_ref, exp4_plan,  # noqa: E402,F401
-                    exp4_relations_ref, merge_shard_stats, num_buckets_exp1, num_distinct_sharded)
+                    exp4_plan_sharded, exp4_relations_ref, merge_exp4, merge_shard_stats, num_buckets_exp1,
+                    num_distinct_sharded)

@@ -272,3 +272,48 @@ def allreduce_max(value: float, device) -> float:
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def exp4_join(ctx, plan: str, R: torch.Tensor, S: torch.Tensor, T: torch.Tensor, nb: int, row_base=(0, 0, 0),
+              group=None, checksum: bool = True) -> dict:
+    """Experiment 4 on this rank of the multi-GPU strand: R {k,a}, S {k,a}, T {k,a} are
+    this rank's contiguous slices ((n, 2) int32 device tensors; their first global rows in row_base).
+    The three relations are co-partitioned by bucket range of the one FK hash (R on R.k, S and T on
+    S.a / T.a: owner(bucket) = bucket * world / nb, hj3d_partition, stable, global rows), their
+    counts travel in ONE collective and their pairs in one exchange (three asynchronous pair
+    all-to-alls); the rank builds its S and T tables over its bucket range (one hj3d_build_many) and
+    runs the two-table probe strand on its R pairs (hj3d_probe2: Ndu, main_experiment4.cc:831-941,
+    or Chj, :943-1043). The counters are all-reduced (sums; the triple hash's xor by all-gather), so
+    every rank returns the single-table result."""
+    import hj3d
+    from .plans import EXP4_SUM
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    kind = hj3d.HJ3D_NESTED if plan == "Ndu" else hj3d.HJ3D_CHAIN
+    dev = R.device
+    rels = [hj3d.Rel(R, 0, row_base=row_base[0]), hj3d.Rel(S, 1, row_base=row_base[1]),
+            hj3d.Rel(T, 1, row_base=row_base[2])]
+    send = [torch.empty((max(r.n, 1), 2), dtype=torch.int32, device=dev) for r in rels]
+    cnt = torch.zeros((3, world), dtype=torch.int64, device=dev)
+    for k in range(3):
+        ctx.partition(rels[k], nb, world, send[k], cnt[k])
+    sc, rc = exchange_counts(cnt, group)
+    recv = [torch.empty((max(int(sum(rc[k])), 1), 2), dtype=torch.int32, device=dev) for k in range(3)]
+    got, works = [], []
+    for k in range(3):
+        v, w = exchange_pairs_async(send[k], sc[k], rc[k], recv[k], group)
+        got.append(v)
+        works.append(w)
+    for w in works:
+        if w is not None:
+            w.wait()
+    lo, hi = hj3d.part_range(nb, world, rank)
+    ts, tt = hj3d.Table(ctx, kind, nb, lo, hi), hj3d.Table(ctx, kind, nb, lo, hi)
+    own = [hj3d.Rel(got[k], 0, row_word=1, n=int(sum(rc[k]))) for k in range(3)]
+    ctx.build_many([ts, tt], [own[1], own[2]])
+    r = ctx.probe2(ts, tt, own[0], checksum=checksum)
+    ts.close()
+    tt.close()
+    out = dict(zip(EXP4_SUM, allreduce_sum_u64([r[k] for k in EXP4_SUM], dev)))
+    out["xor_h"] = allreduce_xor_u64(r["xor_h"], dev)
+    out["per_rank"] = {"probe_tuples": own[0].n, "build_tuples": own[1].n + own[2].n}
+    return out

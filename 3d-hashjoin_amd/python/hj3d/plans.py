@@ -240,3 +240,72 @@ def exp4_plan(ctx: Context, plan: str, R, S, T, nb: int, fused: bool = True) -> 
         tt.build(rt)
     r = ctx.probe2(ts, tt, Rel(R, key_word=0))
     return r
+
+
+EXP4_SUM = ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp", "c_unnest_1", "c_unnest_2", "c_top",
+            "sum_a", "sum_b", "sum_c", "sum_h")
+
+
+def merge_exp4(parts: list) -> dict:
+    """Experiment-4 counters of disjoint bucket ranges (probe2 results): every counter and row sum
+    adds (each R tuple, and every S / T tuple it can meet, lives in exactly one range), the triple
+    hash xor-folds."""
+    from . import MASK64
+    out = {k: sum(r[k] for r in parts) & MASK64 for k in EXP4_SUM}
+    x = 0
+    for r in parts:
+        x ^= r["xor_h"]
+    out["xor_h"] = x
+    return out
+
+
+def exp4_plan_sharded(ctx: Context, plan: str, R, S, T, nb: int, parts: int, timing: list | None = None,
+                      checksum: bool = True) -> dict:
+    """Experiment 4 split as the multi-GPU strand splits it (Ndu co-partitions R, S and T
+    on the one FK hash, one exchange), emulated on ONE device owner after owner: R (on R.k), S and T
+    (on S.a, T.a) are partitioned into `parts` bucket ranges by the exchange partitioner
+    (hj3d_partition: stable, so received pairs keep global row order, which fixes the chaining form's
+    chain order); owner p builds its S and T tables over [lo, hi) from its pairs (explicit global rows,
+    one hj3d_build_many for both) and runs the two-table probe strand with its R pairs (hj3d_probe2:
+    main_experiment4.cc:831-941 Ndu, 943-1043 Chj). The owners' counters add up to the single-device
+    run's (merge_exp4). timing: per-owner build / probe ms appended (library timers)."""
+    import torch
+    from . import T_BUILD, T_PARTITION, T_PROBE, part_range
+    kind = HJ3D_NESTED if plan == "Ndu" else HJ3D_CHAIN
+    dev = R.device
+    rels = [Rel(R, key_word=0), Rel(S, key_word=1), Rel(T, key_word=1)]
+    bufs = [torch.empty((max(r.n, 1), 2), dtype=torch.int32, device=dev) for r in rels]
+    cnts = torch.zeros((3, parts), dtype=torch.int64, device=dev)
+    if timing is not None:
+        ctx.timing(True)
+        ctx.timer_reset()
+    for k in range(3):
+        ctx.partition(rels[k], nb, parts, bufs[k], cnts[k])
+    cs = [[0] + torch.cumsum(cnts[k], 0).tolist() for k in range(3)]
+
+    def timers():
+        ctx.sync()
+        d = {}
+        for name, ph in (("partition", T_PARTITION), ("build", T_BUILD), ("probe", T_PROBE)):
+            ms, cnt = ctx.timer(ph)
+            if cnt:
+                d[name] = ms
+        ctx.timer_reset()
+        return d
+    if timing is not None:
+        timing.append(dict(owner="partition", **timers()))
+    res = []
+    for p in range(parts):
+        lo, hi = part_range(nb, parts, p)
+        ts, tt = Table(ctx, kind, nb, lo, hi), Table(ctx, kind, nb, lo, hi)
+        own = [Rel(bufs[k][cs[k][p]:cs[k][p + 1]], key_word=0, row_word=1, n=cs[k][p + 1] - cs[k][p]) for k in range(3)]
+        ts.reserve(max(own[1].n, 1))
+        tt.reserve(max(own[2].n, 1))
+        ctx.build_many([ts, tt], [own[1], own[2]])
+        res.append(ctx.probe2(ts, tt, own[0], checksum=checksum))
+        if timing is not None:
+            timing.append(dict(owner=p, bucket_lo=lo, bucket_hi=hi, probe_tuples=own[0].n, build_tuples=own[1].n + own[2].n,
+                               **timers()))
+        ts.close()
+        tt.close()
+    return merge_exp4(res)

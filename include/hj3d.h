@@ -66,7 +66,10 @@ typedef struct hj3d_table hj3d_table; /* a device-resident hash table (chaining 
  * key_off of every tuple (main_experiment1.cc:86 tuple {k,a,b} -> stride 12, key_off 0 for
  * R.k, 4 for S.a). Row id of tuple i: row_base + i, or the u32 at row_off when
  * row_off != HJ3D_ROW_IMPLICIT (exchanged (key,row) pairs on multi-GPU). Row ids are the
- * identity of tuples: they are what the reference's tuple pointers become. */
+ * identity of tuples: they are what the reference's tuple pointers become. The chain orders the
+ * counters follow are derived from row order, so a build relation's explicit row ids must ascend in
+ * its scan order (the reference's insertion order), as received pairs do: the exchange keeps each
+ * source's pairs in row order and concatenates the sources in rank order. */
 typedef struct {
   const void* base;
   uint64_t n;
@@ -203,9 +206,16 @@ enum {
   /* HJ3D_OPT_RP_UNFUSED (0/1, default 0): small implicit-row build partitions run as two launches
    * (histogram, then scatter) instead of the fused one-launch partition with its grid barrier
    * (A/B measurements and the parity test of both forms). The fused form runs only when the
-   * occupancy API confirms all its workgroups are resident; should a barrier still not complete
-   * within 0.2 s, the next hj3d_probe_result / hj3d_probe2_result returns HJ3D_EDEVICE. */
-  HJ3D_OPT_RP_UNFUSED = 15
+   * occupancy API confirms all its workgroups are resident (another stream holding CUs can still
+   * delay some); should a barrier not complete within 0.2 s, its workgroups go on with partial
+   * partition sizes and the table is invalid: hj3d_table_stats / _size / _export / _finish of that
+   * table and the next hj3d_probe_result / hj3d_probe2_result return HJ3D_EDEVICE. A rebuild of the
+   * table replaces it. */
+  HJ3D_OPT_RP_UNFUSED = 15,
+  /* HJ3D_OPT_DIAG_GBAR (ticks of the 100 MHz clock, default 0 = off): diagnostic for the failure path
+   * above. The fused partition's barrier then times out after this many ticks, and its workgroup 0
+   * never arrives, so every barrier of such a build times out (tests). */
+  HJ3D_OPT_DIAG_GBAR = 16
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Timing events for a host's own phase timers (the bench's build / probe boundaries): HIP events

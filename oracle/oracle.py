@@ -188,12 +188,14 @@ def nested_plan(build, bkey, probe, pkey, nb, unnest, agg=True, min_ms=0.0, min_
     return _plan(lib().orc_nested_plan, build, bkey, probe, pkey, nb, unnest, agg, min_ms, min_reps, brow, prow)
 
 
-def exp4_plan(R, S, T, nb, nested, agg=True, min_ms=0.0, min_reps=1) -> dict:
-    """Experiment-4 Ndu (nested=True) / Chj (nested=False); R/S/T are (n,2) {k,a} arrays."""
+def exp4_plan(R, S, T, nb, nested, agg=True, min_ms=0.0, min_reps=1, keys=(0, 1, 1), rows=(None, None, None)) -> dict:
+    """Experiment-4 Ndu (nested=True) / Chj (nested=False); R/S/T are (n,2) {k,a} arrays (keys: the key
+    word of R, S, T; rows: their explicit row-id words, None = row index; e.g. received (key, row)
+    pairs on a rank of the multi-GPU strand: keys (0, 0, 0), rows (1, 1, 1))."""
     R = np.ascontiguousarray(R, dtype=np.uint32)
     S = np.ascontiguousarray(S, dtype=np.uint32)
     T = np.ascontiguousarray(T, dtype=np.uint32)
-    rr, rs, rt = _rel(R, 0), _rel(S, 1), _rel(T, 1)
+    rr, rs, rt = _rel(R, keys[0], rows[0]), _rel(S, keys[1], rows[1]), _rel(T, keys[2], rows[2])
     res = _Exp4Res()
     rc = lib().orc_exp4_plan(C.byref(rr), C.byref(rs), C.byref(rt), nb, int(nested), int(agg), float(min_ms),
                              int(min_reps), C.byref(res))

@@ -230,3 +230,79 @@ def test_exchange_refusal_is_collective():
         p.join(timeout=60)
         assert p.exitcode == 0
     assert res == {0: ("peer short", 20), 1: ("short", 20)}
+
+
+EXP4_KEYS = ("c_probe_rs", "c_probe_rs_cmp", "c_probe_rt", "c_probe_rt_cmp", "c_unnest_1", "c_unnest_2", "c_top")
+
+
+def _exp4_worker(rank, port, q):
+    """Experiment 4 on the multi-GPU strand's layout (hj3d.dist.exp4_join's steps, the join done by the
+    oracle): R, S, T co-partitioned by bucket range of the one FK hash, all counts in one collective,
+    three pair all-to-alls, the rank's Ndu / Chj over its received pairs, counters all-reduced."""
+    import json
+    import torch
+    import torch.distributed as dist
+    from hj3d import dist as hdist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "exp4_R16_a3_A4_b2_B2.json")))
+        log2R, a, A, b, B = g["generator_args"][1:6]
+        Sa, Ta = O.gen_exp4(log2R, a, A, b, B)
+        nb, cardR = g["nb"], 1 << log2R
+        keys = [np.arange(cardR, dtype=np.uint32), Sa, Ta]
+        send, cnts = [], []
+        for k in range(3):
+            n = len(keys[k])
+            lo, hi = rank * n // WORLD, (rank + 1) * n // WORLD
+            pairs, counts = partition(keys[k][lo:hi], np.arange(lo, hi, dtype=np.uint32), nb, WORLD)
+            send.append(pairs)
+            cnts.append(counts)
+        sc, rc = hdist.exchange_counts(torch.from_numpy(np.stack(cnts)))
+        recv = []
+        for k in range(3):
+            rbuf = torch.empty((max(sum(rc[k]), 1), 2), dtype=torch.int32)
+            got, work = hdist.exchange_pairs_async(torch.from_numpy(send[k].view(np.int32)), sc[k], rc[k], rbuf)
+            assert work is None or work.wait()
+            recv.append(got.numpy().view(np.uint32))
+        out = {}
+        for plan in ("Ndu", "Chj"):
+            e = O.exp4_plan(recv[0], recv[1], recv[2], nb, plan == "Ndu", keys=(0, 0, 0), rows=(1, 1, 1))
+            sums = [e.get(k, 0) for k in EXP4_KEYS] + [e["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h")]
+            out[plan] = (hdist.allreduce_sum_u64(sums, "cpu"), hdist.allreduce_xor_u64(e["out"]["xor_h"], "cpu"),
+                         [len(r) for r in recv])
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exp4_co_partitioned_world2():
+    """Experiment 4 (Ndu and Chj) split over two ranks by bucket range of the FK hash equals the
+    reference binary's fixture exp4_R16_a3_A4_b2_B2: every probe / comparison / unnest counter, c_top
+    and the output checksums, after the all-reduce."""
+    import json
+    import torch.multiprocessing as mp
+
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "exp4_R16_a3_A4_b2_B2.json")))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_exp4_worker, args=(r, port, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(WORLD))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for plan in ("Ndu", "Chj"):
+        ref = g["plans"][plan]
+        tot, x, _ = res[0][plan]
+        assert (tot, x) == res[1][plan][:2], plan
+        want = [ref["c_probe_RS"], ref["c_probe_RS_cmp"], ref["c_probe_RT"], ref["c_probe_RT_cmp"],
+                ref.get("c_unnest_1", 0), ref.get("c_unnest_2", 0), ref["c_top"]]
+        assert tot[:7] == want, (plan, tot[:7], want)  # (Chj has no unnest operators: 0, 0)
+        assert tot[7:] == [ref["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h")] and x == ref["out"]["xor_h"], plan
+        # both ranks own a share of every relation
+        assert min(res[0][plan][2] + res[1][plan][2]) > 0

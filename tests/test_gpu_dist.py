@@ -235,3 +235,97 @@ def test_rccl_exchange_large_message(ctx, comm):
     assert got.shape[0] == n and torch.equal(got, send)
     del send, recv, got
     torch.cuda.empty_cache()
+
+
+def _exp4_fixture():
+    import json
+    return json.load(open(os.path.join(ROOT, "tests", "golden", "exp4_R16_a3_A4_b2_B2.json")))
+
+
+def _exp4_check(plan, got, ref):
+    for k in ("c_probe_RS", "c_probe_RS_cmp", "c_probe_RT", "c_probe_RT_cmp", "c_top"):
+        assert got[k.lower()] == ref[k], (plan, k, got[k.lower()], ref[k])
+    if plan == "Ndu":
+        assert (got["c_unnest_1"], got["c_unnest_2"]) == (ref["c_unnest_1"], ref["c_unnest_2"])
+    assert {k: got[k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")} == \
+           {k: ref["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")}, plan
+
+
+@pytest.mark.parametrize("plan", ["Ndu", "Chj"])
+def test_rccl_exp4_strand_equals_reference(ctx, comm, plan):
+    """Experiment 4 on the multi-GPU strand (hj3d.dist.exp4_join) with the exchange on libhj3d's RCCL
+    communicator at world size 1: R, S, T co-partitioned, counts in one collective, three
+    asynchronous pair exchanges, one hj3d_build_many, hj3d_probe2, counters all-reduced; equal to the
+    reference binary's fixture exp4_R16_a3_A4_b2_B2."""
+    import torch.distributed as dist
+    import hj3d
+    from hj3d import dist as hdist
+    g = _exp4_fixture()
+    R, S, T = hj3d.exp4_relations_ref(*g["generator_args"][1:6])
+    own_group = not dist.is_initialized()
+    if own_group:  # exp4_join reads rank / world from torch.distributed (gloo, this process alone)
+        import socket
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    hdist.use_comm(comm)
+    try:
+        got = hdist.exp4_join(ctx, plan, R, S, T, g["nb"])
+    finally:
+        hdist.use_comm(None)
+        if own_group:
+            dist.destroy_process_group()
+    _exp4_check(plan, got, g["plans"][plan])
+
+
+def _exp4_rank(rank, port, q):
+    import torch
+    import torch.distributed as dist
+    import hj3d
+    from hj3d import dist as hdist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=2)
+    try:
+        ctx = hj3d.Context(0)
+        g = _exp4_fixture()
+        R, S, T = hj3d.exp4_relations_ref(*g["generator_args"][1:6])
+        sl = []
+        for x in (R, S, T):
+            lo, hi = rank * x.shape[0] // 2, (rank + 1) * x.shape[0] // 2
+            sl.append((x[lo:hi].contiguous(), lo))
+        out = {}
+        for plan in ("Ndu", "Chj"):
+            got = hdist.exp4_join(ctx, plan, sl[0][0], sl[1][0], sl[2][0], g["nb"], row_base=tuple(b for _, b in sl))
+            out[plan] = {k: v for k, v in got.items()}
+        torch.cuda.synchronize()
+        ctx.close()
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_exp4_two_rank_rehearsal_equals_reference():
+    """hj3d.dist.exp4_join with two ranks on this one GPU (gloo, the exchange staged through host
+    memory; RCCL allows one rank per device): each rank holds half of R, S and T, and both ranks'
+    all-reduced results equal the reference binary's fixture."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    procs = [mpc.Process(target=_exp4_rank, args=(r, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    g = _exp4_fixture()
+    for plan in ("Ndu", "Chj"):
+        assert res[0][plan]["per_rank"]["probe_tuples"] > 0 and res[1][plan]["per_rank"]["probe_tuples"] > 0
+        for r in (0, 1):
+            _exp4_check(plan, res[r][plan], g["plans"][plan])

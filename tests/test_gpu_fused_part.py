@@ -116,3 +116,46 @@ def test_timing_events_measure_the_stream(ctx):
     assert 0 < b < a and a + b <= total * 1.05 + 0.05, (a, b, total)
     assert a + b >= 0.5 * total, (a, b, total)
     t.close()
+
+
+def test_fused_partition_barrier_timeout_is_reported(ctx):
+    """The fused partition's failure path (HJ3D_OPT_DIAG_GBAR: its grid barrier cannot complete, every
+    workgroup times out after 1 ms and goes on with partial sizes): the table's statistics, size,
+    export and finish, and the next probe result, return HJ3D_EDEVICE; the context's arrival counter
+    stays in step, so the next build on the same context is exact again and reads clean."""
+    import hj3d
+    rng = np.random.default_rng(11)
+    n = 3_000_000
+    B = O.tuples3(rng.permutation(n).astype(np.uint32), np.zeros(n, np.uint32))
+    P = O.tuples3(np.arange(n // 2, dtype=np.uint32), rng.integers(0, n, n // 2).astype(np.uint32))
+    e = O.chain_plan(B, 0, P, 1, n, True)
+    dB, dP = dev(B), dev(P)
+    t = hj3d.Table(ctx, hj3d.HJ3D_CHAIN, n)
+    ctx.diag_gbar(100_000)  # 1 ms
+    try:
+        t.build(hj3d.Rel(dB, 0))
+    finally:
+        ctx.diag_gbar(0)
+    assert t.build_path(finish=False) == "radix", t.build_path(finish=False)
+    import ctypes as C
+    lib = hj3d.lib()
+    npay, nsub = C.c_uint64(), C.c_uint64()
+    for what, call in (("stats", t.stats), ("finish", t.finish),
+                       ("size", lambda: ctx._check(lib.hj3d_table_size(ctx.h, t.h, None, None), "size")),
+                       ("export", lambda: ctx._check(lib.hj3d_table_export(ctx.h, t.h, None, None, None, C.byref(npay),
+                                                                           C.byref(nsub)), "export"))):
+        with pytest.raises(hj3d.Hj3dError) as ei:
+            call()
+        assert ei.value.status == hj3d.HJ3D_EDEVICE, what
+        assert "barrier" in str(ei.value), what
+    with pytest.raises(hj3d.Hj3dError) as ei:
+        ctx.probe(t, hj3d.Rel(dP, 1), unique=True)
+    assert ei.value.status == hj3d.HJ3D_EDEVICE
+    # a rebuild on the same context (and the same table) is exact and reads clean
+    for _ in range(3):
+        t.build(hj3d.Rel(dB, 0))
+        r = ctx.probe(t, hj3d.Rel(dP, 1), unique=True)
+        assert (r.n_out, r.n_cmps, r.sum_h, r.xor_h) == (e.c_probe, e.c_cmp, e.out["sum_h"], e.out["xor_h"])
+        st = t.stats()
+        assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
+    t.close()

@@ -249,6 +249,35 @@ def test_exp4_plans_bit_exact(ctx, name, g, path):
         ctx.radix_min(1 << 20)
 
 
+@pytest.mark.parametrize("parts", [2, 3, 8])
+@pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
+def test_exp4_owner_split_equals_reference(ctx, name, g, parts):
+    """Experiment 4 co-partitioned by bucket range of the FK hash (R, S and T) and run
+    owner after owner on this GPU (hj3d.exp4_plan_sharded: per owner one hj3d_build_many of its S and
+    T pairs, explicit global rows, and hj3d_probe2 with its R pairs): the summed counters and
+    checksums equal the reference binary's fixture, Ndu and Chj. The multi-GPU strand's per-rank
+    compute without the exchange (unmeasured on hardware at N > 1)."""
+    import hj3d
+    log2R, a, A, b, B = g["generator_args"][1:6]
+    Sa, Ta = O.gen_exp4(log2R, a, A, b, B)
+    n, cardR = len(Sa), 1 << log2R
+    R = dev(O.tuples2(np.arange(cardR, dtype=np.uint32), np.zeros(cardR, np.uint32)))
+    S = dev(O.tuples2(np.arange(n, dtype=np.uint32), Sa))
+    T = dev(O.tuples2(np.arange(n, dtype=np.uint32), Ta))
+    for plan in ("Ndu", "Chj"):
+        got = hj3d.exp4_plan_sharded(ctx, plan, R, S, T, g["nb"], parts)
+        _exp4_compare(plan, got, g["plans"][plan])
+
+
+def _exp4_compare(plan, got, ref):
+    for k in ("c_probe_RS", "c_probe_RS_cmp", "c_probe_RT", "c_probe_RT_cmp", "c_top"):
+        assert got[k.lower()] == ref[k], (plan, k, got[k.lower()], ref[k])
+    if plan == "Ndu":
+        assert got["c_unnest_1"] == ref["c_unnest_1"] and got["c_unnest_2"] == ref["c_unnest_2"]
+    assert {k: got[k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")} == \
+           {k: ref["out"][k] for k in ("sum_a", "sum_b", "sum_c", "sum_h", "xor_h")}, plan
+
+
 def _exp4_check(ctx, g, R, S, T):
     """Both plans, with the two builds as one hj3d_build_many call (one launch sequence for the two
     nested tables) and as two hj3d_build calls."""
@@ -548,6 +577,43 @@ def test_build_many_one_table_gives_up(ctx, dense, sync):
         ctx.timing(False)
         ctx.sync_build(False)
         ctx.radix_min(1 << 20)
+
+
+@pytest.mark.parametrize("explicit", [1, 0], ids=["r1_explicit", "r0_explicit"])
+def test_build_many_mixed_row_modes(ctx, explicit):
+    """hj3d_build_many partitions both relations in one pass. With one relation on implicit rows and
+    the other on explicit row ids, large enough for the whole-segment scatter (k_rp_wscatter, >= 4
+    tiles of 16384 per workgroup), both tables must carry their own rows: counters, output checksums
+    and statistics equal the oracle's per table (explicit rows: ascending, with gaps, over a wide range)."""
+    import hj3d
+    rng = np.random.default_rng(41 + explicit)
+    nb, n = 2_000_003, 9_000_000
+    rels, brow = [], []
+    for k in range(2):
+        r = np.zeros((n, 3), np.uint32)
+        r[:, 1] = rng.integers(0, 2_500_000, n, dtype=np.uint32)
+        if k == explicit:
+            # (ascending in scan order, as the ABI requires of explicit build rows: the reference's
+            # insertion order)
+            r[:, 2] = np.sort(rng.choice(1_000_000_000, n, replace=False)).astype(np.uint32)
+        rels.append(r)
+        brow.append(2 if k == explicit else None)
+    P = O.tuples3(rng.integers(0, 2_500_000, 1_500_000, dtype=np.uint32), np.zeros(1_500_000, np.uint32))
+    exp = [O.nested_plan(rels[k], 1, P, 0, nb, True, brow=brow[k]) for k in range(2)]
+    ts = [hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb) for _ in range(2)]
+    dr = [dev(r) for r in rels]
+    ctx.build_many(ts, [hj3d.Rel(dr[k], 1, row_word=brow[k]) for k in range(2)])
+    dP = dev(P)
+    for k in range(2):
+        assert ts[k].build_path() == "nested_agg", ts[k].build_path()
+        got = ctx.probe(ts[k], hj3d.Rel(dP, 0), unnest=True)
+        e = exp[k]
+        assert (got.n_matched, got.n_cmps, got.n_out) == (e.c_probe, e.c_cmp, e.c_unnest), k
+        assert {f: getattr(got, f) for f in ("sum_a", "sum_b", "sum_h", "xor_h")} == \
+            {f: e.out[f] for f in ("sum_a", "sum_b", "sum_h", "xor_h")}, k
+        assert {f: ts[k].stats()[f] for f in STAT_KEYS} == {f: e.stats[f] for f in STAT_KEYS}, k
+    for t in ts:
+        t.close()
 
 
 @pytest.mark.parametrize("keys_per_bucket", [1, 4])
