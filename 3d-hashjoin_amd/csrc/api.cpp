@@ -200,7 +200,6 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       return HJ3D_OK;
     case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_PK: ctx->nested_pk = value != 0; return HJ3D_OK;
-    case HJ3D_OPT_PK_COMPACT: ctx->pk_compact = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SYNC_BUILD: ctx->sync_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_2L: ctx->nested_2l = value != 0; return HJ3D_OK;
     case HJ3D_OPT_RP_UNFUSED: ctx->rp_unfused = value != 0; return HJ3D_OK;
@@ -443,9 +442,6 @@ static hipError_t build_one(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build)
   hipError_t e;
   t->pending = false;  // a build in flight for the old content is replaced (its copy stays stream-ordered)
   t->gbar_tag = 0;     // (set again by a fused build partition)
-  // the build's row range (implicit rows: row_base + [0, n)); explicit rows: unknown
-  t->row_lo = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base < (1ull << 32) ? uint32_t(build->row_base) : 0u;
-  t->row_rr = build->row_off == HJ3D_ROW_IMPLICIT && build->row_base + build->n <= (1ull << 32) ? build->n : 0u;
   if (t->desc.kind == HJ3D_CHAIN) {
     bool sorted = false;
     t->path = "radix";

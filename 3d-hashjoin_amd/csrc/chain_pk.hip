@@ -28,57 +28,18 @@ namespace hj3d {
 namespace {
 
 constexpr int kPkBlock = 1024;
-// build-time tunables (A/B variants, scripts/gpu_variant_sweep.sh)
-#ifndef HJ3D_PK_ROUNDS
-#define HJ3D_PK_ROUNDS 8  // tuples per thread and tile: 8192-tuple tiles
-#endif
-#ifndef HJ3D_PK_AHEAD
-#define HJ3D_PK_AHEAD 1   // tiles of keys in flight: 1 (loaded after the stage is built) or 2
-#endif
-#ifndef HJ3D_PK_FLAT
-#define HJ3D_PK_FLAT 0    // probe: walk each wave's regions as one stream always (1; measured slower at config B) or only short ones
-#endif
-#ifndef HJ3D_PK_NTREG
-#define HJ3D_PK_NTREG 1   // partition: region segments stored non-temporal (0: plain; nt 0.452 -> 0.447 ms, and the probe reading them 0.493 -> 0.489)
-#endif
-#ifndef HJ3D_PK_ST32
-#define HJ3D_PK_ST32 0    // partition: region pairs stored as two 4-B stores (A/B)
-#endif
-#ifndef HJ3D_PK_NTLOAD
-#define HJ3D_PK_NTLOAD 1  // partition: probe keys loaded non-temporal (0: plain; nt 0.447 -> 0.436 ms, probe phase -2 %)
-#endif
-#ifndef HJ3D_PK_DIAG
-#define HJ3D_PK_DIAG 0    // diagnostic variants (results wrong): 1 partitioner without region stores, 2 probe without LDS lookups, 3 probe without staging the slice, 4 probe without the first walk position's entry read
-#endif
-#ifndef HJ3D_PK_SINK
-#define HJ3D_PK_SINK 0    // probe: absent items store to a sink (fixed store count per chunk)
-#endif
-#ifndef HJ3D_PK_FEWBAR
-#define HJ3D_PK_FEWBAR 1  // partition: five barriers per tile instead of seven (0: A/B variant)
-#endif
-#ifndef HJ3D_PK_GUARD
-#define HJ3D_PK_GUARD 1   // partition: key loads and rank atomics guarded per tuple (else clamped, unconditional)
-#endif
-constexpr int kPkRounds = HJ3D_PK_ROUNDS;
-#ifndef HJ3D_PK_SEG
-#define HJ3D_PK_SEG 16    // pairs per region segment (16: 128 B)
-#endif
-#ifndef HJ3D_PK_STAGE
-#define HJ3D_PK_STAGE 17408  // LDS stage (pairs): the tile + the carried pairs (< SEG per slice)
-#endif
+// Tunables, fixed by the sweeps recorded in DESIGN.md 4.1 (the losing variants are gone from the
+// source): 8192-tuple tiles (4096: 0.556 ms, 8192: 0.466 ms for k_pk_part at config B), the next tile's
+// keys loaded once the stage is built (two tiles ahead spilled), 128-B region segments (64-B: slower in
+// both kernels), non-temporal key loads (0.447 -> 0.436 ms) and region stores (0.452 -> 0.447 ms),
+// five barriers per tile, guarded key loads and rank atomics (the clamped form was not faster).
+constexpr int kPkRounds = 8;
 constexpr int kPkTile = kPkBlock * kPkRounds;
 constexpr int kPkTBits = 32 - __builtin_clz(uint32_t(kPkTile - 1));  // bits of a rank inside the tile
-constexpr uint32_t kPkSeg = HJ3D_PK_SEG;
-static_assert(kPkSeg == 8 || kPkSeg == 16, "64- or 128-B segments");
-constexpr uint32_t kPkStage = kPkTile + (kPkSeg - 1) * 1024 > HJ3D_PK_STAGE ? HJ3D_PK_STAGE : kPkTile + (kPkSeg - 1) * 1024;
+constexpr uint32_t kPkSeg = 16;                                     // pairs per region segment (128 B)
+constexpr uint32_t kPkStage = 17408;  // LDS stage (pairs): the tile + the carried pairs (< kPkSeg per slice)
 static_assert(kPkTile <= kPkStage && kPkStage < 65536, "the tile alone fits the stage; stage offsets in 16 bits");
 constexpr uint32_t kSortedMaxPk = 32;
-#ifndef HJ3D_PK_SWZ
-#define HJ3D_PK_SWZ 0  // partition: stage[] slots XOR-swizzled (i ^ (i >> 5) & 31) against the ~16-pair stride of per-slice runs (A/B)
-#endif
-// stage slot of pair i of k_pk_part's stage: a bijection inside each 32-pair (256-B) block, so the
-// per-thread run accesses (thread me at its run start, runs ~16 pairs apart) spread over the banks
-__device__ __forceinline__ uint32_t pk_sw(uint32_t i) { return HJ3D_PK_SWZ ? i ^ ((i >> 5) & 31u) : i; }
 constexpr uint32_t kOvfFlag = 0x80000000u;
 
 // control words (u64) of one probe strand
@@ -102,10 +63,9 @@ __device__ __forceinline__ void pk_ovf_append(bool me, uint2 e, uint2* __restric
 // Regions: region[(g * P + p) * cap + k], counts[g * P + p] pairs. One slice per thread (P <= 1024):
 // thread p carries slice p's < 16 leftover pairs in registers. SEL: a one-word selection fused in.
 // Memory ordering: vmcnt counts loads and stores together, in issue order, so a load can only be
-// waited for together with every older store. The keys of tile t+2 are therefore loaded (always,
-// clamped at the end: a fixed number of loads) right after tile t's stage is built; by default the
-// next tile's (HJ3D_PK_AHEAD = 1), with HJ3D_PK_AHEAD = 2 tile t+2's, so that waiting for tile t+1's
-// keys waits for tile t-1's region stores, never for tile t's (measured slower: register spills).
+// waited for together with every older store. The next tile's keys are loaded right after this tile's
+// stage is built (loading two tiles ahead, so that the wait would never cover this tile's region
+// stores, spilled registers and measured slower).
 template <bool IMPLICIT, bool SEL>
 __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint32_t ntiles, uint32_t cap,
                                                       uint2* __restrict__ region, uint32_t* __restrict__ counts,
@@ -126,57 +86,25 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   uint32_t my_kc = 0, my_cur = 0, my_end = cap;
 #pragma unroll
   for (int j = 0; j < int(kPkSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
-  uint32_t ha[kPkRounds], hb[kPkRounds], pa[SEL ? kPkRounds : 1], pb[SEL ? kPkRounds : 1];
+  uint32_t ha[kPkRounds], pa[SEL ? kPkRounds : 1];
   // explicit rows: loaded with the key at tile prefetch and kept in registers (the row word shares
   // the key's line; loading it again after the ranking phase fetched that line twice: 15.4 B per
   // 8-B received pair, round 3).
-  uint32_t wa[IMPLICIT ? 1 : kPkRounds], wb[IMPLICIT ? 1 : kPkRounds];
-// {key, row} pairs: two 4-B loads issued back to back (the second hits the line the first brought
-// in) measured faster than one 8-B load: 1e8 received pairs, same box, 0.505 / 0.505 against 0.597 /
-// 0.593 ms (profiles/r04f_ab_pairs.log). 1: the 8-B form (A/B).
-#ifndef HJ3D_PK_PAIR8
-#define HJ3D_PK_PAIR8 0
-#endif
-  const bool pair8 = HJ3D_PK_PAIR8 && !IMPLICIT && r.stride == 8 && r.key_off == 0 && r.row_off == 4 &&
-                     (reinterpret_cast<uintptr_t>(r.base) & 7u) == 0;
-  // a wave-uniform 64-bit tile pointer + 32-bit lane offsets (the loads take the scalar-base form)
+  uint32_t wa[IMPLICIT ? 1 : kPkRounds];
+  // {key, row} pairs: two 4-B loads issued back to back (the second hits the line the first brought
+  // in) measured faster than one 8-B load: 1e8 received pairs, same box, 0.505 / 0.505 against
+  // 0.597 / 0.593 ms (profiles/r04f_ab_pairs.log).
   auto load = [&](uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
                   uint32_t (&rw)[IMPLICIT ? 1 : kPkRounds], uint32_t tile) __attribute__((always_inline)) {
-    if constexpr (HJ3D_PK_GUARD) {
-      const uint32_t base = tile * kPkTile;
+    const uint32_t base = tile * kPkTile;
 #pragma unroll
-      for (int j = 0; j < kPkRounds; ++j) {
-        const uint32_t i = base + uint32_t(j) * kPkBlock + me;
-        const char* t = r.base + uint64_t(i) * r.stride;
-        if constexpr (!IMPLICIT) {
-          if (pair8) {
-            const uint64_t* a8 = reinterpret_cast<const uint64_t*>(t);
-            const uint64_t kv = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(a8) : *a8) : 0ull;
-            h[j] = uint32_t(kv);
-            rw[j] = uint32_t(kv >> 32);
-          } else {
-            const uint32_t* ak = reinterpret_cast<const uint32_t*>(t + r.key_off);
-            const uint32_t* ar = reinterpret_cast<const uint32_t*>(t + r.row_off);
-            h[j] = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(ak) : *ak) : 0u;
-            rw[j] = i < n ? (HJ3D_PK_NTLOAD ? __builtin_nontemporal_load(ar) : *ar) : 0u;
-          }
-        } else if (HJ3D_PK_NTLOAD) {
-          h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
-        } else {
-          h[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + r.key_off) : 0u;
-        }
-        if constexpr (SEL) pw[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + sel.word_off) : 0u;
-      }
-    } else {
-      const uint32_t base = min(tile * kPkTile, n - 1), lim = n - 1 - base;
-      const char* tp = r.base + uint64_t(base) * r.stride;
-#pragma unroll
-      for (int j = 0; j < kPkRounds; ++j) {
-        const uint32_t o = min(uint32_t(j) * kPkBlock + me, lim) * r.stride;  // unconditional: clamped
-        h[j] = *reinterpret_cast<const uint32_t*>(tp + o + r.key_off);
-        if constexpr (!IMPLICIT) rw[j] = *reinterpret_cast<const uint32_t*>(tp + o + r.row_off);
-        if constexpr (SEL) pw[j] = *reinterpret_cast<const uint32_t*>(tp + o + sel.word_off);
-      }
+    for (int j = 0; j < kPkRounds; ++j) {
+      const uint32_t i = base + uint32_t(j) * kPkBlock + me;
+      const char* t = r.base + uint64_t(i) * r.stride;
+      h[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.key_off)) : 0u;
+      if constexpr (!IMPLICIT)
+        rw[j] = i < n ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(t + r.row_off)) : 0u;
+      if constexpr (SEL) pw[j] = i < n ? *reinterpret_cast<const uint32_t*>(t + sel.word_off) : 0u;
     }
   };
   auto to_ovf = [&](uint2 e, uint32_t p, bool me_) __attribute__((always_inline)) {  // packed pair of slice p -> {h, row}
@@ -217,13 +145,11 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   uint32_t npassed = 0;
   auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
                      uint32_t (&rw)[IMPLICIT ? 1 : kPkRounds]) __attribute__((always_inline)) {
-    // HJ3D_PK_FEWBAR: loc[me] is cleared right after its count is read (nothing touches it again
-    // in the tile) and no barrier ends the tile: the next tile's first LDS writes (stage, seginfo,
-    // sbase) come after its ranking barrier, which every thread reaches only when done reading
-    if (!HJ3D_PK_FEWBAR) loc[me] = 0;
+    // loc[me] is cleared right after its count is read (nothing touches it again in the tile) and no
+    // barrier ends the tile: the next tile's first LDS writes (stage, seginfo, sbase) come after its
+    // ranking barrier, which every thread reaches only when done reading
     const uint32_t base = tile * kPkTile;
     uint32_t rk[kPkRounds];
-    if (!HJ3D_PK_FEWBAR) __syncthreads();
     // hash, bucket, slice, rank: the LDS atomics are unconditional (invalid tuples add 0 to slot 0)
 #pragma unroll
     for (int j = 0; j < kPkRounds; ++j) {
@@ -237,23 +163,16 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
         npassed += pass;
       }
       const bool ok = pass && bl < pk.nbl;
-      if constexpr (HJ3D_PK_GUARD) {
-        rk[j] = kInvalid;
-        if (ok) {
-          const uint32_t p = pk.dw.div(bl);
-          h[j] = ((bl - p * pk.W) << pk.qbits) | q;  // the packed pair's first word
-          rk[j] = (p << kPkTBits) | atomicAdd(&loc[p], 1u);
-        }
-      } else {
-        const uint32_t p = ok ? pk.dw.div(bl) : 0u;
-        h[j] = ((bl - p * pk.W) << pk.qbits) | q;
-        const uint32_t rank = atomicAdd(&loc[p], ok ? 1u : 0u);
-        rk[j] = ok ? (p << kPkTBits) | rank : kInvalid;
+      rk[j] = kInvalid;
+      if (ok) {
+        const uint32_t p = pk.dw.div(bl);
+        h[j] = ((bl - p * pk.W) << pk.qbits) | q;  // the packed pair's first word
+        rk[j] = (p << kPkTBits) | atomicAdd(&loc[p], 1u);
       }
     }
     __syncthreads();
     const uint32_t my_c = me < P ? loc[me] : 0u;
-    if (HJ3D_PK_FEWBAR) loc[me] = 0;
+    loc[me] = 0;
     const auto seg_counts = [&]() __attribute__((always_inline)) {
       const uint32_t L = my_kc + my_c;
       return (L << 16) | (L / kPkSeg);
@@ -270,7 +189,7 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       sbase[me] = my_loc + my_kc;
 #pragma unroll
       for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_kc) stage[pk_sw(my_loc + j)] = creg[j];
+        if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
       for (uint32_t sg = 0; sg < my_len / kPkSeg; ++sg) {
         // segment-aligned (cap is a multiple of kPkSeg) unless a mid-stream flush moved the cursor:
         // a segment goes to the region only whole, else (all of it) to the overflow list
@@ -289,27 +208,18 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       uint32_t row;
       if constexpr (IMPLICIT) row = rb + li;
       else row = rw[j];
-      stage[pk_sw(sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1)))] = make_uint2(h[j], row);
+      stage[sbase[rk[j] >> kPkTBits] + (rk[j] & ((1u << kPkTBits) - 1))] = make_uint2(h[j], row);
     }
-    load(h, pw, rw, tile + HJ3D_PK_AHEAD * gridDim.x);  // the next tile(s) (clamped past the end)
+    load(h, pw, rw, tile + gridDim.x);  // the next tile (keys past the end load nothing)
     __syncthreads();
     // whole segments: kPkSeg consecutive lanes store one 128-B segment
     for (uint32_t kk = me; kk < nfull * kPkSeg; kk += kPkBlock) {
       const uint2 si = seginfo[kk / kPkSeg];
       const uint32_t j = kk % kPkSeg;
-      const uint2 e = stage[pk_sw(si.y + j)];
+      const uint2 e = stage[si.y + j];
       const bool spill = si.x & kOvfFlag;
-      if (!spill && HJ3D_PK_DIAG != 1) {
-        if (HJ3D_PK_ST32) {  // two 4-B stores (A/B)
-          uint32_t* w = reinterpret_cast<uint32_t*>(region + si.x + j);
-          __builtin_nontemporal_store(e.x, w);
-          __builtin_nontemporal_store(e.y, w + 1);
-        } else if (HJ3D_PK_NTREG) {
-          __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(region + si.x + j));
-        } else {
-          region[si.x + j] = e;
-        }
-      }
+      if (!spill)
+        __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(region + si.x + j));
       to_ovf(e, si.x & ~kOvfFlag, spill);
     }
     // the run's tail (< one segment) becomes the slice's carry
@@ -317,26 +227,15 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       const uint32_t F = my_len - my_len % kPkSeg;
 #pragma unroll
       for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_len - F) creg[j] = stage[pk_sw(my_loc + F + j)];
+        if (uint32_t(j) < my_len - F) creg[j] = stage[my_loc + F + j];
       my_cur += F;
       my_kc = my_len - F;
     }
-    if (!HJ3D_PK_FEWBAR) __syncthreads();
   };
-  if (HJ3D_PK_FEWBAR) {
-    loc[me] = 0;
-    __syncthreads();
-  }
+  loc[me] = 0;
+  __syncthreads();
   load(ha, pa, wa, blockIdx.x);
-  if constexpr (HJ3D_PK_AHEAD == 2) {
-    load(hb, pb, wb, blockIdx.x + gridDim.x);
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += 2 * gridDim.x) {
-      process(tile, ha, pa, wa);
-      if (tile + gridDim.x < ntiles) process(tile + gridDim.x, hb, pb, wb);
-    }
-  } else {
-    for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa, wa);
-  }
+  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa, wa);
   flush_carry();
   if (me < P) counts[blockIdx.x * P + me] = min(my_cur, my_end);
   // n_probe: every scanned tuple (the reference's probe count), or the selection's passing tuples
@@ -359,13 +258,9 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
 // rank by slice with a wave-level multi-split (one ballot per bit of c, one LDS atomic per slice and
 // wave), stage the tile slice-major in LDS, write each slice's run out with consecutive lanes on
 // consecutive pairs. Pairs past a fine region's capacity go to the overflow list as {h, row}.
-#ifndef HJ3D_SP_BLOCK
-#define HJ3D_SP_BLOCK 256  // k_pk_split workgroup size (several per CU; 1024: 4.21 ms, 512: 3.50, 256: 3.39 at config D)
-#endif
-#ifndef HJ3D_SP_PREFETCH
-#define HJ3D_SP_PREFETCH 1  // k_pk_split: the next tile's pairs loaded while this one is split (A/B)
-#endif
-constexpr int kSpBlock = HJ3D_SP_BLOCK;
+// workgroup size: several per CU (1024: 4.21 ms, 512: 3.50, 256: 3.39 at config D); the next tile's
+// pairs are loaded while this one is split (3.51 ms without)
+constexpr int kSpBlock = 256;
 constexpr int kSpRounds = 8;
 constexpr int kSpTile = kSpBlock * kSpRounds;
 constexpr uint32_t kSpMaxC = 64;
@@ -425,11 +320,11 @@ __global__ __launch_bounds__(kSpBlock) void k_pk_split(const uint2* __restrict__
     }
   };
   uint2 cv[kSpRounds];
-  if (HJ3D_SP_PREFETCH) load(cv, 0);
+  load(cv, 0);
   uint32_t par = 0;
   for (uint32_t t0 = 0; t0 < total; t0 += kSpTile, par ^= 1u) {
     uint2 nv[kSpRounds];
-    load(HJ3D_SP_PREFETCH ? nv : cv, HJ3D_SP_PREFETCH ? t0 + kSpTile : t0);
+    load(nv, t0 + kSpTile);
     uint32_t cc[kSpRounds], rk[kSpRounds];
 #pragma unroll
     for (int j = 0; j < kSpRounds; ++j) {
@@ -487,10 +382,8 @@ __global__ __launch_bounds__(kSpBlock) void k_pk_split(const uint2* __restrict__
       if (fit) reg2[d] = e;
       pk_ovf_append(!fit, make_uint2(pk.hash_of(e.x, pbase + c), e.y), ovf, ctl);
     }
-    if constexpr (HJ3D_SP_PREFETCH) {
 #pragma unroll
-      for (int j = 0; j < kSpRounds; ++j) cv[j] = nv[j];
-    }
+    for (int j = 0; j < kSpRounds; ++j) cv[j] = nv[j];
   }
   __syncthreads();
   if (me < C && pbase + me < pk.P) cnt2[uint64_t(s) * pk.P + pbase + me] = min(cur[me], cap2);
@@ -498,27 +391,11 @@ __global__ __launch_bounds__(kSpBlock) void k_pk_split(const uint2* __restrict__
 
 // ---- k_pk_probe ----
 constexpr uint32_t kLdsWords = kPkLdsWords;
-#ifndef HJ3D_PB_LD32
-#define HJ3D_PB_LD32 0  // packed pairs loaded as two 4-B loads instead of one 8-B load (A/B)
-#endif
-#ifndef HJ3D_PB_ST32
-#define HJ3D_PB_ST32 0  // output pairs stored as two 4-B stores instead of one 8-B store (A/B)
-#endif
-__device__ __forceinline__ void pair_st(uint2* p, uint32_t lo, uint32_t hi, bool split) {
-  if (split) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(p);
-    __builtin_nontemporal_store(lo, w);
-    __builtin_nontemporal_store(hi, w + 1);
-  } else {
-    __builtin_nontemporal_store((uint64_t(hi) << 32) | lo, reinterpret_cast<uint64_t*>(p));
-  }
+// packed pairs in and output pairs out as one non-temporal 8-B access each (two 4-B accesses: no gain)
+__device__ __forceinline__ void pair_st(uint2* p, uint32_t lo, uint32_t hi) {
+  __builtin_nontemporal_store((uint64_t(hi) << 32) | lo, reinterpret_cast<uint64_t*>(p));
 }
 __device__ __forceinline__ uint64_t pair_ld(const uint2* p) {
-  if (HJ3D_PB_LD32) {
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
-    const uint32_t lo = __builtin_nontemporal_load(w), hi = __builtin_nontemporal_load(w + 1);
-    return (uint64_t(hi) << 32) | lo;
-  }
   return __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
 }
 // K = pairs per lane and chunk (the next chunk in flight), chosen per probe from the expected
@@ -534,7 +411,7 @@ template <int K, int MODE, bool CK>
 __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t valid, uint64_t slot0,
                                                const uint32_t* ldir, const uint2* lent, const PkGeom& pk,
                                                uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
-                                               uint64_t out_cap, uint2* __restrict__ sink) {
+                                               uint64_t out_cap) {
   uint32_t nm = 0, sc = 0, nv = 0;
 #pragma unroll
   for (int g = 0; g < K; g += K) {
@@ -545,14 +422,14 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t 
       const bool ok = (valid >> (g + j)) & 1u;
       const uint32_t x = uint32_t(v[g + j]);
       q[j] = x & pk.qmask;
-      const uint32_t w = HJ3D_PK_DIAG == 2 ? 0u : ldir[ok ? x >> pk.qbits : 0u];
+      const uint32_t w = ldir[ok ? x >> pk.qbits : 0u];
       d[j] = ok ? w : 0u;
       match[j] = kInvalid;
       cmps[j] = d[j] & 0xFFFFu;
       live[j] = cmps[j] != 0 && cmps[j] <= kSortedMaxPk;
     }
 #pragma unroll
-    for (uint32_t c = HJ3D_PK_DIAG == 4 ? 1 : 0; c < 3; ++c) {
+    for (uint32_t c = 0; c < 3; ++c) {
 #pragma unroll
       for (int j = 0; j < K; ++j) {
         const uint32_t nn = d[j] & 0xFFFFu;
@@ -608,12 +485,7 @@ __device__ __forceinline__ void pk_probe_items(const uint64_t (&v)[K], uint32_t 
       sc += cmps[j];
       if (MODE == 1) {
         const uint64_t slot = slot0 + uint32_t((g + j) * 64);
-        if (HJ3D_PK_SINK) {  // every lane stores (absent items to the sink): a fixed number of stores per chunk
-          uint2* dst = (ok && slot < out_cap) ? out + slot : sink + (threadIdx.x & 63);
-          __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(dst));
-        } else if (ok && slot < out_cap) {
-          pair_st(out + slot, row, match[j], HJ3D_PB_ST32);
-        }
+        if (ok && slot < out_cap) pair_st(out + slot, row, match[j]);
       }
       if (CK && m) {
         acc[4] += row;
@@ -711,160 +583,17 @@ __device__ __forceinline__ void pk_stage(const uint32_t* __restrict__ off, const
   }
 }
 
-// ---- compact slice image (k_pk_probe with COMPACT, 512-thread workgroups, two per CU) ----
-// The directory keeps 16-bit entry starts (count = next start - start; a slice holds < 2^16
-// entries), the entries one word each: q * rr + (row - rlo), q = h / NB, which fits 32 bits when
-// q_max * rr < 2^32 (the host checks; b = 1 tables: rr = NB). An entry whose word would reach
-// 0xFFFFFFFF (q = q_max and a large row, ~0.1 % of entries) is stored as kWideEntry, which never
-// matches; a probe that ends without a match after seeing one redoes its bucket in HBM. The image
-// is ~6 B per bucket instead of 12, so two slices' workgroups share a CU (LDS 64 KB each): one
-// workgroup stages while the other walks.
-constexpr uint32_t kWideEntry = 0xFFFFFFFFu;
-constexpr uint32_t kLdsWordsC = 15872;  // 62 KB: the compact image of one slice
-__device__ __forceinline__ void pk_stage_c(const uint32_t* __restrict__ off, const uint2* __restrict__ ent, uint32_t b0,
-                                           uint32_t nbs, uint32_t e0, uint32_t ne, const PkGeom& pk,
-                                           uint16_t* ldir, uint32_t* lent, int block) {
-  constexpr int kStage = 12;
-  const uint32_t nmax = max(nbs + 1, ne);
-  for (uint32_t k0 = threadIdx.x; k0 < nmax; k0 += block * kStage) {
-    uint32_t a[kStage];
-    uint2 x[kStage];
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * block;
-      a[u] = k <= nbs ? off[b0 + k] : 0u;
-      x[u] = k < ne ? ent[e0 + k] : make_uint2(0, 0);
-    }
-#pragma unroll
-    for (int u = 0; u < kStage; ++u) {
-      const uint32_t k = k0 + u * block;
-      if (k <= nbs) ldir[k] = uint16_t(a[u] - e0);
-      if (k < ne) {
-        const uint64_t w = uint64_t(pk.dnb.div(x[u].x)) * pk.rr + (x[u].y - pk.rlo);
-        lent[k] = w >= kWideEntry ? kWideEntry : uint32_t(w);
-      }
-    }
-  }
-}
-
-// pk_probe_items on the compact image; `wide` gets the lanes whose bucket held a kWideEntry and
-// found no match (their item j: bit j), for the HBM redo.
 template <int K, int MODE, bool CK>
-__device__ __forceinline__ void pk_probe_items_c(const uint64_t (&v)[K], uint32_t valid, uint64_t slot0,
-                                                 const uint16_t* ldir, const uint32_t* lent, const PkGeom& pk,
-                                                 uint64_t (&acc)[kProbeFields], uint2* __restrict__ out,
-                                                 uint64_t out_cap, uint32_t& wide) {
-  uint32_t nm = 0, sc = 0;
-  uint32_t s[K], nn[K], match[K], cmps[K], base[K];
-  bool live[K], sawwide[K];
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const bool ok = (valid >> j) & 1u;
-    const uint32_t x = uint32_t(v[j]);
-    const uint32_t b = ok ? x >> pk.qbits : 0u;
-    s[j] = ldir[b];
-    nn[j] = ok ? uint32_t(ldir[b + 1]) - s[j] : 0u;
-    base[j] = (x & pk.qmask) * pk.rr;
-    match[j] = kInvalid;
-    cmps[j] = nn[j];
-    live[j] = nn[j] != 0 && nn[j] <= kSortedMaxPk;
-    sawwide[j] = false;
-  }
-#pragma unroll
-  for (uint32_t c = 0; c < 3; ++c) {
-#pragma unroll
-    for (int j = 0; j < K; ++j) {
-      const bool ok = live[j] && c < nn[j];
-      const uint32_t e = lent[ok ? s[j] + (c == 0 ? 0u : nn[j] - c) : 0u];
-      const bool hit = ok && e != kWideEntry && e - base[j] < pk.rr;
-      sawwide[j] = sawwide[j] || (ok && e == kWideEntry);
-      match[j] = hit ? e - base[j] + pk.rlo : match[j];
-      cmps[j] = hit ? c + 1 : cmps[j];
-      live[j] = live[j] && !hit;
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    if (live[j] && nn[j] > 3) {
-      for (uint32_t c = 3; c < nn[j]; ++c) {
-        const uint32_t e = lent[s[j] + nn[j] - c];
-        sawwide[j] = sawwide[j] || e == kWideEntry;
-        if (e != kWideEntry && e - base[j] < pk.rr) {
-          cmps[j] = c + 1;
-          match[j] = e - base[j] + pk.rlo;
-          break;
-        }
-      }
-    } else if (nn[j] > kSortedMaxPk) {  // long bucket in arrival order: order-free form
-      uint32_t minrow = kInvalid, lo_m = kInvalid, hi_m = 0, cnt = 0;
-      for (uint32_t k = s[j]; k < s[j] + nn[j]; ++k) {
-        const uint32_t e = lent[k];
-        if (e == kWideEntry) {
-          sawwide[j] = true;
-          continue;
-        }
-        const uint32_t row = e % pk.rr + pk.rlo;  // rare path: a division
-        minrow = min(minrow, row);
-        if (e - base[j] < pk.rr) {
-          ++cnt;
-          lo_m = min(lo_m, row);
-          hi_m = max(hi_m, row);
-        }
-      }
-      if (sawwide[j]) {
-        // the order-free form needs every row of the bucket: redo it in HBM
-      } else if (cnt != 0 && lo_m == minrow) {
-        cmps[j] = 1;
-        match[j] = lo_m;
-      } else if (cnt != 0) {
-        uint32_t gt = 0;
-        for (uint32_t k = s[j]; k < s[j] + nn[j]; ++k) gt += lent[k] % pk.rr + pk.rlo > hi_m;
-        cmps[j] = 2 + gt;
-        match[j] = hi_m;
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < K; ++j) {
-    const bool ok = (valid >> j) & 1u;
-    // a bucket with a wide entry and no match in LDS (or a long one with any wide entry): the whole
-    // item is redone against the table in HBM (counters and output there)
-    const bool redo = ok && sawwide[j] && (match[j] == kInvalid || nn[j] > kSortedMaxPk);
-    wide |= uint32_t(redo) << j;
-    if (redo) continue;
-    const uint32_t row = uint32_t(v[j] >> 32);
-    const bool m = match[j] != kInvalid;
-    nm += m;
-    sc += ok ? cmps[j] : 0u;
-    if (MODE == 1) {
-      const uint64_t slot = slot0 + uint32_t(j * 64);
-      if (ok && slot < out_cap)
-        __builtin_nontemporal_store((uint64_t(match[j]) << 32) | row, reinterpret_cast<uint64_t*>(out + slot));
-    }
-    if (CK && m) {
-      acc[4] += row;
-      acc[5] += match[j];
-      const uint64_t ph = pair_hash(row, match[j]);
-      acc[7] += ph;
-      acc[8] ^= ph;
-    }
-  }
-  acc[1] += nm;
-  acc[2] += nm;
-  acc[3] += sc;
-}
-
-template <int K, int MODE, bool CK, int BLOCK = kPkBlock, bool COMPACT = false>
-__global__ __launch_bounds__(BLOCK) void k_pk_probe(const uint2* __restrict__ region,
+__global__ __launch_bounds__(kPkBlock) void k_pk_probe(const uint2* __restrict__ region,
                                                        const uint32_t* __restrict__ counts, uint32_t G, uint32_t cap,
                                                        uint32_t splits, bool flat, const uint32_t* __restrict__ off,
                                                        const uint2* __restrict__ ent, PkGeom pk, FastMod fm,
                                                        uint2* __restrict__ out, uint64_t out_cap,
                                                        const uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
                                                        uint64_t* __restrict__ partials, uint64_t* __restrict__ res,
-                                                       int accumulate, uint2* __restrict__ sink) {
-  static_assert(COMPACT || BLOCK == kPkBlock, "the full image is staged by 1024 threads");
-  __shared__ uint32_t lds[COMPACT ? kLdsWordsC : kLdsWords];
+                                                       int accumulate) {
+  constexpr int BLOCK = kPkBlock;
+  __shared__ uint32_t lds[kLdsWords];
   __shared__ uint32_t wtot[BLOCK / kWave];
   __shared__ uint32_t rpre[BLOCK / kWave][65];
   __shared__ uint64_t bbase;
@@ -877,13 +606,9 @@ __global__ __launch_bounds__(BLOCK) void k_pk_probe(const uint2* __restrict__ re
   const uint32_t b0 = p * pk.W;
   const uint32_t nbs = min(pk.W, pk.nbl - b0);
   const uint32_t e0 = off[b0], e1 = off[b0 + nbs], ne = e1 - e0;
-  // compact: 16-bit starts (nbs + 1 of them), then one word per entry
-  const uint32_t dirw = (nbs + 2) / 2 + 1;
-  const bool fits = COMPACT ? uint64_t(dirw) + ne <= kLdsWordsC : (nbs + 2) + 2ull * ne <= kLdsWords;
+  const bool fits = (nbs + 2) + 2ull * ne <= kLdsWords;
   uint32_t* ldir = lds;
   uint2* lent = reinterpret_cast<uint2*>(lds + ((nbs + 2) & ~1u));
-  uint16_t* ldir16 = reinterpret_cast<uint16_t*>(lds);
-  uint32_t* lent32 = lds + dirw;
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
 
   // this block's regions: wave w takes g = g_lo + w + 16 k (lane k holds region k's count)
@@ -909,9 +634,9 @@ __global__ __launch_bounds__(BLOCK) void k_pk_probe(const uint2* __restrict__ re
   auto src_of = [&](uint32_t k) __attribute__((always_inline)) { return region + (g_lo + wid + kWaves * k) * P * cap + p * cap; };
 
   // one chunk = K x 64 consecutive items of the wave's stream (flat: regions concatenated;
-  // otherwise a chunk stays inside one region). Loads and stores of the steady-state loops are
-  // unconditional (clamped addresses, absent items stored to the sink): with a fixed count per chunk
-  // the wait for the next chunk's pairs leaves this chunk's stores in flight.
+  // otherwise a chunk stays inside one region). Loads of the steady-state loops are unconditional
+  // (clamped addresses). (Stores of absent items to a sink, for a fixed store count per chunk, were
+  // tried and not kept.)
   // flat: each lane keeps its own cursor, region cr holding stream positions [its start, nst), and
   // steps it forward (positions only grow, the region starts come from rpre): a compare per item
   const auto src_off = [&](uint32_t k) __attribute__((always_inline)) {
@@ -1000,33 +725,9 @@ __global__ __launch_bounds__(BLOCK) void k_pk_probe(const uint2* __restrict__ re
     }
   };
   if (fits) {
-    walk([&]() __attribute__((always_inline)) {
-           if constexpr (COMPACT) {
-             pk_stage_c(off, ent, b0, nbs, e0, ne, pk, ldir16, lent32, BLOCK);
-           } else if (HJ3D_PK_DIAG == 3) {  // no staging: an empty directory (every probe misses)
-             for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) ldir[k] = 0;
-           } else {
-             pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent);
-           }
-         },
+    walk([&]() __attribute__((always_inline)) { pk_stage(off, ent, b0, nbs, e0, ne, pk.dnb, ldir, lent); },
          [&](const uint64_t (&v)[K], uint32_t valid, uint32_t srel) __attribute__((always_inline)) {
-           if constexpr (COMPACT) {
-             uint32_t wide = 0;
-             pk_probe_items_c<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir16, lent32, pk, acc, out, out_cap, wide);
-             if (wide) {  // buckets with an entry too wide for the compact image: redo in HBM
-               const uint64_t slot0 = bbase + wpre + srel;
-#pragma unroll
-               for (int j = 0; j < K; ++j) {
-                 if (!((wide >> j) & 1u)) continue;
-                 const uint32_t x = uint32_t(v[j]), bl = b0 + (x >> pk.qbits);
-                 const uint32_t st = off[bl];
-                 pk_probe_hbm<MODE, CK>(pk.hash_of(x, p), uint32_t(v[j] >> 32), st, off[bl + 1] - st, ent,
-                                        slot0 + j * 64, acc, out, out_cap);
-               }
-             }
-           } else {
-             pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap, sink);
-           }
+           pk_probe_items<K, MODE, CK>(v, valid, bbase + wpre + srel, ldir, lent, pk, acc, out, out_cap);
          });
   } else {
     walk([&]() __attribute__((always_inline)) {},
@@ -1293,9 +994,6 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_build(const uint2* __restrict__
 // expected item slots per region, region lengths ~ N(L, L) (a region gets each of L * (#regions)
 // tuples with probability 1 / #regions); ties go to the larger K (fewer chunks).
 static int pk_items(double L) {
-#ifdef HJ3D_PK_ITEMS
-  return HJ3D_PK_ITEMS;
-#endif
   int best = kItemsMax;
   double best_slots = 0.0;
   const double sd = std::sqrt(L > 1.0 ? L : 1.0);
@@ -1454,61 +1152,18 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   const bool ck = flags & HJ3D_PROBE_CHECKSUM;
   const int acc = (flags & HJ3D_PROBE_ACCUMULATE) ? 1 : 0;
   const uint64_t preg = uint64_t(Gp) * pl.P;
-  const bool flat = HJ3D_PK_FLAT || double(r.n) / double(preg) < 256.0;
+  // short regions (< 256 pairs expected) are walked as one flattened stream per wave (always-flat
+  // walks measured slower at config B's ~384-pair regions)
+  const bool flat = double(r.n) / double(preg) < 256.0;
   const int items = ctx->pk_items ? ctx->pk_items : flat ? kItemsMax : pk_items(double(r.n) / double(preg));
   uint2* o = static_cast<uint2*>(out);
   uint64_t* partials = ctx->scratch[kScrPartial].as<uint64_t>();
-  // the compact slice image: a known build row range whose words q * rr + row fit 32 bits below
-  // q_max, and a slice image (with 6 sigma of headroom on its entries) within kLdsWordsC
-  PkGeom pkc = pk;
-  bool compact = false;
-  if (ctx->pk_compact && t->row_rr && t->row_rr < (1ull << 32) &&
-      uint64_t(0xFFFFFFFFull / nb) * t->row_rr <= 0xFFFFFFFFull) {
-    const double ex = double(t->n_build) / pl.P;
-    const double words = (pl.W + 2) / 2 + 1 + ex + 6.0 * std::sqrt(ex > 1.0 ? ex : 1.0);
-    compact = words <= double(kLdsWordsC);
-    pkc.rr = uint32_t(t->row_rr);
-    pkc.rlo = t->row_lo;
-  }
-  if (compact) {
-    // twice the workgroups (two per CU): every slice's regions split over two when one wave of
-    // workgroups would leave CUs idle
-    const uint32_t want_c = uint32_t(ctx->num_cus) * 4;
-    uint32_t sp2 = pl.P < want_c ? (want_c + pl.P - 1) / pl.P : 1u;
-    if (sp2 > Gp) sp2 = Gp;
-    const uint32_t nb2 = pl.P * sp2;
-    if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nb2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)
-      return e;
-    partials = ctx->scratch[kScrPartial].as<uint64_t>();
-    KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
-#define HJ3D_PKC_LAUNCH(K, MODE, CK)                                                                                 \
-  tk.launch(k_pk_probe<K, MODE, CK, 512, true>, dim3(nb2), dim3(512), s, pregion, pcounts, Gp, pcap, sp2, flat,     \
-            t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pkc, t->fm, o, out_cap, ovf, ctl, partials, res, acc, \
-            reinterpret_cast<uint2*>(ctl + 64))
-#define HJ3D_PKC_LAUNCH_K(MODE, CK)               \
-  switch (items) {                                \
-    case 5: HJ3D_PKC_LAUNCH(5, MODE, CK); break;  \
-    case 6: HJ3D_PKC_LAUNCH(6, MODE, CK); break;  \
-    case 7: HJ3D_PKC_LAUNCH(7, MODE, CK); break;  \
-    default: HJ3D_PKC_LAUNCH(8, MODE, CK); break; \
-  }
-    if (emit) {
-      if (ck) HJ3D_PKC_LAUNCH_K(1, true)
-      else HJ3D_PKC_LAUNCH_K(1, false)
-    } else {
-      if (ck) HJ3D_PKC_LAUNCH_K(0, true)
-      else HJ3D_PKC_LAUNCH_K(0, false)
-    }
-#undef HJ3D_PKC_LAUNCH_K
-#undef HJ3D_PKC_LAUNCH
-    return hipGetLastError();
-  }
   {
     KernelSpan tk(ctx, HJ3D_T_PROBE_KERNEL);
 #define HJ3D_PK_LAUNCH(K, MODE, CK)                                                                                  \
   tk.launch(k_pk_probe<K, MODE, CK>, dim3(nblocks), dim3(kPkBlock), s, pregion, pcounts, Gp, pcap,              \
                      splits, flat, t->off.as<const uint32_t>(), t->ent.as<const uint2>(), pk, t->fm, o, out_cap, ovf, \
-                     ctl, partials, res, acc, reinterpret_cast<uint2*>(ctl + 64))
+                     ctl, partials, res, acc)
 #define HJ3D_PK_LAUNCH_K(MODE, CK)               \
   switch (items) {                               \
     case 5: HJ3D_PK_LAUNCH(5, MODE, CK); break;  \

@@ -17,9 +17,6 @@
 namespace hj3d {
 namespace {
 
-#ifndef HJ3D_NDU_DIAG
-#define HJ3D_NDU_DIAG 0  // diagnostic variant (checksums wrong): 1 light matches skip their sub-row reads
-#endif
 constexpr int kItems = 2;
 constexpr uint64_t kInline2 = 64;
 constexpr int kF = 12;  // c_probe_rs, cmp_rs, c_probe_rt, cmp_rt, unnest_1, unnest_2, top, sum_a, sum_b, sum_c, sum_h, xor_h
@@ -126,7 +123,7 @@ __device__ __forceinline__ void ndu_tail(uint64_t (&a)[kF], uint32_t pr, const N
   a[5] += prod;
   a[6] += prod;
   if (prod <= kInline2) {
-    if (!HJ3D_NDU_DIAG) light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w, ck);
+    light_triples(a, pr, S, T, MS.z, MS.w, MT.z, MT.w, ck);
   } else {
     const uint64_t slot = atomicAdd(reinterpret_cast<unsigned long long*>(nheavy), 1ull);
     heavy[slot] = Heavy2{pr, ms, mt, 0};

@@ -97,10 +97,6 @@ struct RelView {
   __device__ __forceinline__ uint32_t key(uint64_t i) const {
     return *reinterpret_cast<const uint32_t*>(base + i * stride + key_off);
   }
-  // the same as a non-temporal load (streamed once: keeps the stream from displacing L2 lines)
-  __device__ __forceinline__ uint32_t key_nt(uint64_t i) const {
-    return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + i * stride + key_off));
-  }
   __device__ __forceinline__ uint32_t row(uint64_t i) const {
     if (row_off == 0xFFFFFFFFu) return uint32_t(row_base + i);
     return __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(base + i * stride + row_off));

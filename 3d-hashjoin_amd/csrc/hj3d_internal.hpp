@@ -101,7 +101,6 @@ struct hj3d_ctx {
   bool nested_2l = false;         // HJ3D_OPT_NESTED_2L: the exact two-level partition + register aggregation
   bool rp_unfused = false;        // HJ3D_OPT_RP_UNFUSED: small build partitions as histogram + scatter launches
   bool sync_build = false;        // HJ3D_OPT_SYNC_BUILD: nested builds resolved before hj3d_build returns
-  bool pk_compact = false;        // HJ3D_OPT_PK_COMPACT: the packed probe's compact slice image where it applies
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
   // restores them), zeroed once here; words 64..127 are the sink of its unconditional stores
   hj3d::DevBuf ctl;
@@ -141,10 +140,6 @@ struct hj3d_table {
   bool built = false;
   const char* path = "none";  // which build made the table (hj3d_table_build_path)
   char path_buf[40] = {0};    // hj3d_table_build_path of a table not resolved yet: path + "?"
-  // build rows lie in [row_lo, row_lo + row_rr) (implicit-row builds; 0: unknown): the compact
-  // probe image packs q * row_rr + (row - row_lo) into one word
-  uint32_t row_lo = 0;
-  uint64_t row_rr = 0;
   // nested builds: the counts (main records, give-up flag) are copied to pinned host memory behind
   // the build and read at the table's next use (table_resolve), not waited for inside hj3d_build
   bool pending = false, pending_agg = false;
@@ -346,7 +341,6 @@ PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nb_local, uint64_t n_build);
 struct PkGeom {
   FastDiv32 dnb, dw;  // / NB, / W
   uint32_t nb, lo, nbl, W, P, qbits, qmask;
-  uint32_t rr = 0, rlo = 0;  // compact probe image: build rows in [rlo, rlo + rr), entries q * rr + row - rlo
   // hash of a packed pair in slice p
   __device__ __forceinline__ uint32_t hash_of(uint32_t v, uint32_t p) const {
     return (v & qmask) * nb + lo + p * W + (v >> qbits);
@@ -462,9 +456,9 @@ enum ScratchSlot {
 hipError_t reduce_partials(const uint64_t* partials, uint32_t nblocks, int nf, int nxor, uint64_t* res, hipStream_t s,
                            uint64_t set0 = ~0ull, const uint64_t* base0 = nullptr);
 
-#ifndef HJ3D_TIMER_EVENT_FLAGS
-#define HJ3D_TIMER_EVENT_FLAGS hipEventDisableSystemFence  // timer events (hipEventDefault: A/B)
-#endif
+// timer events: no system-scope fence when recorded (a default event writes the L2 back and left the
+// GPU idle ~10 us between the kernels around it: config B probe 0.887 -> 0.881 ms, r05z_ev_ab)
+constexpr unsigned HJ3D_TIMER_EVENT_FLAGS = hipEventDisableSystemFence;
 // Event spans on the context stream when timing is enabled (hj3d_ctx_timer): a PhaseTimer
 // brackets whatever is enqueued during its lifetime.
 inline hipEvent_t take_event(hj3d_ctx* ctx) {
@@ -497,26 +491,17 @@ struct PhaseTimer {
 // One kernel's span for the per-kernel timers: the two events travel with the dispatch
 // (hipExtLaunchKernel), so timing a kernel puts no marker packet between it and its neighbours.
 // launch(kernel, grid, block, stream, args...) launches with or without them.
-#ifndef HJ3D_EXT_TIMING
-#define HJ3D_EXT_TIMING 1
-#endif
 struct KernelSpan {
   hj3d_ctx* ctx;
   int phase;
   hipEvent_t a = nullptr, b = nullptr;
-  PhaseTimer* marker = nullptr;  // HJ3D_EXT_TIMING = 0: the marker-event form, for A/B
   KernelSpan(hj3d_ctx* c, int p) : ctx(c), phase(p) {
     if (!ctx->timing || p < 0) return;
-    if (!HJ3D_EXT_TIMING) {
-      marker = new PhaseTimer(c, p);
-      return;
-    }
     a = take_event(ctx);
     b = a ? take_event(ctx) : nullptr;
     if (!b) a = nullptr;
   }
   ~KernelSpan() {
-    delete marker;
     if (a && b) ctx->spans[phase].push_back({a, b});
   }
   template <typename F, typename... Args>

@@ -252,26 +252,14 @@ __global__ __launch_bounds__(kBlock) void k_expand_heavy(const Heavy* __restrict
 // workgroup form one (nearly) contiguous, coalesced range. Heavier slots are queued and written
 // by k_expand_heavy_flat with all workgroups.
 constexpr uint32_t kHeavyOut = 8192;
-#ifndef HJ3D_EXP_U
-#define HJ3D_EXP_U 4  // k_expand_light: outputs per thread and step (1: one at a time, A/B)
-#endif
-constexpr int kExpU = HJ3D_EXP_U;
-#ifndef HJ3D_EXP_XCD
-#define HJ3D_EXP_XCD 1  // k_expand_light: slot blocks XCD-ordered (0: A/B; config D Nrs probe 6.14 -> 5.64 ms, C unchanged)
-#endif
-#ifndef HJ3D_RN_XCD
-#define HJ3D_RN_XCD 1  // nested probe on slices wider than LDS: shared slices, XCD-ordered blocks (0: A/B)
-#endif
-#ifndef HJ3D_RN_SPLITS
-#define HJ3D_RN_SPLITS 16  // workgroups per wide slice (16: one region stream per wave at G = 256)
-#endif
-constexpr uint32_t kHbmSplits = HJ3D_RN_SPLITS;
-#ifndef HJ3D_RN_PK
-#define HJ3D_RN_PK 1  // nested probe of more than 2048 LDS slices on the packed two-level partition (0: A/B, wide slices)
-#endif
-#ifndef HJ3D_RN_STATIC
-#define HJ3D_RN_STATIC 1  // k_rn_probe_seg, materialised unnest: fixed store count per chunk (0: A/B)
-#endif
+// Fixed by measurement: k_expand_light takes four outputs per thread and
+// step (one: 0.829 against 0.813 ms at config C; eight: 0.805 against 0.794) and its slot blocks
+// XCD-ordered (config D Nrs probe 6.14 -> 5.64 ms); a nested probe on slices wider than LDS shares
+// each slice among kHbmSplits XCD-ordered workgroups (8 / 16 / 32: 8.43 / 8.24 / 9.12 ms at D); more
+// than 2048 LDS slices go through the packed two-level partition; the materialised unnest stores a
+// fixed count per chunk (0.813 -> 0.791 ms at C).
+constexpr int kExpU = 4;
+constexpr uint32_t kHbmSplits = 16;  // one region stream per wave at G = 256
 static_assert(kBlock == 256, "k_expand_light's binary search covers 256 slots in 8 steps");
 
 struct SlotSrc {
@@ -304,11 +292,11 @@ __global__ __launch_bounds__(kBlock) void k_expand_light(SlotSrc src, uint64_t n
   __shared__ uint64_t lpos[kBlock];
   __shared__ uint32_t wsum[kBlock / kWave];
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  // XCD-ordered blocks (HJ3D_EXP_XCD): workgroup b runs on XCD b % 8, so consecutive slot blocks
+  // XCD-ordered blocks: workgroup b runs on XCD b % 8, so consecutive slot blocks
   // (probe tuples of one slice: their keys' sub rows lie in one window of `sub`) would read that
   // window into eight L2s; XCD x takes the x-th eighth of the blocks instead
   uint32_t bid = blockIdx.x;
-  if (HJ3D_EXP_XCD) {
+  {
     const uint32_t per = gridDim.x / 8;
     if (bid < per * 8) bid = (bid % 8) * per + bid / 8;
   }
@@ -611,7 +599,7 @@ __global__ __launch_bounds__(kJBlock) void k_rn_probe_seg(const uint2* __restric
   uint32_t* ldir = lds;
   uint4* lmain = reinterpret_cast<uint4*>(lds + dirw);
   uint64_t acc[kProbeFields] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-  if constexpr (MODE == kCountUN && FITS && HJ3D_RN_STATIC) {
+  if constexpr (MODE == kCountUN && FITS) {
     // materialised unnest: every item of a chunk writes its three slot words, in straight-line
     // code (absent items to the sink), so the chunk's store count is fixed and the wait for the
     // next chunk's pairs (loaded before these stores) leaves the stores in flight
@@ -880,7 +868,7 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   } ctl_reset{ctx, s};
   {
     const uint64_t P0 = (uint64_t(nbl) + w_fit - 1) / w_fit;
-    if (HJ3D_RN_PK && !sel && w_fit >= 64 && P0 > 2048 && P0 <= 65536) {
+    if (!sel && w_fit >= 64 && P0 > 2048 && P0 <= 65536) {
       const uint64_t G = uint64_t(ctx->num_cus);
       const uint64_t P1 = (P0 + G - 1) / G * G;  // whole waves of probe workgroups
       const uint32_t W1 = uint32_t((uint64_t(nbl) + P1 - 1) / P1);
@@ -897,7 +885,7 @@ hipError_t radix_nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel
   // the blocks are ordered so that an XCD's workgroups take consecutive (slice, share) pairs: the
   // ~32 workgroups of an XCD work on two slices at a time, whose directory and main records
   // (~1 MB each) stay in its 4 MB L2 instead of 32 different slices thrashing it.
-  const bool wide = !pkd && HJ3D_RN_XCD && pp.W > w_fit && pp.splits < kHbmSplits && pp.G >= kHbmSplits;
+  const bool wide = !pkd && pp.W > w_fit && pp.splits < kHbmSplits && pp.G >= kHbmSplits;
   if (wide) pp.splits = kHbmSplits;
   const uint32_t nblocks = pp.P * pp.splits;
   if ((e = ctx->scratch[kScrPartial].ensure(uint64_t(nblocks + 2) * kProbeFields * sizeof(uint64_t))) != hipSuccess)

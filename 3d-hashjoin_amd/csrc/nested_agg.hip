@@ -74,6 +74,9 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_REG
 #define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
 #endif
+#ifndef HJ3D_NAGG_REG_SLOTS
+#define HJ3D_NAGG_REG_SLOTS 4  // largest register-form table: SLOTS x 1024 slots (6: A/B, config E's 5,701)
+#endif
 #ifndef HJ3D_NAGG_REG_FILL
 #define HJ3D_NAGG_REG_FILL 0.85  // largest mean partition (fraction of the register capacity) for k_nagg_reg
 #endif
@@ -88,6 +91,9 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
 
+#ifndef HJ3D_NAGG_ELECT
+#define HJ3D_NAGG_ELECT 2  // hot-key wave leader election: 2 partitions above 5/4 of the mean size (default), 1 every partition, 0 none
+#endif
 #ifndef HJ3D_NAGG_ENDBAR
 #define HJ3D_NAGG_ENDBAR 0  // a barrier after the last round of a partition too (1: A/B)
 #endif
@@ -223,6 +229,7 @@ struct NaggTabs {
   uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
   uint64_t* hc[2] = {nullptr, nullptr};      // the tables' pinned host mirrors of the counts words (or none)
   uint32_t* sink = nullptr;  // pass B's stores of items without a row (the context's store-sink words)
+  uint32_t elect_min = 0;    // partitions of at least this many pairs elect a wave leader per hot key
 };
 // one partition (global index gp) of k_nagg
 template <int BLOCK, int SLOTS, bool PK>
@@ -248,6 +255,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
   // (table ti's sub rows are numbered from its first pair: ps[ti * P])
   const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = ps[ti * tabs.P];
+  const bool elect = total >= tabs.elect_min;  // (uniform per workgroup)
   nagg_clk(gp, 0);
   nagg_clk(gp, 7);
   const int lane = threadIdx.x & 63;
@@ -361,7 +369,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         bool a = (actm >> u) & 1u;
-        const uint64_t am = __ballot(a);
+        const uint64_t am = elect ? __ballot(a) : 0ull;
         if (am) {  // the wave's first active key, if several lanes hold it (a Zipf hot key)
           const int leader = __ffsll((unsigned long long)am) - 1;
           const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
@@ -472,7 +480,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       for (int u = 0; u < kAggU; ++u) {
         bool a = (actm >> u) & 1u;
         uint32_t* dst = tabs.sink;
-        const uint64_t am = __ballot(a);
+        const uint64_t am = elect ? __ballot(a) : 0ull;
         if (am) {
           const int leader = __ffsll((unsigned long long)am) - 1;
           const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
@@ -948,6 +956,11 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   tabs.P = P;
   tabs.nt = nt;
   tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
+  // the hot-key election of the streaming form: in every partition, in partitions above 5/4 of the
+  // mean only, or nowhere (HJ3D_NAGG_ELECT 1 / 2 / 0)
+  tabs.elect_min = HJ3D_NAGG_ELECT == 1 ? 0u
+                   : HJ3D_NAGG_ELECT == 2 ? uint32_t(std::min<uint64_t>(5 * n / (4 * uint64_t(PT)), 0xFFFFFFFFull))
+                                          : 0xFFFFFFFFu;
   for (uint32_t k = 0; k < nt; ++k) {
     tabs.pbase[k] = k ? uint32_t(rr[0].n) : 0u;
     tabs.off[k] = tt[k]->off.as<uint32_t>();
@@ -1006,6 +1019,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   if (!lds_attr) {
     for (const void* k : {reinterpret_cast<const void*>(&k_nagg_reg<true, 4>),
                           reinterpret_cast<const void*>(&k_nagg_reg<false, 4>),
+                          reinterpret_cast<const void*>(&k_nagg_reg<true, 6>),
+                          reinterpret_cast<const void*>(&k_nagg_reg<false, 6>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, true>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
@@ -1019,16 +1034,26 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)
   const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
-  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= HJ3D_NAGG_REG_FILL * kRegCap && capr <= 4 * kRegBlock &&
-                   reg_lds_words(capr, W) * 4 <= 160 * 1024;
+  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= HJ3D_NAGG_REG_FILL * kRegCap &&
+                   capr <= uint32_t(HJ3D_NAGG_REG_SLOTS) * kRegBlock && reg_lds_words(capr, W) * 4 <= 160 * 1024;
   if (reg) {
     const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);
-    if (pk)
-      hipLaunchKernelGGL((k_nagg_reg<true, 4>), dim3(std::min<uint32_t>(PT, G)), dim3(kRegBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, PT, mtmp, dcount, capr, src, tabs, nullptr);
-    else
-      hipLaunchKernelGGL((k_nagg_reg<false, 4>), dim3(std::min<uint32_t>(PT, G)), dim3(kRegBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, PT, mtmp, dcount, capr, src, tabs, order);
+    const dim3 gr(std::min<uint32_t>(PT, G)), bl(kRegBlock);
+    if (capr <= 4 * kRegBlock) {
+      if (pk)
+        hipLaunchKernelGGL((k_nagg_reg<true, 4>), gr, bl, lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, PT, mtmp, dcount,
+                           capr, src, tabs, nullptr);
+      else
+        hipLaunchKernelGGL((k_nagg_reg<false, 4>), gr, bl, lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, PT, mtmp, dcount,
+                           capr, src, tabs, order);
+    } else {
+      if (pk)
+        hipLaunchKernelGGL((k_nagg_reg<true, 6>), gr, bl, lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, PT, mtmp, dcount,
+                           capr, src, tabs, nullptr);
+      else
+        hipLaunchKernelGGL((k_nagg_reg<false, 6>), gr, bl, lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, PT, mtmp, dcount,
+                           capr, src, tabs, order);
+    }
     if (path) *path = pk ? "nested_agg_slices_reg" : two ? "nested_agg_2l_reg" : "nested_agg_reg";
   } else if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
     const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);

@@ -93,24 +93,13 @@ __global__ void k_part_counts(const uint32_t* __restrict__ offs, uint32_t ntiles
 // run's place in p's area), stages the tile destination-major in LDS and writes the runs out with
 // consecutive lanes on consecutive pairs. The next tile's keys load while this one is written.
 // Per tuple: the tuple read once (12 B at the headline layout) + one 8-B pair written.
-#ifndef HJ3D_XP_ROUNDS
-#define HJ3D_XP_ROUNDS 8  // tuples per thread and tile (8: 8192-tuple tiles)
-#endif
-#ifndef HJ3D_XP_NT
-#define HJ3D_XP_NT 1  // pairs stored non-temporal (0: plain; A/B)
-#endif
 // Two 512-thread workgroups per CU (4096-tuple tiles): one workgroup's barrier-separated phases
 // overlap the other's memory waits. 1e9 tuples into 8 destinations, same box: one 1024-thread
 // workgroup per CU 4.81 / 4.80 ms, two of 512 threads 4.20 / 4.19 ms, three 4.80 / 4.76 ms
 // (profiles/r04c_ab_xpart.log).
-#ifndef HJ3D_XP_BLOCK
-#define HJ3D_XP_BLOCK 512  // threads per workgroup
-#endif
-#ifndef HJ3D_XP_WGS
-#define HJ3D_XP_WGS 2  // persistent workgroups per CU
-#endif
-constexpr int kXpBlock = HJ3D_XP_BLOCK;
-constexpr int kXpRounds = HJ3D_XP_ROUNDS;
+constexpr int kXpBlock = 512;  // threads per workgroup
+constexpr int kXpWgs = 2;      // persistent workgroups per CU
+constexpr int kXpRounds = 8;   // tuples per thread and tile (4096-tuple tiles); pairs stored non-temporal
 constexpr int kXpTile = kXpBlock * kXpRounds;  // rank inside the tile: < 2^16
 constexpr int kXpMaxParts = 256;
 
@@ -234,10 +223,7 @@ __global__ __launch_bounds__(kXpBlock) void k_xpart(RelView r, FastMod fm, uint6
       const uint64_t pos = gbase[d] + (kk - sbase[d]);
       const uint2 e = stage[kk];
       uint2* dst = kk < nt && pos < stride ? out + d * stride + pos : sink + me;
-      if (HJ3D_XP_NT)
-        __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(dst));
-      else
-        *dst = e;
+      __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(dst));
     }
   }
 }
@@ -682,7 +668,7 @@ hipError_t partition_strided(hj3d_ctx* ctx, const hj3d_rel& r, uint64_t nb, uint
   if ((e = hipMemsetAsync(counts, 0, parts * sizeof(uint64_t), s)) != hipSuccess) return e;
   if (r.n == 0) return hipSuccess;
   const uint64_t ntiles = (r.n + kXpTile - 1) / kXpTile;
-  const uint64_t want = uint64_t(ctx->num_cus) * HJ3D_XP_WGS;  // persistent: HJ3D_XP_WGS workgroups per CU
+  const uint64_t want = uint64_t(ctx->num_cus) * kXpWgs;  // persistent: kXpWgs workgroups per CU
   const unsigned grid = unsigned(ntiles < want ? ntiles : want);
   uint32_t pbits = 0;
   while ((1u << pbits) < parts) ++pbits;

@@ -26,45 +26,14 @@ constexpr int kPBlock = 1024;                    // partition kernels: 16 waves
 constexpr int kPRounds = 16;
 constexpr int kPTile = kPBlock * kPRounds;       // 16384 tuples per partition tile
 constexpr int kPRoundsR = 8;                     // k_rp_part1r: 8192-tuple tiles
-#ifndef HJ3D_PSEG
-#define HJ3D_PSEG 16
-#endif
-#ifndef HJ3D_PROBE_WFRAC
-#define HJ3D_PROBE_WFRAC 0.8
-#endif
-constexpr int kPSeg = HJ3D_PSEG;                 // k_rp_part1r: 128-B region segments
-#ifndef HJ3D_NT_BUILD
-#define HJ3D_NT_BUILD 0  // build kernels: loads / stores non-temporal (A/B; measured worse: R is read twice, the
-                         // pairs re-read by the build, the table by the probe, all from the Infinity Cache)
-#endif
-template <typename T>
-__device__ __forceinline__ T nt_ld(const T* p) {
-  if constexpr (HJ3D_NT_BUILD) {
-    if constexpr (sizeof(T) == 8) {
-      const uint64_t v = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(p));
-      T t;
-      __builtin_memcpy(&t, &v, 8);
-      return t;
-    } else {
-      return __builtin_nontemporal_load(p);
-    }
-  }
-  return *p;
-}
-__device__ __forceinline__ void nt_st(uint2* p, uint2 e) {
-  if constexpr (HJ3D_NT_BUILD) __builtin_nontemporal_store((uint64_t(e.y) << 32) | e.x, reinterpret_cast<uint64_t*>(p));
-  else *p = e;
-}
-__device__ __forceinline__ void nt_st(uint32_t* p, uint32_t v) {
-  if constexpr (HJ3D_NT_BUILD) __builtin_nontemporal_store(v, p);
-  else *p = v;
-}
-__device__ __forceinline__ uint32_t key_ld(const RelView& r, uint64_t i) { return HJ3D_NT_BUILD ? r.key_nt(i) : r.key(i); }
+constexpr int kPSeg = 16;                        // k_rp_part1r: 128-B region segments
+constexpr double kProbeWFrac = 0.8;              // partitioned probes: slice width at this share of the LDS
+// Build kernels load and store through the caches (non-temporal forms measured worse: R is read
+// twice, the pairs re-read by the build and the table by the probe, all from the Infinity Cache).
+__device__ __forceinline__ void put(uint2* p, uint2 e) { *p = e; }
+__device__ __forceinline__ void put(uint32_t* p, uint32_t v) { *p = v; }
 static_assert(kPTile == 1 << 14, "k_rp_scatter packs (partition, rank) as p << 14 | rank");
 constexpr uint32_t kMaxParts = 2048;             // fan-out limit of one partition pass
-#ifndef HJ3D_PROBE_WAVES
-#define HJ3D_PROBE_WAVES 1  // partitioned probes: slice count rounded up to whole waves of workgroups (0: A/B)
-#endif
 constexpr uint32_t kBuildSlice = 16384;          // buckets per build partition (64 KB of LDS counters)
 constexpr uint32_t kSortedMax = 32;             // buckets up to this size are kept sorted by row
 
@@ -120,7 +89,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist(RelTiles rt, FastMod fm, ui
 #pragma unroll
     for (int j = 0; j < ROUNDS; ++j) {  // all loads of the tile in flight together
       const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
-      key[j] = tile < ntiles && i < r.n ? key_ld(r, i) : 0u;
+      key[j] = tile < ntiles && i < r.n ? r.key(i) : 0u;
     }
   };
   load(blockIdx.x);
@@ -183,7 +152,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
     for (int j = 0; j < ROUNDS; ++j) {
       const uint64_t i = b + uint64_t(j) * kPBlock + threadIdx.x;
       const bool ok = tile < ntiles && i < r.n;
-      h[j] = ok ? key_ld(r, i) : 0u;
+      h[j] = ok ? r.key(i) : 0u;
       rw[j] = explicit_rows && ok ? r.row(i) : 0u;
     }
   };
@@ -232,7 +201,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
     for (uint32_t k = threadIdx.x; k < m; k += kPBlock) {
       const uint2 e = stage[k];
       const uint32_t p = pofs + fw.div(fm.mod(e.x) - lo);
-      nt_st(out + gb[p] + (k - loc[p]), e);
+      put(out + gb[p] + (k - loc[p]), e);
     }
     __syncthreads();
     for (uint32_t p = threadIdx.x; p < P; p += kPBlock)  // advance the cursors by the tile's runs
@@ -253,14 +222,10 @@ __global__ __launch_bounds__(kPBlock) void k_rp_scatter(RelTiles rt, FastMod fm,
 // Phase 2 stages kFzGroup tiles per pass. One relation only (hj3d_build; hj3d_build_many's two
 // relations keep the two launches: at config E, 4 tiles per workgroup, the fused form measured
 // 66.9 against 19.4 + 43.8 us, at config B, 5 tiles, 87.0 against 26.4 + 67.5 us).
-#ifndef HJ3D_RP_FUSED
-#define HJ3D_RP_FUSED 1  // small implicit-row inputs: the fused one-launch partition (0: hist + scatter, A/B)
-#endif
-#ifndef HJ3D_RP_FZ_GROUP
-#define HJ3D_RP_FZ_GROUP 2  // fused partition: tiles staged per pass of phase 2 (1: one pass per tile, A/B)
-#endif
+// (Phase 2 with one tile per staging pass: 0.1378 / 0.1386 against 0.1344 / 0.1346 ms build at
+// config B, r05y_B; HJ3D_OPT_RP_UNFUSED keeps the two-launch form for A/B and its parity test.)
 constexpr int kFzRounds = 8;
-constexpr int kFzGroup = HJ3D_RP_FZ_GROUP;
+constexpr int kFzGroup = 2;  // tiles staged per pass of phase 2
 constexpr int kFzTMax = 6;  // tiles per workgroup held in registers (48 hashes per thread)
 // On a timeout the workgroup sets the context's word bar[1] (read with the probe results) and writes
 // the launch's tag (the context's fused-launch sequence number) into the table's flag word `tflag`
@@ -329,8 +294,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, ui
 #pragma unroll
     for (int j = 0; j < R; ++j) {
       const uint32_t li = uint32_t(j) * kPBlock + me;
-      hv[t][j] = li < nl ? (HJ3D_NT_BUILD ? __builtin_nontemporal_load(reinterpret_cast<const uint32_t*>(tb + li * r.stride))
-                                          : *reinterpret_cast<const uint32_t*>(tb + li * r.stride))
+      hv[t][j] = li < nl ? (*reinterpret_cast<const uint32_t*>(tb + li * r.stride))
                          : 0u;
     }
   }
@@ -405,7 +369,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, ui
     for (uint32_t k = me; k < m; k += kPBlock) {
       const uint2 e = stage[k];
       const uint32_t p = fz.dw.div(fz.bucket(e.x));
-      nt_st(out + gb[p] + (k - loc[p]), e);
+      put(out + gb[p] + (k - loc[p]), e);
     }
     __syncthreads();
     for (uint32_t p = me; p < P; p += kPBlock) gb[p] += (p + 1 < P ? loc[p + 1] : m) - loc[p];
@@ -426,18 +390,11 @@ __global__ __launch_bounds__(kPBlock) void k_rp_fused(RelTiles rt, FzGeom fz, ui
 // overflow anything, and the output is one contiguous range per partition, as k_rp_scatter's.
 // Tuples: the tiles of k_rp_hist (kPTile = 16384), as two 8192-tuple halves.
 // PPT = 1: P <= 1024, 128-B segments; PPT = 2: P <= 2048, 64-B segments (a smaller carry).
-#ifndef HJ3D_RP_WS
-#define HJ3D_RP_WS 1  // the build-side partition writes whole segments (k_rp_wscatter; 0: k_rp_scatter, A/B)
-#endif
-#ifndef HJ3D_RP_WS_MIN
-#define HJ3D_RP_WS_MIN 4  // ... from this many tiles per partitioning workgroup on
-#endif
-#ifndef HJ3D_RP_SMALL_ROUNDS
-#define HJ3D_RP_SMALL_ROUNDS 8  // below that: the plain scatter on tiles of this many x 1024 tuples (16: A/B)
-#endif
-#ifndef HJ3D_RP_SMALL_WGS
-#define HJ3D_RP_SMALL_WGS 1  // ... with this many workgroups per CU (its ~100 VGPRs leave room for one)
-#endif
+// The build-side partition writes whole segments (k_rp_wscatter) from kRpWsMin tiles per
+// partitioning workgroup on; below that the plain scatter (k_rp_scatter) on kRpSmallRounds x 1024-tuple
+// tiles, one workgroup per CU (its ~100 VGPRs leave room for one).
+constexpr uint32_t kRpWsMin = 4;
+constexpr int kRpSmallRounds = 8;
 constexpr int kWsRounds = 8;
 constexpr int kWsSub = kPBlock * kWsRounds;  // 8192 tuples per half tile
 template <int PPT>
@@ -492,7 +449,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelTiles rt, FastMod fm
 #pragma unroll
     for (int j = 0; j < kWsRounds; ++j) {
       const uint64_t i = base + uint64_t(j) * kPBlock + me;
-      h[j] = i < r.n ? key_ld(r, i) : 0u;
+      h[j] = i < r.n ? r.key(i) : 0u;
       if constexpr (EXPL) rw[j] = i < r.n ? r.row(i) : 0u;
     }
   };
@@ -595,7 +552,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelTiles rt, FastMod fm
       const uint2 si = seginfo[kk / SEG];
       const uint32_t j = kk % SEG;
       const uint2 e = stage[(si.y & 0xFFFFu) + j];
-      if (j >= (si.y >> 16)) nt_st(out + si.x + j, e);
+      if (j >= (si.y >> 16)) put(out + si.x + j, e);
     }
     // each run's tail (< one segment) becomes the partition's carry. (The next half tile's first
     // stage / seginfo writes follow its ranking barrier, which every thread reaches only after
@@ -640,7 +597,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist2(RelView r, FastMod fm, uin
 #pragma unroll
   for (int j = 0; j < kPRounds; ++j) {
     const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    key[j] = i < r.n ? key_ld(r, i) : 0u;
+    key[j] = i < r.n ? r.key(i) : 0u;
   }
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     uint32_t bl[kPRounds];
@@ -653,7 +610,7 @@ __global__ __launch_bounds__(kPBlock) void k_rp_hist2(RelView r, FastMod fm, uin
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j) {
       const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      key[j] = i < r.n ? key_ld(r, i) : 0u;
+      key[j] = i < r.n ? r.key(i) : 0u;
     }
 #pragma unroll
     for (int j = 0; j < kPRounds; ++j)
@@ -775,7 +732,7 @@ __global__ __launch_bounds__(kS2Block) void k_rp_split2(const uint2* __restrict_
       cof[q] = uint8_t(fi[j]);
     }
     __syncthreads();
-    for (uint32_t q = me; q < len; q += kS2Block) nt_st(out + dbase[cof[q]] + q, stage[q]);
+    for (uint32_t q = me; q < len; q += kS2Block) put(out + dbase[cof[q]] + q, stage[q]);
     __syncthreads();
   }
 }
@@ -842,10 +799,6 @@ __global__ __launch_bounds__(kJBlock) void k_rp_build(const uint2* __restrict__ 
 constexpr uint32_t kBuildSlice2 = 8192;
 constexpr uint32_t kBuildSlice2Max = 10240;  // wider slices keep the partition count <= 1024 (k_rp_wscatter<1>)
 constexpr uint32_t kBuildStage = 14400;
-#ifndef HJ3D_B3_HALF
-#define HJ3D_B3_HALF 0  // chaining build: half-width slices, two 512-thread k_rp_build3 workgroups per CU (A/B)
-#endif
-constexpr uint32_t kB3HalfW = 5120, kB3HalfStage = 6656;  // 72 KB of LDS: two workgroups per CU
 
 // The staged build as a persistent kernel (one 1024-thread workgroup per CU takes partitions
 // blockIdx.x, blockIdx.x + gridDim.x, ...): the next partition's pairs are loaded into registers
@@ -857,8 +810,8 @@ constexpr uint32_t kB3HalfW = 5120, kB3HalfStage = 6656;  // 72 KB of LDS: two w
 // stay in arrival order) and is written to the CSR. Larger partitions (skewed keys) scatter
 // through HBM instead (sorting their small buckets there).
 constexpr int kB3Per = 12;  // pairs per thread held in registers: partitions up to 12 * BLOCK pairs
-// BLOCK = 1024: one workgroup per CU, slices up to kBuildSlice2Max buckets; BLOCK = 512
-// (HJ3D_B3_HALF): two per CU on half-width slices (WMAX, STAGE: its LDS share)
+// One 1024-thread workgroup per CU, slices up to WMAX buckets, STAGE pairs of LDS stage. (Two
+// 512-thread workgroups per CU on half-width slices measured slower: build 0.191 against 0.164 ms.)
 template <int BLOCK, uint32_t WMAX, uint32_t STAGE>
 __global__ __launch_bounds__(BLOCK) void k_rp_build3(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                      FastMod fm, uint32_t lo, uint32_t nbl, uint32_t W, uint32_t P,
@@ -876,7 +829,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_build3(const uint2* __restrict__ p
 #pragma unroll
     for (int u = 0; u < kB3Per; ++u) {
       const uint32_t i = s0 + u * BLOCK + threadIdx.x;
-      e[u] = i < s1 ? nt_ld(pairs + i) : make_uint2(0, 0);
+      e[u] = i < s1 ? pairs[i] : make_uint2(0, 0);
     }
   };
   auto build = [&](uint2 (&e)[kB3Per], uint32_t p) __attribute__((always_inline)) {
@@ -924,7 +877,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_build3(const uint2* __restrict__ p
     __syncthreads();
     lds_excl_scan<BLOCK>(cnt, nbs, wsum);
     if (threadIdx.x == 0) cnt[nbs] = m;
-    for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) nt_st(off + b0 + k, s0 + cnt[k]);
+    for (uint32_t k = threadIdx.x; k < nbs; k += BLOCK) put(off + b0 + k, s0 + cnt[k]);
     if (b0 + nbs == nbl && threadIdx.x == 0) off[nbl] = s1;
     __syncthreads();
 #pragma unroll
@@ -941,7 +894,7 @@ __global__ __launch_bounds__(BLOCK) void k_rp_build3(const uint2* __restrict__ p
         for (uint32_t k = bs; k < bs + n; ++k) r += stage[k].y < x.y;
         pos = bs + r;
       }
-      nt_st(ent + s0 + pos, x);
+      put(ent + s0 + pos, x);
     }
     __syncthreads();
   };
@@ -1626,19 +1579,19 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   // carries ride into later tiles): config C (24 tiles per workgroup) 0.735 -> 0.543 ms; with 1-2.4
   // tiles each (configs E and B) most runs are flushed partial anyway and the plain write-out
   // measured faster (E, both tables in one pass: 51.8 against 2 x 20 us; B: 70.4 against 67.4 us).
-  // Small inputs take the plain scatter on HJ3D_RP_SMALL_ROUNDS x 1024-tuple tiles instead (more,
+  // Small inputs take the plain scatter on kRpSmallRounds x 1024-tuple tiles instead (more,
   // evenly spread tiles: config B's 611 tiles of 16384 gave 157 workgroups 2 and 99 of them 3),
   // one workgroup per CU.
   const uint32_t nt16 = uint32_t((r.n + kPTile - 1) / kPTile) + (r1 ? uint32_t((r1->n + kPTile - 1) / kPTile) : 0u);
-  const bool ws = HJ3D_RP_WS && nt16 >= HJ3D_RP_WS_MIN * (nt16 < cus ? nt16 : cus);
-  const uint32_t rounds = ws ? uint32_t(kPRounds) : uint32_t(HJ3D_RP_SMALL_ROUNDS);
+  const bool ws = nt16 >= kRpWsMin * (nt16 < cus ? nt16 : cus);
+  const uint32_t rounds = ws ? uint32_t(kPRounds) : uint32_t(kRpSmallRounds);
   const uint32_t tsz = kPBlock * rounds;
   const uint32_t nt0 = uint32_t((r.n + tsz - 1) / tsz), nt1 = r1 ? uint32_t((r1->n + tsz - 1) / tsz) : 0u;
   const uint32_t ntiles = nt0 + nt1;
   if (ntiles == 0) return hipMemsetAsync(ps, 0, (uint64_t(PT) + 1) * sizeof(uint32_t), s);
   if (PT > kMaxParts) return hipErrorNotSupported;
   // G persistent workgroups in both passes, one row of run offsets per workgroup
-  const uint32_t gmax = ws ? cus : cus * HJ3D_RP_SMALL_WGS;
+  const uint32_t gmax = cus;
   const uint32_t g = ntiles < gmax ? ntiles : gmax;
   if ((e = ctx->scratch[kScrPHist].ensure(uint64_t(PT) * g * sizeof(uint32_t))) != hipSuccess) return e;
   uint32_t* hist = ctx->scratch[kScrPHist].as<uint32_t>();
@@ -1660,7 +1613,7 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
   // registers and the G workgroups are co-resident (the grid barrier needs all of them at once)
   const bool implicit = r.row_off == HJ3D_ROW_IMPLICIT && (!r1 || r1->row_off == HJ3D_ROW_IMPLICIT);
   const uint32_t tpw = (ntiles + g - 1) / g;
-  if (HJ3D_RP_FUSED && !ctx->rp_unfused && !r1 && !ws && rounds == uint32_t(kFzRounds) && implicit && tpw <= uint32_t(kFzTMax) &&
+  if (!ctx->rp_unfused && !r1 && !ws && rounds == uint32_t(kFzRounds) && implicit && tpw <= uint32_t(kFzTMax) &&
       t->desc.num_buckets >= 2 && t->desc.num_buckets < (1ull << 32) && pl.W >= 2) {
     const void* kf = tpw <= 2   ? reinterpret_cast<const void*>(&k_rp_fused<2>)
                      : tpw == 3 ? reinterpret_cast<const void*>(&k_rp_fused<3>)
@@ -1714,7 +1667,7 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
       hipLaunchKernelGGL(k_rp_hist<kPRounds>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw, PT, ntiles,
                          hist, cur);
     else
-      hipLaunchKernelGGL(k_rp_hist<HJ3D_RP_SMALL_ROUNDS>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw,
+      hipLaunchKernelGGL(k_rp_hist<kRpSmallRounds>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local, pl.fw,
                          PT, ntiles, hist, cur);
   }
   {
@@ -1733,7 +1686,7 @@ hipError_t partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r
       else HJ3D_WS_LAUNCH(2, false);
     } else
 #undef HJ3D_WS_LAUNCH
-      hipLaunchKernelGGL(k_rp_scatter<HJ3D_RP_SMALL_ROUNDS>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local,
+      hipLaunchKernelGGL(k_rp_scatter<kRpSmallRounds>, dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, t->nb_local,
                          pl.fw, PT, ntiles, hist, cur, cur_next, ps, out);
   }
   return hipGetLastError();
@@ -1847,15 +1800,8 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   // of k_rp_build3's persistent workgroups; config B: 1221 -> 1024 partitions of 9766 buckets)
   uint32_t W2 = kBuildSlice2;
   const uint32_t Wk = uint32_t((uint64_t(nbl) + kPBlock - 1) / kPBlock);
-  if (HJ3D_RP_WS && Wk > W2 && Wk <= kBuildSlice2Max && fill * Wk * 1.25 <= kBuildStage) W2 = Wk;
+  if (Wk > W2 && Wk <= kBuildSlice2Max && fill * Wk * 1.25 <= kBuildStage) W2 = Wk;
   bool staged = fill * W2 * 1.25 <= kBuildStage && (uint64_t(nbl) + W2 - 1) / W2 <= kMaxParts;
-  // HJ3D_B3_HALF: half-width slices (up to 2048 of them), two 512-thread build workgroups per CU
-  const uint32_t Wh = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
-  const bool half = HJ3D_B3_HALF && Wh <= kB3HalfW && fill * std::max(Wh, 1024u) * 1.25 <= kB3HalfStage;
-  if (half) {
-    W2 = std::max(Wh, 1024u);
-    staged = true;
-  }
   const Plan pl = plan_for(nbl, staged ? W2 : kBuildSlice, r.n);
   if (pl.P > kMaxParts) return hipErrorNotSupported;  // > 2048 x 16384 buckets: the direct build
   if ((e = ctx->scratch[kScrPairs].ensure((r.n ? r.n : 1) * sizeof(uint2))) != hipSuccess) return e;
@@ -1864,13 +1810,9 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
   uint32_t* ps = ctx->scratch[kScrPStart].as<uint32_t>();
   if ((e = partition_pairs(ctx, t, r, pl, pairs, ps, s)) != hipSuccess) return e;
   if (nbl && staged) {
-    const uint32_t cus = uint32_t(ctx->num_cus) * (half ? 2u : 1u);
+    const uint32_t cus = uint32_t(ctx->num_cus);
     const uint32_t g = pl.P < cus ? pl.P : cus;
-    if (half)
-      hipLaunchKernelGGL((k_rp_build3<512, kB3HalfW, kB3HalfStage>), dim3(g), dim3(512), 0, s, pairs, ps, t->fm,
-                         uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
-    else
-      hipLaunchKernelGGL((k_rp_build3<kJBlock, kBuildSlice2Max, kBuildStage>), dim3(g), dim3(kJBlock), 0, s, pairs, ps,
+    hipLaunchKernelGGL((k_rp_build3<kJBlock, kBuildSlice2Max, kBuildStage>), dim3(g), dim3(kJBlock), 0, s, pairs, ps,
                          t->fm, uint32_t(t->desc.bucket_lo), nbl, pl.W, pl.P, t->off.as<uint32_t>(), t->ent.as<uint2>());
     if (rows_sorted) *rows_sorted = true;
   } else if (nbl) {
@@ -1964,7 +1906,7 @@ hipError_t radix_partition_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   // more than kMaxParts slices: wider slices that no longer fit LDS (probed through L2 by the
   // non-fitting kernel, still one bucket range per workgroup)
   if ((uint64_t(nbl) + W - 1) / W > kMaxParts) W = uint32_t((uint64_t(nbl) + kMaxParts - 1) / kMaxParts);
-  if (HJ3D_PROBE_WAVES) {
+  {
     // the probe runs one LDS-bound workgroup per CU and slice: round the slice count up to whole
     // waves of workgroups (narrower slices), so no last wave of a few slices costs a full one
     // (config C: 1302 slices = 5.1 waves -> 1536 = 6). Not past the whole-segment partitioner's
@@ -2065,7 +2007,7 @@ hipError_t radix_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, ui
   const double fill = t->n_build ? double(t->n_build) / double(t->nb_local) : 0.0;
   ProbeParts pp;
   unsigned long long* npass = nullptr;
-  if ((e = radix_partition_probe(ctx, t, r, uint32_t(HJ3D_PROBE_WFRAC * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s, sel,
+  if ((e = radix_partition_probe(ctx, t, r, uint32_t(kProbeWFrac * kProbeLdsWords / (1.0 + 2.0 * fill)), &pp, s, sel,
                                  sel ? &npass : nullptr)) != hipSuccess)
     return e;
   SegLaunch L;

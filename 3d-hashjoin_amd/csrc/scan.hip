@@ -6,21 +6,15 @@
 // words carry a per-call epoch, so nothing is cleared between calls; the last tile resets the
 // ticket. HBM traffic: 1 read + 1 write of the array.
 // u64: reduce-then-scan in three launches (per-tile sums, one workgroup scanning the tile sums,
-// per-tile scan: 2 reads + 1 write); HJ3D_SCAN64_LB = 1 selects the same single pass as u32
-// (k_scan_lb64, flag << 62 | value status words cleared by a fill before each call), which
-// measured slower: the look-back chain across XCDs costs more than the two extra launches. The two forms share the status
-// buffer: u32 epochs stay below 2^28, and a word a u64 call left has flag bits at 2^28 or 2^29 of
-// the u32 epoch field, so it never reads as published.
+// per-tile scan: 2 reads + 1 write). A single-pass look-back form as for u32 measured slower
+// (config C probe + unnest 0.820-0.827 against 0.813 ms, r04p: the look-back chain across XCDs
+// costs more than the two extra launches) and was removed.
 #include "hj3d_internal.hpp"
 
 namespace hj3d {
 namespace {
 
 constexpr int kScanItems = 16;
-#ifndef HJ3D_SCAN64_LB
-#define HJ3D_SCAN64_LB 0  // u64 scans: 1 = one-pass decoupled look-back (A/B: config C probe + unnest phase
-                          // 0.813 ms with the three-launch reduce-then-scan, 0.820-0.827 with it; r04p)
-#endif
 constexpr int kTile = kBlock * kScanItems;  // 4096
 
 template <typename T>
@@ -202,88 +196,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_lb(const uint32_t* in, uint32_t
   }
 }
 
-// u64 form of k_scan_lb: status word = flag << 62 | value (values < 2^62), cleared before every call
-// (no room for an epoch), so one fill + one scan launch instead of reduce-then-scan's three.
-constexpr uint64_t kLb64Agg = 1ull << 62, kLb64Inc = 2ull << 62, kLb64Val = (1ull << 62) - 1;
-__device__ __forceinline__ uint64_t lb_exclusive64(const uint64_t* status, uint32_t t) {
-  const int lane = threadIdx.x & 63;
-  uint64_t excl = 0;
-  int64_t hi = int64_t(t) - 1;
-  while (hi >= 0) {
-    const int64_t q = hi - lane;
-    const uint64_t w = q >= 0 ? __hip_atomic_load(status + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kLb64Inc;
-    const uint32_t f = uint32_t(w >> 62);
-    const uint64_t inc = __ballot(f == 2u), nready = __ballot(f == 0u);
-    const int fi = inc ? __ffsll((unsigned long long)inc) - 1 : 63;  // nearest inclusive (or the whole step)
-    const uint64_t need = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
-    if (nready & need) continue;  // a predecessor in range has not published yet: read again
-    uint64_t v = lane <= fi ? (w & kLb64Val) : 0ull;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    excl += v;
-    if (inc) break;
-    hi -= 64;
-  }
-  return excl;
-}
-
-__global__ __launch_bounds__(kBlock) void k_scan_lb64(const uint64_t* in, uint64_t* out, uint64_t n,
-                                                      uint64_t* __restrict__ status, uint32_t* __restrict__ ticket,
-                                                      uint32_t ntiles) {
-  __shared__ uint64_t lds[kBlock / kWave];
-  __shared__ uint64_t tile[kScanPad];
-  __shared__ uint32_t tid_s;
-  __shared__ uint64_t pre_s;
-  if (threadIdx.x == 0) tid_s = atomicAdd(ticket, 1u);
-  __syncthreads();
-  const uint32_t t = tid_s;
-  const uint64_t base = uint64_t(t) * kTile;
-#pragma unroll
-  for (int j = 0; j < kScanItems; ++j) {
-    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
-    tile[scan_slot(k)] = base + k < n ? in[base + k] : 0ull;
-  }
-  __syncthreads();
-  uint64_t v[kScanItems];
-  uint64_t local = 0;
-#pragma unroll
-  for (int j = 0; j < kScanItems; ++j) {
-    v[j] = tile[scan_slot(threadIdx.x * kScanItems + j)];
-    local += v[j];
-  }
-  uint64_t total;
-  uint64_t pre = block_excl_scan(local, lds, &total);
-  const int wid = threadIdx.x >> 6;
-  if (threadIdx.x == 0)
-    __hip_atomic_store(status + t, (t == 0 ? kLb64Inc : kLb64Agg) | total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (wid == 0 && t > 0) {  // the first wave looks back over the tiles taken before this one
-    const uint64_t excl = lb_exclusive64(status, t);
-    if (threadIdx.x == 0) {
-      __hip_atomic_store(status + t, kLb64Inc | (excl + total), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      pre_s = excl;
-    }
-  } else if (threadIdx.x == 0) {
-    pre_s = 0;
-  }
-  if (threadIdx.x == 0 && t == ntiles - 1) {
-    out[n] = pre_s + total;
-    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // every ticket is taken
-  }
-  __syncthreads();
-  pre += pre_s;
-#pragma unroll
-  for (int j = 0; j < kScanItems; ++j) {
-    tile[scan_slot(threadIdx.x * kScanItems + j)] = pre;
-    pre += v[j];
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < kScanItems; ++j) {
-    const uint32_t k = uint32_t(j) * kBlock + threadIdx.x;
-    if (base + k < n) out[base + k] = tile[scan_slot(k)];
-  }
-}
-
 template <typename T>
 hipError_t excl_scan(hj3d_ctx* ctx, const T* in, T* out, uint64_t n, hipStream_t s) {
   if (n == 0) return hipMemsetAsync(out, 0, sizeof(T), s);
@@ -374,20 +286,7 @@ hipError_t exclusive_scan_u32(hj3d_ctx* ctx, const uint32_t* in, uint32_t* out, 
   return hipGetLastError();
 }
 hipError_t exclusive_scan_u64(hj3d_ctx* ctx, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s) {
-  if (n == 0) return hipMemsetAsync(out, 0, sizeof(uint64_t), s);
-  const uint64_t tiles = (n + kTile - 1) / kTile;
-  if (!HJ3D_SCAN64_LB || tiles >= (1ull << 31)) return excl_scan<uint64_t>(ctx, in, out, n, s);
-  // values and sums must stay below 2^62 (the status word's value field): output counts and
-  // offsets of one probe are far below that
-  DevBuf& st = ctx->scan_status;
-  hipError_t e = st.ensure(tiles * sizeof(uint64_t));
-  if (e == hipSuccess) e = hipMemsetAsync(st.p, 0, tiles * sizeof(uint64_t), s);  // (epoch 0 for the u32 form)
-  if (e == hipSuccess) e = ctx->ensure_ctl();
-  if (e != hipSuccess) return e;
-  uint32_t* ticket = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + kCtlScanTicket);
-  hipLaunchKernelGGL(k_scan_lb64, dim3(unsigned(tiles)), dim3(kBlock), 0, s, in, out, n, st.as<uint64_t>(), ticket,
-                     uint32_t(tiles));
-  return hipGetLastError();
+  return excl_scan<uint64_t>(ctx, in, out, n, s);
 }
 
 namespace {

@@ -287,7 +287,8 @@ def exp4_join(ctx, plan: str, R: torch.Tensor, S: torch.Tensor, T: torch.Tensor,
     every rank returns the single-table result."""
     import hj3d
     from .plans import EXP4_SUM
-    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    # the ranks of the exchange: libhj3d's communicator when one is set (use_comm), else the group's
+    rank, world = (_comm.rank, _comm.world) if _comm is not None else (dist.get_rank(group), dist.get_world_size(group))
     kind = hj3d.HJ3D_NESTED if plan == "Ndu" else hj3d.HJ3D_CHAIN
     dev = R.device
     rels = [hj3d.Rel(R, 0, row_base=row_base[0]), hj3d.Rel(S, 1, row_base=row_base[1]),

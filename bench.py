@@ -44,10 +44,37 @@ STAT_KEYS = ("nb", "empty", "entries", "distinct", "cc0_min", "cc0_max", "cc0_su
 OUT_KEYS = ("n", "sum_a", "sum_b", "sum_h", "xor_h")
 
 
-def latest_pmc():
+def lib_sha16():
+    """sha256 (16 hex digits) of the libhj3d.so this process loads (HJ3D_LIB or the in-tree build)."""
+    import hashlib
+    path = os.environ.get("HJ3D_LIB") or os.path.join(ROOT, "3d-hashjoin_amd", "lib", "libhj3d.so")
+    try:
+        with open(path, "rb") as fh:
+            return hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        return None
+
+
+def pmc_candidates(pattern):
+    """PMC summaries under profiles/ matching `pattern`, best first: one taken on the library this
+    process runs (its lib_sha16), then the most recently collected (collected_unix), then by name."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc.json")))
-    return files[-1] if files else ""
+    me = lib_sha16()
+    rows = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", pattern)):
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        rows.append((d.get("lib_sha16") == me and me is not None, d.get("collected_unix", 0), path))
+    return [p for _, _, p in sorted(rows, reverse=True)]
+
+
+def latest_pmc():
+    files = [p for p in pmc_candidates("r*_pmc.json") if not os.path.basename(p).split("_pmc")[0].endswith(
+        ("_C", "_E", "_Dsh", "_D_shards"))]
+    return files[0] if files else ""
 
 
 def parse():
@@ -717,6 +744,7 @@ def main():
                 traffic = (pmc.get(dom) or {}).get("traffic_bytes_per_launch")
         except (OSError, ValueError):
             traffic = None
+    pmc_src = os.path.relpath(args.pmc_json, ROOT) if pmc else None
     if pmc:
         for k in kernels:
             if k in pmc:
@@ -735,6 +763,26 @@ def main():
         workload = (f"config D: exp1 key/FK plan {plan}, |R|={nR_tot} |S|={nS_tot} in total over {world} GPU(s) "
                     f"(|R|={nR} |S|={nS} on rank 0), uniform FKs, b={args.b}")
 
+    # The roofline's unit. Unique chaining (Csr): the longer of the two timed probe-phase kernels, which
+    # are the step's largest. The 3D plans: the step's largest kernels are the build's aggregation
+    # (k_nagg) and the unnest expansion (k_expand_light), which carry no per-kernel timers, so the line
+    # is bounded on the probe + unnest PHASE (SURVEY §8(d) bytes) and reports the build phase beside it;
+    # the timed partition / probe kernels stay under roofline.kernels.
+    if unique:
+        roof = {"bound": "hbm", "achieved": kernels[dom]["achieved_GBs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": kernels[dom]["frac"], "traffic": traffic, "kernel": dom,
+                "kernel_avg_ms": kernels[dom]["avg_ms"], "alg_bytes_per_launch": kernels[dom]["alg_bytes"]}
+    else:
+        # build: read the 12-B tuple, write the (hash, row) pair, read it back, write the 4-B sub row
+        build_alg = (nB if sharded else (nS_tot if plan.startswith("Nrs") else nR_tot) // world) * (12 + 8 + 8 + 4)
+        roof = {"bound": "hbm", "achieved": phase_alg / (probe_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                "frac": phase_alg / (probe_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                "kernel": "phase (probe + unnest)", "alg_bytes_per_launch": phase_alg,
+                "note": "3D plan: the step's largest kernels (k_nagg in the build, k_expand_light in the unnest) "
+                        "have no per-kernel timers; the line is bounded on the probe + unnest phase",
+                "build_phase": {"ms": build_ms, "alg_bytes": build_alg,
+                                "achieved_GBs": build_alg / (build_ms * 1e-3) / 1e9,
+                                "frac": build_alg / (build_ms * 1e-3) / 1e9 / PEAK_HBM_GBS}}
     line = {
         "metric": metric,
         "value": nS_tot / (probe_ms * 1e-3),  # |S| probe tuples (Csr) = |S| output pairs (every plan)
@@ -769,9 +817,7 @@ def main():
         "join_tuples_per_s": nS_tot / ((build_ms + probe_ms) * 1e-3),
         "input_generation_s": gen_s,
         "roofline": {
-            "bound": "hbm", "achieved": kernels[dom]["achieved_GBs"], "peak": PEAK_HBM_GBS, "unit": "GB/s",
-            "frac": kernels[dom]["frac"], "traffic": traffic,
-            "kernel": dom, "kernel_avg_ms": kernels[dom]["avg_ms"], "alg_bytes_per_launch": kernels[dom]["alg_bytes"],
+            **roof,
             "kernels": kernels,
             "kernel_timing": ("HIP events riding on the kernels' dispatches over K kernel-timing steps after the "
                               "(uninstrumented) timed steps" if instrumented else
@@ -788,6 +834,9 @@ def main():
         "verification": verify,
         "verified_bit_exact": verified,
     }
+    if pmc_src:
+        line["roofline"]["pmc_source"] = pmc_src
+        line["roofline"]["pmc_same_library"] = pm.get("lib_sha16") is not None and pm.get("lib_sha16") == lib_sha16()
     _with_copy_peak(line["roofline"], copy_peak(torch, ctx, dev))
     pp = line["roofline"]["probe_phase"]
     if line["roofline"].get("copy_peak_GBs"):
@@ -852,9 +901,7 @@ def reference_columns_cached(nR, nS, maker, barrier):
 
 def _load_pmc(path, workload):
     """The PMC summary at `path` if it was taken on `workload` (scripts/pmc_summary.py)."""
-    import glob
-    cands = ([path] if path else []) + sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{workload}_pmc.json")),
-                                              reverse=True)
+    cands = ([path] if path else []) + pmc_candidates(f"r*_{workload}_pmc.json")
     pm = None
     for path in cands:
         try:
@@ -868,6 +915,7 @@ def _load_pmc(path, workload):
     if pm is None:
         return None
     pm["_path"] = os.path.relpath(path, os.path.dirname(os.path.abspath(__file__)))
+    pm["_same_library"] = pm.get("lib_sha16") is not None and pm.get("lib_sha16") == lib_sha16()
     return pm
 
 
@@ -1049,6 +1097,7 @@ def main_single_config(args):
             k: {"traffic": v, "fetch": pm["kernels"][k].get("fetch_bytes"), "write": pm["kernels"][k].get("write_bytes")}
             for k, v in tr.items() if k in ph_build + ph_probe}
         line["roofline"]["pmc_source"] = pm.get("_path")
+        line["roofline"]["pmc_same_library"] = pm.get("_same_library")
     _with_copy_peak(line["roofline"], copy_peak(torch, ctx, dev), keys=("achieved", "build_achieved"))
     if args.workload == "C" and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_reference_nrs(max(nR // 10, 1), max(nS // 10, 1), args.theta,

@@ -187,12 +187,8 @@ enum {
    * e.g. config D's 1e8-bucket Nrs table) whenever it applies, not only above 2048 partitions
    * (tests). Region overflow (skewed keys) falls back to the sort build. */
   HJ3D_OPT_NESTED_PK = 11,
-  /* HJ3D_OPT_PK_COMPACT (0/1, default 0): the packed unique probe stages its table slices as a
-   * compact image (16-bit bucket starts, one word per entry: ~6 B per bucket instead of 12) and runs
-   * two 512-thread workgroups per CU, where the table's build rows are implicit (a known row range)
-   * and the slice fits. Measured slower at config B (0.61 against 0.49 ms), so off by default; kept
-   * for A/B measurements and its parity test. */
-  HJ3D_OPT_PK_COMPACT = 12,
+  /* 12: reserved (a compact slice image for the packed probe, measured slower: 0.61 against 0.49 ms
+   * at config B; removed in round 6) */
   /* HJ3D_OPT_SYNC_BUILD (0/1, default 0): hj3d_build / hj3d_build_many finish a nested table before
    * they return (they wait for its counts and run the sort build there if the LDS aggregation build
    * gave up), so the build relation's device memory may be released as soon as the call returns.

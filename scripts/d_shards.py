@@ -53,7 +53,8 @@ def main():
     gen_s = time.perf_counter() - t0
     ctx = hj3d.Context(0)
     # NB of the plans built on S.a: #dv(S.a) by the distributed pre-pass (per-rank bitmaps, OR-merge)
-    dv = hj3d.num_distinct_sharded(ctx, hj3d.Rel(S, key_word=1), nR, a.parts) if a.plan.startswith("Nrs") else 0
+    dv = (hj3d.num_distinct_sharded(ctx, hj3d.Rel(S, key_word=1), nR, a.parts)
+          if hj3d.EXP1_PLANS[a.plan][1] == "S" else 0)
     nb = hj3d.num_buckets_exp1(a.plan, nR, dv, 1)
     out = torch.empty((nS, 2), dtype=torch.int32, device="cuda") if a.plan in ("Csr", "Nrs") else None
     sp = a.xpart == "single"
@@ -97,18 +98,27 @@ def main():
         owners.append(d)
     part_ms = avg("partition", "partition")
     pb_ms, pp_ms = avg("partition", "partition_build"), avg("partition", "partition_probe")
+    # the plan's sides (Csr / Nsr build on R and probe S; Crs / Nrs / NrsNU build on S.a and probe R)
+    # and the partitioners' algorithmic bytes per tuple: the stable two-pass hj3d_partition reads the
+    # 12-B tuple twice and writes the 8-B pair (32 B), the single-pass strided one reads once (20 B)
+    n_build, n_probe = (nR, nS) if hj3d.EXP1_PLANS[a.plan][1] == "R" else (nS, nR)
+    bpt_build, bpt_probe = 32, (20 if sp else 32)
     line = {
         "what": f"config D {a.parts}-owner split emulated on one GPU, plan {a.plan}: per-rank compute at the "
                 f"{a.parts}-GPU geometry, owners run one after another; exchange (xGMI) NOT included; not a "
                 "scaling number",
         "nR": nR, "nS": nS, "num_buckets": nb, "num_dv_Sa": dv or None, "reps": a.reps, "input_generation_s": gen_s,
         "exchange_partition_ms_both_relations": part_ms,
-        "exchange_partition_frac": ((nR + nS) * 20) / (part_ms * 1e-3) / 1e9 / PEAK if part_ms else None,
+        "build_side_tuples": n_build, "probe_side_tuples": n_probe,
+        "exchange_partition_bytes_per_tuple": {"build": bpt_build, "probe": bpt_probe},
+        "exchange_partition_frac": ((n_build * bpt_build + n_probe * bpt_probe) / (part_ms * 1e-3) / 1e9 / PEAK
+                                    if part_ms else None),
         "exchange_partitioner_probe_side": ("single-pass hj3d_partition_strided" if sp else
                                             "stable two-pass hj3d_partition"),
         "exchange_partition_build_ms": pb_ms,
         "exchange_partition_probe_ms": pp_ms,
-        "exchange_partition_probe_frac": (nS * 20) / (pp_ms * 1e-3) / 1e9 / PEAK if pp_ms else None,
+        "exchange_partition_build_frac": (n_build * bpt_build) / (pb_ms * 1e-3) / 1e9 / PEAK if pb_ms else None,
+        "exchange_partition_probe_frac": (n_probe * bpt_probe) / (pp_ms * 1e-3) / 1e9 / PEAK if pp_ms else None,
         "owners": owners,
         "max_owner_probe_ms": max(o["probe_ms"] for o in owners),
         "max_owner_build_ms": max(o["build_ms"] for o in owners),

@@ -4,7 +4,8 @@
 clear, pass A, main records, pass B) and how the partitions' start times spread over the launch.
 
 --workload E: config E's two tables in one build_many (1024 partitions of 3072 buckets);
---workload C: one table over 1e8 Zipf-0.8 keys (config C's build). Prints one JSON object: the
+--workload C: one table over 1e8 Zipf-0.8 keys (config C's build); --workload D: 1e9 uniform keys over
+1e8 (config D's Nrs build, on the packed slices: 65,104 partitions). Prints one JSON object: the
 median / p90 microseconds of every phase over the partitions, the launch span, and the workgroups'
 start-time deciles."""
 import argparse
@@ -19,7 +20,7 @@ sys.path.insert(0, os.path.join(ROOT, "3d-hashjoin_amd", "python"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--workload", default="E", choices=["C", "E"])
+    ap.add_argument("--workload", default="E", choices=["C", "D", "E"])
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
     import numpy as np
@@ -41,6 +42,18 @@ def main():
         def build():
             ctx.build_many([ts, tt], [relS, relT])
             return ts
+    elif a.workload == "D":  # config D's Nrs build shape: 1e9 uniform FKs over 1e8 keys (device generator)
+        S = torch.zeros((1_000_000_000, 3), dtype=torch.int32, device=dev)
+        ctx.gen_keys(S, 0, 0, 0, 0)
+        ctx.gen_fk(S, 1, 0, 100_000_000, 13)
+        relS = hj3d.Rel(S, key_word=1)
+        dv = ctx.num_distinct(relS, 100_000_000)
+        t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, dv)
+        t.reserve(S.shape[0])
+
+        def build():
+            t.build(relS)
+            return t
     else:
         R, S = hj3d.exp1_relations_ref(10_000_000, 100_000_000, True, 0.8, 0, device=dev)
         relS = hj3d.Rel(S, key_word=1)
@@ -75,6 +88,13 @@ def main():
                               "max": round(float(tot.max()), 2)}
     starts = us(x[:, 0] - t0)
     out["start_deciles_us"] = [round(float(np.percentile(starts, q)), 1) for q in range(0, 101, 10)]
+    ends = us(x[:, 5] - t0)
+    out["end_deciles_us"] = [round(float(np.percentile(ends, q)), 1) for q in range(0, 101, 10)]
+    # the longest workgroups (heavy partitions): start, total and pass times (last round), us
+    top = np.argsort(-tot)[:8]
+    out["longest"] = [{"start": round(float(starts[i]), 1), "total": round(float(tot[i]), 1),
+                       "pass_A": round(float(us(x[i, 2] - x[i, 1])), 1), "pass_B": round(float(us(x[i, 4] - x[i, 3])), 1)}
+                      for i in top]
     print(json.dumps(out))
 
 

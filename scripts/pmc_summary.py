@@ -113,8 +113,18 @@ def main():
             d["wait_frac"] = d.get("SQ_WAIT_ANY", 0) / wc
             d["issue_stall_frac"] = d.get("SQ_WAIT_INST_ANY", 0) / wc
             d["active_frac"] = d.get("SQ_ACTIVE_INST_ANY", 0) / wc
+    # which library the counters were taken on (bench.py prefers the summary of the library it runs)
+    import hashlib
+    import time
+    lib_path = os.environ.get("HJ3D_LIB") or os.path.join(ROOT, "3d-hashjoin_amd", "lib", "libhj3d.so")
+    try:
+        with open(lib_path, "rb") as fh:
+            lib_sha16 = hashlib.sha256(fh.read()).hexdigest()[:16]
+    except OSError:
+        lib_sha16 = None
     out = {
         "tag": a.tag, "workload": a.workload, "nR": a.nR, "nS": a.nS, "emit": bool(a.emit),
+        "lib_sha16": lib_sha16, "collected_unix": int(time.time()),
         "command": "rocprofv3 --pmc <group> --kernel-trace -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline"
                    + ("" if a.workload == "B" else f" --workload {a.workload}"),
         "corrections": "FETCH_SIZE, WRITE_SIZE in KiB; FETCH_SIZE x2 (every read request is 128 B, counted as "

@@ -18,7 +18,6 @@ def main():
     ap.add_argument("--nS", type=float, default=1e8)
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--no-emit", action="store_true")
-    ap.add_argument("--compact", type=int, default=0, help="HJ3D_OPT_PK_COMPACT (the probe's compact slice image)")
     ap.add_argument("--layout", default="tuples", choices=["tuples", "pairs", "tuples_rows"],
                     help="probe side: 12-B tuples with implicit rows (config B), received {key, row} pairs "
                          "(8 B, explicit rows: a rank of the multi-GPU strand), or 12-B tuples with an explicit row word")
@@ -29,7 +28,6 @@ def main():
     import hj3d
     nR, nS = int(a.nR), int(a.nS)
     ctx = hj3d.Context(0)
-    ctx.pk_compact(bool(a.compact))
     R = torch.zeros((nR, 3), dtype=torch.int32, device="cuda")
     S = torch.zeros((nS, 3), dtype=torch.int32, device="cuda")
     ctx.gen_keys(R, 0, 0, nR, 11)
@@ -67,7 +65,7 @@ def main():
         t.build(relR)
         probe_all()
     ctx.sync()
-    res = {"label": a.label, "compact": a.compact, "layout": a.layout, "nR": nR, "nS": nS, "emit": out is not None,
+    res = {"label": a.label, "layout": a.layout, "nR": nR, "nS": nS, "emit": out is not None,
            "chunks": a.chunks}
     for k, ph in (("build", hj3d.T_BUILD), ("probe", hj3d.T_PROBE), ("k_pk_part", hj3d.T_SCATTER),
                   ("k_pk_split", hj3d.T_HIST), ("k_pk_probe", hj3d.T_PROBE_KERNEL)):

@@ -257,26 +257,15 @@ def test_rccl_exp4_strand_equals_reference(ctx, comm, plan):
     communicator at world size 1: R, S, T co-partitioned, counts in one collective, three
     asynchronous pair exchanges, one hj3d_build_many, hj3d_probe2, counters all-reduced; equal to the
     reference binary's fixture exp4_R16_a3_A4_b2_B2."""
-    import torch.distributed as dist
     import hj3d
     from hj3d import dist as hdist
     g = _exp4_fixture()
     R, S, T = hj3d.exp4_relations_ref(*g["generator_args"][1:6])
-    own_group = not dist.is_initialized()
-    if own_group:  # exp4_join reads rank / world from torch.distributed (gloo, this process alone)
-        import socket
-        s = socket.socket()
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-        s.close()
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
-    hdist.use_comm(comm)
+    hdist.use_comm(comm)  # (rank and world size from the communicator)
     try:
         got = hdist.exp4_join(ctx, plan, R, S, T, g["nb"])
     finally:
         hdist.use_comm(None)
-        if own_group:
-            dist.destroy_process_group()
     _exp4_check(plan, got, g["plans"][plan])
 
 
@@ -309,12 +298,9 @@ def test_exp4_two_rank_rehearsal_equals_reference():
     """hj3d.dist.exp4_join with two ranks on this one GPU (gloo, the exchange staged through host
     memory; RCCL allows one rank per device): each rank holds half of R, S and T, and both ranks'
     all-reduced results equal the reference binary's fixture."""
-    import socket
     import torch.multiprocessing as mp
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
+    port = 29641  # (a fixed port, as the bench rehearsals above use: the RCCL communicator of this
+    # process opens ephemeral sockets of its own)
     mpc = mp.get_context("spawn")
     q = mpc.Queue()
     procs = [mpc.Process(target=_exp4_rank, args=(r, port, q)) for r in range(2)]

@@ -476,53 +476,6 @@ def test_packed_probe_items_per_lane(ctx, items):
         ctx.radix_min(1 << 20)
 
 
-@pytest.mark.parametrize("nR,nb,nS", [(1_000_000, 1_000_000, 4_000_000), (1_000_003, 1_000_033, 3_000_017),
-                                      (65_537, 65_537, 2_000_000)])
-def test_packed_probe_compact_image_equals_full(ctx, nR, nb, nS):
-    """The compact slice image of the packed probe (16-bit bucket starts, one word q * rr + row per
-    entry, two 512-thread workgroups per CU) gives the full image's counters and output pairs, and
-    the oracle's -- including the buckets that hold an entry too wide for a word (q = q_max with a
-    large row, stored as a never-matching word): probes into them are redone against the table in
-    HBM. The first case has ~7 such entries and ~28 probes into their buckets."""
-    import torch
-    import hj3d
-    rng = np.random.default_rng(nR + nS)
-    Rk = rng.permutation(nR).astype(np.uint32)
-    Sa = rng.integers(0, nR, nS).astype(np.uint32)
-    R = O.tuples3(Rk, np.zeros_like(Rk))
-    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
-    # the words that do not fit: q = floor(h / nb) = q_max and q * nR + row >= 2^32 - 1
-    h = _fmix32_u64(Rk)
-    qmax = 0xFFFFFFFF // nb
-    wide = int(np.sum((h // nb == qmax) & (qmax * nR + np.arange(nR, dtype=np.uint64) >= 0xFFFFFFFF)))
-    e = O.chain_plan(R, 0, S, 1, nb, True)
-    dR, dS = dev(R), dev(S)
-    got = {}
-    try:
-        for compact in (True, False):
-            ctx.pk_compact(compact)
-            out = torch.zeros((nS, 2), dtype=torch.int32, device="cuda")
-            g = hj3d.exp1_plan(ctx, "Csr", dR, dS, nb, out=out, stats=False)
-            host = out.cpu().numpy().view(np.uint32)
-            got[compact] = (g["c_probe"], g["c_cmp"], g["c_top"], g["out"], host_checksums(host))
-    finally:
-        ctx.pk_compact(False)
-    assert got[True] == got[False]
-    assert got[True][:3] == (e.c_probe, e.c_cmp, e.c_top) and got[True][3] == e.out
-    if nR == 1_000_000:
-        assert wide > 0
-
-
-def _fmix32_u64(x):
-    x = x.astype(np.uint64)
-    x ^= x >> np.uint64(16)
-    x = (x * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
-    x ^= x >> np.uint64(13)
-    x = (x * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
-    x ^= x >> np.uint64(16)
-    return x
-
-
 @pytest.mark.parametrize("sync", [False, True], ids=["lazy", "sync"])
 @pytest.mark.parametrize("dense", [0, 1])
 def test_build_many_one_table_gives_up(ctx, dense, sync):
