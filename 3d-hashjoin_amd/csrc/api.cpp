@@ -186,7 +186,6 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
   switch (option) {
     case HJ3D_OPT_FORCE_DIRECT: ctx->force_direct = value != 0; return HJ3D_OK;
     case HJ3D_OPT_RADIX_MIN: ctx->radix_min = value < 0 ? 0 : uint64_t(value); return HJ3D_OK;
-    case HJ3D_OPT_NESTED_RADIX: ctx->nested_radix = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_SORT: ctx->nested_sort = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SEL_UNFUSED: ctx->sel_unfused = value != 0; return HJ3D_OK;
     case HJ3D_OPT_PACKED_PROBE: ctx->pk_off = value == 0; return HJ3D_OK;
@@ -403,8 +402,7 @@ hj3d_status hj3d_build_many(hj3d_ctx* ctx, hj3d_table* const* tables, const hj3d
   }
   // two nested tables of one geometry: one launch sequence (the aggregation build over both)
   if (count == 2 && tables[0]->desc.kind == HJ3D_NESTED && tables[1]->desc.kind == HJ3D_NESTED &&
-      !ctx->nested_sort && !ctx->nested_pk && !nested_radix_applicable(ctx, tables[0], builds[0].n) &&
-      !nested_radix_applicable(ctx, tables[1], builds[1].n)) {
+      !ctx->nested_sort && !ctx->nested_pk) {
     hipError_t e;
     const char* path = "nested_agg";
     {
@@ -464,11 +462,9 @@ static hipError_t build_one(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel* build)
     }
     if (e == hipSuccess && !sorted) e = sort_small_buckets(ctx, t, ctx->stream);
   } else {
-    t->path = "nested_radix";
-    e = nested_radix_applicable(ctx, t, build->n) ? nested_build_radix(ctx, t, *build, ctx->stream)
-                                                  : hipErrorNotSupported;
+    e = hipErrorNotSupported;
     bool agg = false;
-    if (e == hipErrorNotSupported && !ctx->nested_sort) {
+    if (!ctx->nested_sort) {
       e = nested_host_counts(t);
       if (e == hipSuccess) e = nested_build_agg(ctx, t, *build, ctx->stream, &t->path);
       if (e == hipErrorOutOfMemory) {  // partition / slice scratch did not fit: the sort build

@@ -88,7 +88,6 @@ struct hj3d_ctx {
   int timing = 0;  // hj3d_ctx_timing: 0 off, 1 every timer, 2 dispatch-carried kernel spans only
   bool force_direct = false;  // HJ3D_OPT_FORCE_DIRECT: never use the radix-partitioned paths
   uint64_t radix_min = 1u << 20;  // HJ3D_OPT_RADIX_MIN: smallest input that takes the radix paths
-  bool nested_radix = false;      // HJ3D_OPT_NESTED_RADIX
   bool nested_sort = false;       // HJ3D_OPT_NESTED_SORT
   bool sel_unfused = false;       // HJ3D_OPT_SEL_UNFUSED
   hj3d::DevBuf sel;               // hj3d_probe_sel: passing (key, row) pairs when not fused
@@ -391,10 +390,6 @@ hipError_t nested_build_agg(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hip
 // both relations partitioned, one k_nagg grid over both tables' partitions, one scan, one compaction.
 hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* t, const hj3d_rel* r, uint32_t nt, hipStream_t s,
                                  const char** path = nullptr);
-// nested_radix.hip: nested build from the radix-partitioned bucket CSR (large inputs);
-// hipErrorNotSupported when a bucket holds too many distinct keys (use nested_build).
-bool nested_radix_applicable(const hj3d_ctx* ctx, const hj3d_table* t, uint64_t n);
-hipError_t nested_build_radix(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s);
 hipError_t nested_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t flags, void* out,
                         uint64_t out_cap, uint64_t* res_dev, hipStream_t s);
 // partitioned nested probe (every mode of nested_probe); needs t->n_mains

@@ -59,8 +59,8 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_WHOLE
 #define HJ3D_NAGG_WHOLE 1  // a round over the partition's whole bucket range skips the per-pair range test (0: A/B)
 #endif
-#ifndef HJ3D_NAGG_STATIC
-#define HJ3D_NAGG_STATIC 1  // fixed load / store counts per pass step (0: A/B, the guarded form)
+#ifndef HJ3D_NAGG_PKWAVE
+#define HJ3D_NAGG_PKWAVE 1  // slices: each wave walks whole fine regions (0: every lane searches its item's region)
 #endif
 #ifndef HJ3D_NAGG_PKW
 #define HJ3D_NAGG_PKW 1536  // buckets per partition on the packed slices (0: the kAggW-based width).
@@ -91,6 +91,12 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
 #endif
 
+#ifndef HJ3D_NAGG_CAPF
+#define HJ3D_NAGG_CAPF 2.5  // small form: LDS table slots per bucket of the partition (+ the insert slack)
+#endif
+#ifndef HJ3D_NAGG_HOT
+#define HJ3D_NAGG_HOT 1  // heavy partitions: the hot key's rows on the register path (0: A/B)
+#endif
 #ifndef HJ3D_NAGG_ELECT
 #define HJ3D_NAGG_ELECT 2  // hot-key wave leader election: 2 partitions above 5/4 of the mean size (default), 1 every partition, 0 none
 #endif
@@ -208,7 +214,7 @@ __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
 // SLOTS >= cap / BLOCK: table slots per thread in the per-slot loops.
 constexpr uint32_t kAggMaxS2 = 16;  // fine regions per slice (pk_slices)
 __host__ __device__ constexpr uint32_t agg_lds_words(uint32_t cap, uint32_t W, int block) {
-  return 3 * cap + W + uint32_t(block / 64) + 2 + kAggMaxS2 + 2;
+  return 3 * cap + W + uint32_t(block / 64) + 2 + kAggMaxS2 + 2 + 2 * uint32_t(block / 64) + 2;
 }
 // PK: the partition's pairs are slice p's fine regions (pk_slices), packed words as keys.
 struct NaggSrc {
@@ -245,6 +251,11 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   uint32_t& nkeys = wsum[BLOCK / kWave];
   uint32_t& ovf = wsum[BLOCK / kWave + 1];
   uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
+  // hot key of a heavy partition: per-wave hot rows (then their exclusive prefix) and min rows, the
+  // key's slot and its rows' total
+  uint32_t* hotw = rstart + kAggMaxS2 + 2;
+  uint32_t* hotm = hotw + BLOCK / kWave;
+  uint32_t& hslot = hotm[BLOCK / kWave];
   const uint32_t limit = cap - BLOCK - 64;
   const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
   const uint32_t p = gp - ti * tabs.P;                      // partition inside table ti
@@ -282,47 +293,134 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     if constexpr (PK) return src.pk.hash_of(x, p);
     else return x;
   };
-  // PK: per-lane cursor over the S2 fine regions (a thread's item indices only grow inside a pass)
-  uint32_t cr = 0, nst = 0;
+  uint32_t cr = 0, nst = 0;  // (contiguous PK form: the lane's region cursor)
   const uint2* rsrc = nullptr;
-  const auto restart = [&]() __attribute__((always_inline)) {
-    if constexpr (PK) {
-      cr = 0;
-      nst = rstart[1];
-      rsrc = src.fine + uint64_t(p) * src.cap2;
-    }
-  };
-  // kAggU pairs per thread of the partition's stream from f0 (coalesced: item f0 + u * BLOCK + tid)
-  // HJ3D_NAGG_STATIC: every call issues exactly kAggU loads per lane (indices clamped to the last
-  // pair; callers only load when total > 0), so the compiler can wait for the batch in flight with a
-  // counted s_waitcnt at its use instead of vmcnt(0) right after issuing it (a data-dependent number
-  // of loads, or of stores in pass B, made every step wait for the next step's loads)
-  const auto load = [&](uint32_t f0, uint2 (&v)[kAggU]) __attribute__((always_inline)) {
+  // The passes stream the partition's pairs in steps of kAggU items per lane, the next step's loads
+  // in flight. Every step issues exactly kAggU loads per lane (indices clamped to the last pair), so
+  // the compiler waits for the batch in flight with a counted s_waitcnt at its use, not vmcnt(0) right
+  // after issuing it (a data-dependent number of loads, or of stores in pass B, made every step wait
+  // for the next step's loads). Contiguous form: item i0 + u * BLOCK + tid of the partition.
+  // Slices (PK, HJ3D_NAGG_PKWAVE): wave w walks the fine regions w, w + waves, ... one after another,
+  // a step being kAggU x 64 consecutive items of one region, so no item searches for its region.
+  // body(v, valid): v the step's pairs, valid the bit mask of the lane's real items.
+  constexpr uint32_t kNw = BLOCK / kWave;
+  const uint32_t wid = threadIdx.x / kWave;
+  const auto stream = [&](auto&& body) __attribute__((always_inline)) {
+    uint2 v[kAggU], nv[kAggU];
+    if constexpr (PK && HJ3D_NAGG_PKWAVE) {
+      const auto rlen = [&](uint32_t r) __attribute__((always_inline)) { return rstart[r + 1] - rstart[r]; };
+      const auto skip = [&](uint32_t r) __attribute__((always_inline)) {  // the next non-empty region from r
+        while (r < src.S2 && rlen(r) == 0) r += kNw;
+        return r;
+      };
+      const auto wload = [&](uint32_t r, uint32_t q, uint2 (&x)[kAggU]) __attribute__((always_inline)) {
+        if (r >= src.S2) return;
+        const uint2* b = src.fine + (uint64_t(r) * src.pk.P + p) * src.cap2;
+        const uint32_t last = rlen(r) - 1;
 #pragma unroll
-    for (int u = 0; u < kAggU; ++u) {
-      const uint32_t f = HJ3D_NAGG_STATIC ? min(f0 + u * BLOCK + threadIdx.x, total - 1) : f0 + u * BLOCK + threadIdx.x;
-      if constexpr (PK) {
-        v[u] = make_uint2(0, 0);
-        if (HJ3D_NAGG_STATIC || f < total) {
-          while (f >= nst) {
-            ++cr;
-            nst = rstart[cr + 1];
-            rsrc = src.fine + (uint64_t(cr) * src.pk.P + p) * src.cap2;
-          }
-          v[u] = rsrc[f - rstart[cr]];
+        for (int u = 0; u < kAggU; ++u) x[u] = b[min(q + uint32_t(u) * kWave + uint32_t(lane), last)];
+      };
+      uint32_t r = skip(wid), q = 0;
+      wload(r, q, nv);
+      while (r < src.S2) {
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
+        const uint32_t len = rlen(r);
+        uint32_t valid = 0;
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) valid |= uint32_t(q + uint32_t(u) * kWave + uint32_t(lane) < len) << u;
+        q += kAggU * kWave;
+        if (q >= len) {
+          r = skip(r + kNw);
+          q = 0;
         }
-      } else {
-        v[u] = f < total ? pairs[e0 + f] : make_uint2(0, 0);
+        wload(r, q, nv);  // next step in flight
+        body(v, valid);
+      }
+    } else {
+      const auto load = [&](uint32_t f0, uint2 (&x)[kAggU]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) {
+          const uint32_t f = min(f0 + u * BLOCK + threadIdx.x, total - 1);
+          if constexpr (PK) {
+            while (f >= nst) {  // per-lane cursor over the fine regions (indices only grow in a pass)
+              ++cr;
+              nst = rstart[cr + 1];
+              rsrc = src.fine + (uint64_t(cr) * src.pk.P + p) * src.cap2;
+            }
+            x[u] = rsrc[f - rstart[cr]];
+          } else {
+            x[u] = pairs[e0 + f];
+          }
+        }
+      };
+      if constexpr (PK) {
+        cr = 0;
+        nst = rstart[1];
+        rsrc = src.fine + uint64_t(p) * src.cap2;
+      }
+      if (total) load(0, nv);
+      for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
+        load(i0 + BLOCK * kAggU, nv);  // next batch in flight
+        uint32_t valid = 0;
+#pragma unroll
+        for (int u = 0; u < kAggU; ++u) valid |= uint32_t(i0 + u * BLOCK + threadIdx.x < total) << u;
+        body(v, valid);
       }
     }
   };
   uint32_t mrun = 0, srun = 0, mxlen = 0;  // keys and rows of the finished rounds
   uint32_t c0 = 0, span = (nbs + kAggRounds - 1) / kAggRounds;
+  const uint32_t wid_ = threadIdx.x / kWave;
   while (c0 < nbs) {
     const uint32_t c1 = min(nbs, c0 + span);
     const bool whole = HJ3D_NAGG_WHOLE && c0 == 0 && c1 == nbs;
     // a key that no key of this round is: its bucket lies outside [b0 + c0, b0 + c1)
     const uint32_t empty = PK ? (c1 << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
+    // Hot key (HJ3D_NAGG_HOT; heavy partitions, one round over the whole range): a Zipf key holding
+    // most of a partition's rows (config C: 829 K of ~880 K) made its workgroup the launch's
+    // critical path (1.2 of 1.34 ms), each of its rows paying the wave-leader election in both
+    // passes. The key is found from BLOCK pairs sampled evenly over the partition (each wave votes for
+    // its lane 0's key; taken when its votes reach a quarter of the samples); its rows then take a
+    // register path: pass A counts them and their min row per lane (one table update per wave at the
+    // end), pass B places them at the key's range start + the wave's prefix (from pass A's per-wave
+    // counts: both passes walk the stream in one order) + a running ballot count: no LDS atomic.
+    uint32_t H = empty;
+    if (HJ3D_NAGG_HOT && elect && whole && total >= 4u * BLOCK) {
+      if constexpr (PK) __syncthreads();  // (the region starts written above)
+      const uint32_t f = uint32_t(uint64_t(total) * threadIdx.x / BLOCK);
+      uint32_t key;
+      if constexpr (PK) {
+        uint32_t r = 0;
+        while (r + 1 < src.S2 && f >= rstart[r + 1]) ++r;
+        key = src.fine[(uint64_t(r) * src.pk.P + p) * src.cap2 + (f - rstart[r])].x;
+      } else {
+        key = pairs[e0 + f].x;
+      }
+      const uint32_t cand = uint32_t(__builtin_amdgcn_readlane(int(key), 0));
+      const uint32_t votes = uint32_t(__popcll(__ballot(key == cand)));
+      if (lane == 0) {
+        hotw[wid_] = cand;
+        hotm[wid_] = votes;
+      }
+      __syncthreads();
+      uint32_t best = 0;
+#pragma unroll 1
+      for (int w = 0; w < BLOCK / kWave; ++w) {
+        uint32_t sc = 0;
+#pragma unroll 1
+        for (int w2 = 0; w2 < BLOCK / kWave; ++w2) sc += hotw[w2] == hotw[w] ? hotm[w2] : 0u;
+        if (sc > best) {
+          best = sc;
+          H = hotw[w];
+        }
+      }
+      if (best < BLOCK / 4) H = empty;
+      __syncthreads();  // (the scratch words are rewritten below)
+    }
+    const bool hot = H != empty;  // (uniform)
     for (uint32_t s = threadIdx.x; s < cap; s += BLOCK) {
       tkey[s] = empty;
       tcnt[s] = 0;
@@ -336,25 +434,14 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     __syncthreads();
     nagg_clk(gp, 1);
     // ---- pass A: count and min row per key ----
-    uint2 v[kAggU], nv[kAggU];
-    restart();
-    if (HJ3D_NAGG_STATIC) {
-      if (total) load(0, nv);
-#pragma unroll
-      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
-    } else {
-      load(0, v);
-    }
-    for (uint32_t i0 = 0; i0 < total; i0 += BLOCK * kAggU) {
-      if (HJ3D_NAGG_STATIC || i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
+    uint32_t hc = 0, hm = kInvalid;  // hot rows and their min row (this lane)
+    stream([&](const uint2 (&v)[kAggU], uint32_t valid) __attribute__((always_inline)) {
       // home slots of all items read together (one LDS latency for the batch); only items whose
-      // key is not in its home slot walk the probe sequence
-      // active items as one bit mask (a bool array was re-materialised from exec masks per item)
+      // key is not in its home slot walk the probe sequence; active items as one bit mask
       uint32_t actm = 0;
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * BLOCK + threadIdx.x;
         // one round over the whole range (the common case): every pair of the partition is in it,
         // so no bucket (a 64-bit multiply-high per pair on the modulo path) is computed
         bool inr = true;
@@ -362,13 +449,19 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           const uint32_t lb = lbk(v[u].x);
           inr = lb >= c0 && lb < c1;
         }
-        const bool a = i < total && inr;
+        const bool a = ((valid >> u) & 1u) && inr;
         actm |= uint32_t(a) << u;
         k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
       }
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
         bool a = (actm >> u) & 1u;
+        if (hot) {
+          const bool h = a && v[u].x == H;
+          hc += h;
+          hm = h ? min(hm, v[u].y) : hm;
+          a = a && !h;
+        }
         const uint64_t am = elect ? __ballot(a) : 0ull;
         if (am) {  // the wave's first active key, if several lanes hold it (a Zipf hot key)
           const int leader = __ffsll((unsigned long long)am) - 1;
@@ -399,8 +492,34 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           }
         }
       }
+    });
+    if (hot) {  // the hot key into the table: per-wave totals, then one insert
+      uint32_t c = hc;
 #pragma unroll
-      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, kWave);
+      const uint32_t m = wave_min_u32(hm);
+      if (lane == 0) {
+        hotw[wid_] = c;
+        hotm[wid_] = m;
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        uint32_t tot = 0, mn = kInvalid;
+        for (int w = 0; w < BLOCK / kWave; ++w) {  // -> the waves' exclusive prefix
+          const uint32_t x = hotw[w];
+          hotw[w] = tot;
+          tot += x;
+          mn = min(mn, hotm[w]);
+        }
+        const uint32_t sl = tot ? tab_insert(tkey, H, empty, &nkeys, cap, limit) : kInvalid;
+        if (tot && sl == kInvalid) {
+          ovf = 1;
+        } else if (tot) {
+          tcnt[sl] += tot;
+          tmin[sl] = min(tmin[sl], mn);
+        }
+        hslot = sl;
+      }
     }
     __syncthreads();
     nagg_clk(gp, 2);
@@ -449,30 +568,20 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     __syncthreads();
     nagg_clk(gp, 3);
     // ---- pass B: rows into their keys' sub ranges ----
-    restart();
-    if (HJ3D_NAGG_STATIC) {
-      if (total) load(0, nv);
-#pragma unroll
-      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
-    } else {
-      load(0, v);
-    }
-    for (uint32_t i0 = 0; i0 < (HJ3D_NAGG_DIAG == 2 ? 0u : total); i0 += BLOCK * kAggU) {
-      if (HJ3D_NAGG_STATIC || i0 + BLOCK * kAggU < total) load(i0 + BLOCK * kAggU, nv);  // next batch in flight
-      // active items as one bit mask (a bool array was re-materialised from exec masks per item)
+    // (hot key: its range start, from its slot's cursor, + this wave's prefix)
+    uint32_t hcur = hot && hslot != kInvalid ? tcnt[hslot] + hotw[wid_] : 0u;
+    if (HJ3D_NAGG_DIAG != 2)
+    stream([&](const uint2 (&v)[kAggU], uint32_t valid) __attribute__((always_inline)) {
       uint32_t actm = 0;
       uint32_t k0[kAggU];
 #pragma unroll
       for (int u = 0; u < kAggU; ++u) {
-        const uint32_t i = i0 + u * BLOCK + threadIdx.x;
-        // one round over the whole range (the common case): every pair of the partition is in it,
-        // so no bucket (a 64-bit multiply-high per pair on the modulo path) is computed
         bool inr = true;
         if (!whole) {
           const uint32_t lb = lbk(v[u].x);
           inr = lb >= c0 && lb < c1;
         }
-        const bool a = i < total && inr;
+        const bool a = ((valid >> u) & 1u) && inr;
         actm |= uint32_t(a) << u;
         k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
       }
@@ -480,6 +589,13 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       for (int u = 0; u < kAggU; ++u) {
         bool a = (actm >> u) & 1u;
         uint32_t* dst = tabs.sink;
+        if (hot) {
+          const bool h = a && v[u].x == H;
+          const uint64_t hm2 = __ballot(h);
+          if (h) dst = sub + hcur + uint32_t(__popcll(hm2 & lt));
+          hcur += uint32_t(__popcll(hm2));
+          a = a && !h;
+        }
         const uint64_t am = elect ? __ballot(a) : 0ull;
         if (am) {
           const int leader = __ffsll((unsigned long long)am) - 1;
@@ -499,12 +615,10 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           dst = sub + atomicAdd(&tcnt[s], 1u);
         }
         // one store per item and lane, in straight-line code (items without a row store to the
-        // sink): a fixed store count per step (see load)
-        if (HJ3D_NAGG_DIAG != 1 && (HJ3D_NAGG_STATIC || dst != tabs.sink)) *dst = v[u].y;
+        // sink): a fixed store count per step
+        if (HJ3D_NAGG_DIAG != 1) *dst = v[u].y;
       }
-#pragma unroll
-      for (int u = 0; u < kAggU; ++u) v[u] = nv[u];
-    }
+    });
     nagg_clk(gp, 4);
     mrun += nk;
     srun += nrows;
@@ -1028,8 +1142,14 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
       if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
     lds_attr = true;
   }
-  const uint32_t want = uint32_t(1.5 * W) + kSmallBlock + 64;  // the small form's insert slack
-  const uint32_t cap512 = prime_at_least(want < 2048 ? 2048 : want);
+  // the small form's table: ~2.5 slots per bucket where that still fits two workgroups per CU (a lower
+  // load factor leaves fewer keys off their home slot: config D shape 18.06 -> 17.73 ms), else ~1.5
+  uint32_t cap512 = 0;
+  for (const double f : {double(HJ3D_NAGG_CAPF), 1.5}) {
+    const uint32_t want = uint32_t(f * W) + kSmallBlock + 64;  // + the insert slack
+    cap512 = prime_at_least(want < 2048 ? 2048 : want);
+    if (cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) break;
+  }
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)

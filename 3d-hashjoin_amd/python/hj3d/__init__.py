@@ -25,7 +25,7 @@ HJ3D_ROW_IMPLICIT = 0xFFFFFFFF
 HJ3D_CHAIN, HJ3D_NESTED = 0, 1
 PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 0x2, 0x4, 0x8, 0x10
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
-OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_RADIX, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 3, 4, 5, 6
+OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 4, 5, 6
 OPT_PROBE_ITEMS = 7
 OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_SYNC_BUILD, OPT_NESTED_2L = 8, 9, 10, 11, 13, 14
 OPT_RP_UNFUSED = 15
@@ -299,10 +299,6 @@ class Context:
     def force_direct(self, on: bool = True):
         """A/B switch: chaining build/probe without the radix-partitioned kernels."""
         self.set_option(OPT_FORCE_DIRECT, int(on))
-
-    def nested_radix(self, on: bool = True):
-        """Nested builds from the radix-partitioned bucket CSR instead of the key sort."""
-        self.set_option(OPT_NESTED_RADIX, int(on))
 
     def nested_sort(self, on: bool = True):
         """Nested builds by the LSD key sort instead of the partition + LDS aggregation build."""

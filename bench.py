@@ -120,10 +120,10 @@ def parse():
                    help="unique chaining probe: packed pairs, two launches (default), or the (hash, row) pair "
                         "partitioned probe (A/B)")
     p.add_argument("--theta", type=float, default=0.8, help="config C Zipf parameter")
-    p.add_argument("--nested-build", default="agg", choices=["agg", "slices", "sort", "radix"],
+    p.add_argument("--nested-build", default="agg", choices=["agg", "slices", "sort"],
                    help="3D build: bucket-range partition + LDS aggregation (default), the same on the packed "
                         "partitioner's slices (HJ3D_OPT_NESTED_PK, the form of tables above 2048 partitions), LSD "
-                        "key sort (HJ3D_OPT_NESTED_SORT), radix bucket CSR + per-bucket grouping (HJ3D_OPT_NESTED_RADIX)")
+                        "key sort (HJ3D_OPT_NESTED_SORT)")
     p.add_argument("--chain-build", default="auto", choices=["auto", "slices"],
                    help="chaining build: the library's choice (default), or the two-level slice build (pk_build, "
                         "HJ3D_OPT_PK_BUILD) wherever it applies (A/B)")
@@ -938,9 +938,7 @@ def main_single_config(args):
     ctx.timing(0 if args.lib_timing == "auto" else int(args.lib_timing))  # (no timer is read here)
     if args.rp_unfused:
         ctx.rp_unfused(True)
-    if args.nested_build == "radix":
-        ctx.nested_radix(True)
-    elif args.nested_build == "sort":
+    if args.nested_build == "sort":
         ctx.nested_sort(True)
     elif args.nested_build == "slices":
         ctx.nested_pk(True)

@@ -149,10 +149,8 @@ enum {
   /* HJ3D_OPT_RADIX_MIN (tuples): probes of at least this many tuples (builds of at least 1/16 of
    * it) use the radix-partitioned kernels; default 2^20. */
   HJ3D_OPT_RADIX_MIN = 2,
-  /* HJ3D_OPT_NESTED_RADIX (0/1, default 0): build nested tables from the radix-partitioned bucket
-   * CSR with per-bucket key grouping instead of the key sort (faster at low bucket fill, slower
-   * under heavy skew). */
-  HJ3D_OPT_NESTED_RADIX = 3,
+  /* 3: reserved (a nested build from the radix bucket CSR with per-bucket key grouping: faster at low
+   * bucket fill, slower under Zipf skew than the aggregation build; removed in round 6) */
   /* HJ3D_OPT_NESTED_SORT (0/1, default 0): build nested tables by the LSD key sort (nested.hip)
    * instead of the bucket-range partition + per-partition LDS aggregation (nested_agg.hip, the
    * default for large inputs). */

@@ -101,7 +101,6 @@ def test_exp1_both_chaining_paths(ctx, name, g, path):
     dR, dS = dev(R), dev(S)
     if path == "radix":
         ctx.radix_min(0)
-        ctx.nested_radix(True)
     else:
         ctx.force_direct(True)
     try:
@@ -122,15 +121,14 @@ def test_exp1_both_chaining_paths(ctx, name, g, path):
     finally:
         ctx.radix_min(1 << 20)
         ctx.force_direct(False)
-        ctx.nested_radix(False)
 
 
 @pytest.mark.parametrize("nb", [64, 2000, 50000])
 @pytest.mark.parametrize("path", ["radix", "direct"])
 def test_nested_many_keys_per_bucket(ctx, nb, path):
-    """Nested build with many distinct keys per bucket: ~1560 (the radix grouping gives up after
-    64 keys in one bucket and the sort-based build takes over), ~50 (many grouping passes) and
-    ~2 per bucket; every counter and the output equal the oracle's."""
+    """Nested build with many distinct keys per bucket: ~1560 (the aggregation build gives up on
+    key ranges too dense for its LDS table and the sort-based build takes over), ~50 (ranges retried
+    in halves) and ~2 per bucket; every counter and the output equal the oracle's."""
     import hj3d
     rng = np.random.default_rng(nb)
     nR, nS = 100_000, 400_000
@@ -140,7 +138,6 @@ def test_nested_many_keys_per_bucket(ctx, nb, path):
     S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
     if path == "radix":
         ctx.radix_min(0)
-        ctx.nested_radix(True)
     else:
         ctx.force_direct(True)
     try:
@@ -153,7 +150,6 @@ def test_nested_many_keys_per_bucket(ctx, nb, path):
     finally:
         ctx.radix_min(1 << 20)
         ctx.force_direct(False)
-        ctx.nested_radix(False)
 
 
 def test_scan_status_regrowth_ignores_stale_memory():
@@ -530,6 +526,35 @@ def test_build_many_one_table_gives_up(ctx, dense, sync):
         ctx.timing(False)
         ctx.sync_build(False)
         ctx.radix_min(1 << 20)
+
+
+@pytest.mark.parametrize("theta,n,dom", [(1.0, 4_000_000, 200_000), (1.3, 3_000_000, 50_000), (0.8, 6_000_000, 600_000)])
+def test_nested_build_hot_keys(ctx, theta, n, dom):
+    """Zipf-skewed build keys whose hottest keys hold most of their partitions' rows: the heavy
+    partitions find their hot key from a sample and take the register path for its rows (counted
+    per lane in pass A, placed by wave prefix and ballot count in pass B); the other keys keep the
+    LDS table. Counters, output checksums and statistics equal the oracle's (Nrs: nested table on
+    S.a, probe R, unnest; HtNested1::insert, ht_nested.hh:287-311)."""
+    import hj3d
+    rng = np.random.default_rng(int(theta * 10))
+    Sa = (np.minimum(rng.zipf(1.0 + theta if theta > 1.0 else 2.0, n) if theta > 1.0 else
+          _zipf_keys(rng, n, dom, theta), dom) - (1 if theta > 1.0 else 0)).astype(np.uint32)
+    S = O.tuples3(np.arange(n, dtype=np.uint32), Sa)
+    R = O.tuples3(np.arange(dom, dtype=np.uint32), np.zeros(dom, np.uint32))
+    nb = O.num_distinct(Sa)
+    e = O.nested_plan(S, 1, R, 0, nb, True)
+    got = hj3d.exp1_plan(ctx, "Nrs", dev(R), dev(S), nb)
+    assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_unnest, e.c_top)
+    assert got["out"] == e.out
+    assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
+
+
+def _zipf_keys(rng, n, dom, theta):
+    """n keys in [0, dom) with P(k) ~ 1 / (k + 1)^theta (theta < 1: inverse CDF on the exact weights)."""
+    w = 1.0 / np.arange(1, dom + 1, dtype=np.float64) ** theta
+    c = np.cumsum(w)
+    c /= c[-1]
+    return np.searchsorted(c, rng.random(n)).astype(np.uint32)
 
 
 @pytest.mark.parametrize("explicit", [1, 0], ids=["r1_explicit", "r0_explicit"])
