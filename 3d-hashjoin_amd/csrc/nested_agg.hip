@@ -130,31 +130,42 @@ __device__ __forceinline__ uint32_t next_slot(uint32_t s, uint32_t st, uint32_t 
   return s >= cap ? s - cap : s;
 }
 
-// Slot of key h, inserting it if absent (returns kInvalid when the table is at its limit: the
-// caller flags the round as overflowing).
-__device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t* nkeys,
-                                               uint32_t cap, uint32_t limit) {
+// Slot of key h, inserting it if absent; k: the key its home slot held when the caller read it (a
+// stale empty is fine: slots only ever go from empty to a key, and the CAS sees the truth). Returns
+// kInvalid after kMaxProbe slots without a place (a table too full for the round: the caller flags
+// it as overflowing and retries a narrower range). A key at its home slot costs the caller's batched
+// read only; a new key whose home slot was empty one CAS (no re-read, no key counter).
+constexpr uint32_t kMaxProbe = 64;
+__device__ __forceinline__ uint32_t tab_insert_k(uint32_t* tkey, uint32_t h, uint32_t k, uint32_t empty,
+                                                 uint32_t cap) {
   uint32_t s = slot_of(h, cap);
   const uint32_t st = step_of(h, cap);
-  for (;;) {
-    const uint32_t k = tkey[s];
+#pragma unroll 1
+  for (uint32_t n = 0; n < kMaxProbe; ++n) {
     if (k == h) return s;
     if (k == empty) {
-      if (*nkeys >= limit) return kInvalid;
       const uint32_t old = atomicCAS(&tkey[s], empty, h);
-      if (old == empty) {
-        atomicAdd(nkeys, 1u);
-        return s;
-      }
-      if (old == h) return s;
+      if (old == empty || old == h) return s;
     }
     s = next_slot(s, st, cap);
+    k = tkey[s];
   }
+  return kInvalid;
+}
+__device__ __forceinline__ uint32_t tab_insert(uint32_t* tkey, uint32_t h, uint32_t empty, uint32_t cap) {
+  return tab_insert_k(tkey, h, tkey[slot_of(h, cap)], empty, cap);
 }
 
 __device__ __forceinline__ uint32_t tab_find(const uint32_t* tkey, uint32_t h, uint32_t cap) {
   uint32_t s = slot_of(h, cap);
   const uint32_t st = step_of(h, cap);
+  while (tkey[s] != h) s = next_slot(s, st, cap);
+  return s;
+}
+// the same for a key known not to sit in its home slot (the caller's batched read): from the next slot
+__device__ __forceinline__ uint32_t tab_find_away(const uint32_t* tkey, uint32_t h, uint32_t cap) {
+  const uint32_t st = step_of(h, cap);
+  uint32_t s = next_slot(slot_of(h, cap), st, cap);
   while (tkey[s] != h) s = next_slot(s, st, cap);
   return s;
 }
@@ -210,11 +221,18 @@ __device__ uint32_t block_scan_lds(uint32_t* a, uint32_t n, uint32_t* wsum) {
 // One workgroup per partition p (local buckets [b0, b0 + nbs), pairs [ps[p], ps[p+1])).
 // Writes: off[b0 + k] = partition-local main offset of bucket k; mtmp[ps[p] + i] the partition's
 // main records in bucket order (i < its key count, with sub_off global); sub rows; dcount[p].
-// Dynamic LDS (agg_lds_bytes): tkey | tcnt | tmin [cap each] | bcnt [W] | wsum | nkeys, ovf.
+// Dynamic LDS (agg_lds_bytes): tkey | tcnt | tmin [cap each] | (pad to 8 B) | bcnt [max(W, 2 kAggQ per
+// wave)] | wsum | (unused), ovf | region starts | hot-key words. bcnt doubles as pass A's per-wave miss
+// queues (kAggQ pairs per wave): its counts live only from the end of pass A to pass B.
 // SLOTS >= cap / BLOCK: table slots per thread in the per-slot loops.
 constexpr uint32_t kAggMaxS2 = 16;  // fine regions per slice (pk_slices)
+constexpr uint32_t kAggQ = 128;     // pass A's miss queue: pairs per wave (a ring, flushed 64 at a time)
+__host__ __device__ constexpr uint32_t agg_bcnt_words(uint32_t W, int block) {
+  return W > 2u * kAggQ * uint32_t(block / 64) ? W : 2u * kAggQ * uint32_t(block / 64);
+}
 __host__ __device__ constexpr uint32_t agg_lds_words(uint32_t cap, uint32_t W, int block) {
-  return 3 * cap + W + uint32_t(block / 64) + 2 + kAggMaxS2 + 2 + 2 * uint32_t(block / 64) + 2;
+  return 3 * cap + 1 + agg_bcnt_words(W, block) + uint32_t(block / 64) + 2 + kAggMaxS2 + 2 + 2 * uint32_t(block / 64) +
+         2;
 }
 // PK: the partition's pairs are slice p's fine regions (pk_slices), packed words as keys.
 struct NaggSrc {
@@ -246,9 +264,10 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
   uint32_t* tmin = tcnt + cap;   // min row, then (after the main records are written) unused
-  uint32_t* bcnt = tmin + cap;   // keys per bucket of the round, then their main offsets
-  uint32_t* wsum = bcnt + W;
-  uint32_t& nkeys = wsum[BLOCK / kWave];
+  // keys per bucket of the round, then their main offsets (8-B aligned: pass A's miss queues)
+  uint32_t* bcnt = tmin + cap + ((3 * cap) & 1u);
+  const uint32_t bwords = agg_bcnt_words(W, BLOCK);
+  uint32_t* wsum = bcnt + bwords;
   uint32_t& ovf = wsum[BLOCK / kWave + 1];
   uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
   // hot key of a heavy partition: per-wave hot rows (then their exclusive prefix) and min rows, the
@@ -256,7 +275,6 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   uint32_t* hotw = rstart + kAggMaxS2 + 2;
   uint32_t* hotm = hotw + BLOCK / kWave;
   uint32_t& hslot = hotm[BLOCK / kWave];
-  const uint32_t limit = cap - BLOCK - 64;
   const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
   const uint32_t p = gp - ti * tabs.P;                      // partition inside table ti
   uint32_t* __restrict__ off = tabs.off[ti];
@@ -371,6 +389,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       }
     }
   };
+  uint2* wq = reinterpret_cast<uint2*>(bcnt) + wid * kAggQ;  // pass A's miss queue of this wave
   uint32_t mrun = 0, srun = 0, mxlen = 0;  // keys and rows of the finished rounds
   uint32_t c0 = 0, span = (nbs + kAggRounds - 1) / kAggRounds;
   const uint32_t wid_ = threadIdx.x / kWave;
@@ -426,15 +445,32 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       tcnt[s] = 0;
       tmin[s] = kInvalid;
     }
-    for (uint32_t k = threadIdx.x; k < c1 - c0; k += BLOCK) bcnt[k] = 0;
-    if (threadIdx.x == 0) {
-      nkeys = 0;
-      ovf = 0;
-    }
+    // bcnt past the miss queues (each wave clears its own queue's words after its last flush)
+    for (uint32_t k = kNw * 2 * kAggQ + threadIdx.x; k < c1 - c0; k += BLOCK) bcnt[k] = 0;
+    if (threadIdx.x == 0) ovf = 0;
     __syncthreads();
     nagg_clk(gp, 1);
     // ---- pass A: count and min row per key ----
     uint32_t hc = 0, hm = kInvalid;  // hot rows and their min row (this lane)
+    // Items whose key is not in its home slot (new keys, keys placed further along their probe
+    // sequence: ~1 in 4 at config D) go to the wave's miss queue instead of walking the probe
+    // sequence in place: in place, nearly every item had a few such lanes, so the wave ran a divergent
+    // probe loop per item; the queue is walked with every lane busy once it holds 64 items.
+    uint32_t qh = 0, qt = 0;  // (wave-uniform) ring head and tail, pairs
+    const auto qtake = [&](bool take) __attribute__((always_inline)) {  // this lane's pair at the head
+      __builtin_amdgcn_wave_barrier();
+      if (take) {
+        const uint2 e = wq[(qh + uint32_t(lane)) & (kAggQ - 1)];
+        const uint32_t s = tab_insert(tkey, e.x, empty, cap);
+        if (s == kInvalid) {
+          ovf = 1;
+        } else {
+          atomicAdd(&tcnt[s], 1u);
+          atomicMin(&tmin[s], e.y);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    };
     stream([&](const uint2 (&v)[kAggU], uint32_t valid) __attribute__((always_inline)) {
       // home slots of all items read together (one LDS latency for the batch); only items whose
       // key is not in its home slot walk the probe sequence; active items as one bit mask
@@ -471,7 +507,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           if (__popcll(same) > 1) {
             const uint32_t rmin = wave_min_u32(mine ? v[u].y : kInvalid);
             if (lane == leader) {
-              const uint32_t s = tab_insert(tkey, hl, empty, &nkeys, cap, limit);
+              const uint32_t s = tab_insert(tkey, hl, empty, cap);
               if (s == kInvalid) {
                 ovf = 1;
               } else {
@@ -482,17 +518,27 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
             a = a && !mine;
           }
         }
-        if (a) {
-          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_insert(tkey, v[u].x, empty, &nkeys, cap, limit);
-          if (s == kInvalid) {
-            ovf = 1;
-          } else {
-            atomicAdd(&tcnt[s], 1u);
-            atomicMin(&tmin[s], v[u].y);
-          }
+        const bool miss = a && k0[u] != v[u].x;
+        if (a && !miss) {
+          const uint32_t s = slot_of(v[u].x, cap);
+          atomicAdd(&tcnt[s], 1u);
+          atomicMin(&tmin[s], v[u].y);
+        }
+        const uint64_t mb = __ballot(miss);
+        if (miss) wq[(qt + uint32_t(__popcll(mb & lt))) & (kAggQ - 1)] = v[u];
+        qt += uint32_t(__popcll(mb));
+        if (qt - qh >= kWave) {  // 64 pairs: one with every lane
+          qtake(true);
+          qh += kWave;
         }
       }
     });
+    qtake(uint32_t(lane) < qt - qh);
+    {  // this wave's queue words back to bucket counts (zero) for the main slots below
+      uint32_t* qw = reinterpret_cast<uint32_t*>(wq);
+      for (uint32_t k = uint32_t(lane); k < 2 * kAggQ; k += kWave)
+        if (wid_ * 2 * kAggQ + k < c1 - c0) qw[k] = 0;
+    }
     if (hot) {  // the hot key into the table: per-wave totals, then one insert
       uint32_t c = hc;
 #pragma unroll
@@ -511,7 +557,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           tot += x;
           mn = min(mn, hotm[w]);
         }
-        const uint32_t sl = tot ? tab_insert(tkey, H, empty, &nkeys, cap, limit) : kInvalid;
+        const uint32_t sl = tot ? tab_insert(tkey, H, empty, cap) : kInvalid;
         if (tot && sl == kInvalid) {
           ovf = 1;
         } else if (tot) {
@@ -611,7 +657,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           }
         }
         if (a) {
-          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find(tkey, v[u].x, cap);
+          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find_away(tkey, v[u].x, cap);
           dst = sub + atomicAdd(&tcnt[s], 1u);
         }
         // one store per item and lane, in straight-line code (items without a row store to the
@@ -679,10 +725,8 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
   uint32_t* bcnt = tmin + cap;
   uint32_t* img = bcnt + W;
   uint32_t* wsum = img + kRegCap;
-  uint32_t& nkeys = wsum[kRegBlock / kWave];
   uint32_t& ovf = wsum[kRegBlock / kWave + 1];
   uint32_t* rst = wsum + kRegBlock / kWave + 2;  // [2][kAggMaxS2 + 2]: region starts of the two slices in turn
-  const uint32_t limit = cap - kRegBlock - 64;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
   uint32_t mxlen = 0;
@@ -752,10 +796,7 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
         tmin[s] = kInvalid;
       }
       for (uint32_t k = threadIdx.x; k < nbs; k += kRegBlock) bcnt[k] = 0;
-      if (threadIdx.x == 0) {
-        nkeys = 0;
-        ovf = 0;
-      }
+      if (threadIdx.x == 0) ovf = 0;
     }
     starts(idx + gridDim.x, b ^ 1u);  // the next partition's region starts (PK)
     __syncthreads();
@@ -783,7 +824,7 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
             if (__popcll(same) > 1) {
               const uint32_t rmin = wave_min_u32(mine ? e.y : kInvalid);
               if (lane == leader) {
-                const uint32_t s = tab_insert(tkey, hl, empty, &nkeys, cap, limit);
+                const uint32_t s = tab_insert(tkey, hl, empty, cap);
                 if (s == kInvalid) {
                   ovf = 1;
                 } else {
@@ -795,7 +836,7 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
             }
           }
           if (a) {
-            const uint32_t s = k0[u] == e.x ? slot_of(e.x, cap) : tab_insert(tkey, e.x, empty, &nkeys, cap, limit);
+            const uint32_t s = k0[u] == e.x ? slot_of(e.x, cap) : tab_insert_k(tkey, e.x, k0[u], empty, cap);
             if (s == kInvalid) {
               ovf = 1;
             } else {

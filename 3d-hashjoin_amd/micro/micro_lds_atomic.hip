@@ -5,6 +5,9 @@
 //   mode 2: atomicAdd without using the result (no return)
 //   mode 3: plain ds_read + ds_write on per-wave private counters (lost updates, timing only)
 //   mode 4: ds_read only
+//   mode 5: atomicCAS (compare-and-swap with return) on 1018 shared counters
+//   mode 6: atomicMin without return on 1018 shared counters
+//   mode 7: atomicAdd + atomicMin without return on one random slot (k_nagg pass A's hit path)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
@@ -26,6 +29,9 @@ __global__ __launch_bounds__(1024) void k(unsigned* out, int rounds) {
       if (MODE == 2) atomicAdd(&cnt[p], 1u);
       if (MODE == 3) { const unsigned v = cnt[wbase + p]; cnt[wbase + p] = v + 1; acc += v; }
       if (MODE == 4) acc += cnt[wbase + p];
+      if (MODE == 5) acc += atomicCAS(&cnt[p], x, x + 1u);
+      if (MODE == 6) atomicMin(&cnt[p], x);
+      if (MODE == 7) { atomicAdd(&cnt[p], 1u); atomicMin(&cnt[1024 + p], x); }
     }
   }
   __syncthreads();
@@ -58,5 +64,8 @@ int main() {
   run("atomic no-return, shared", k<2>);
   run("plain read+write, private", k<3>);
   run("plain read only", k<4>);
+  run("atomicCAS rtn, shared", k<5>);
+  run("atomicMin no-return, shared", k<6>);
+  run("atomicAdd + atomicMin no-return", k<7>);
   return 0;
 }
