@@ -31,7 +31,11 @@
 namespace hj3d {
 namespace {
 
-constexpr uint32_t kAggW = 6144;     // max buckets per partition (one LDS table round at fill <= ~1.3)
+#ifndef HJ3D_NAGG_WMAX
+#define HJ3D_NAGG_WMAX 6144
+#endif
+constexpr uint32_t kAggW = HJ3D_NAGG_WMAX;  // max buckets per partition (one LDS table round at fill <= ~1.3)
+
 // LDS hash table slots (prime, sized per build: ~1.6 slots per bucket of the partition + the insert
 // slack below; at most 10223): with double hashing every probe step visits all slots (double
 // hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6). The table
@@ -53,6 +57,7 @@ constexpr int kAggU = HJ3D_NAGG_U;   // pairs per thread and step (the next step
 #endif
 constexpr int kSmallBlock = HJ3D_NAGG_SB;
 constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap <= 6144)
+constexpr size_t kSmallLds = 81920, kBigLds = 160 * 1024;  // dynamic LDS of the two forms (two / one per CU)
 #ifndef HJ3D_NAGG_PER_CU
 #define HJ3D_NAGG_PER_CU 2  // target partitions per CU when the table is small (A/B: 4 with 256 threads)
 #endif
@@ -67,9 +72,6 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 // Uniform keys, 1e9 tuples / 1e8 buckets: 26.1 ms (5,357 buckets, one 1024-thread workgroup per CU)
 // -> 19.9 ms (2,048) -> 18.5 ms (1,536; two 512-thread workgroups per CU, a quarter of the sub-row
 // window); 1,024 exceeds the 65,536 slices (profiles/r04n_ab_pkw.log)
-#endif
-#ifndef HJ3D_NAGG_DIAG
-#define HJ3D_NAGG_DIAG 0  // diagnostic variants (tables wrong): 1 pass B without its sub-row stores, 2 without pass B
 #endif
 #ifndef HJ3D_NAGG_REG
 #define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
@@ -92,7 +94,7 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #endif
 
 #ifndef HJ3D_NAGG_CAPF
-#define HJ3D_NAGG_CAPF 2.5  // small form: LDS table slots per bucket of the partition (+ the insert slack)
+#define HJ3D_NAGG_CAPF 1.5  // small form: LDS table slots per bucket of the partition (+ the insert slack)
 #endif
 #ifndef HJ3D_NAGG_HOT
 #define HJ3D_NAGG_HOT 1  // heavy partitions: the hot key's rows on the register path (0: A/B)
@@ -100,8 +102,8 @@ constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap 
 #ifndef HJ3D_NAGG_ELECT
 #define HJ3D_NAGG_ELECT 2  // hot-key wave leader election: 2 partitions above 5/4 of the mean size (default), 1 every partition, 0 none
 #endif
-#ifndef HJ3D_NAGG_ENDBAR
-#define HJ3D_NAGG_ENDBAR 0  // a barrier after the last round of a partition too (1: A/B)
+#ifndef HJ3D_NAGG_HOTSPLIT
+#define HJ3D_NAGG_HOTSPLIT 1  // heavy one-level partitions: hot key split off first (k_nagg_hot; 0: A/B)
 #endif
 
 #ifndef HJ3D_NAGG_CLK
@@ -230,9 +232,15 @@ constexpr uint32_t kAggQ = 128;     // pass A's miss queue: pairs per wave (a ri
 __host__ __device__ constexpr uint32_t agg_bcnt_words(uint32_t W, int block) {
   return W > 2u * kAggQ * uint32_t(block / 64) ? W : 2u * kAggQ * uint32_t(block / 64);
 }
+// fixed words: tkey, tcnt [cap each] | wsum (waves + 2: block-scan sums, ovf) | region starts
+// (kAggMaxS2 + 2) | hot-key words (2 waves + 2), rounded to 8 B; then the region R: in pass A tmin [cap]
+// | bcnt [agg_bcnt_words] (8-B aligned: the miss queues), in pass B the sub-row image (every word of the
+// allocation past the fixed ones)
+__host__ __device__ constexpr uint32_t agg_fixed_words(uint32_t cap, int block) {
+  return (2 * cap + uint32_t(block / 64) + 2 + kAggMaxS2 + 2 + 2 * uint32_t(block / 64) + 2 + 1) & ~1u;
+}
 __host__ __device__ constexpr uint32_t agg_lds_words(uint32_t cap, uint32_t W, int block) {
-  return 3 * cap + 1 + agg_bcnt_words(W, block) + uint32_t(block / 64) + 2 + kAggMaxS2 + 2 + 2 * uint32_t(block / 64) +
-         2;
+  return agg_fixed_words(cap, block) + cap + (cap & 1u) + agg_bcnt_words(W, block);
 }
 // PK: the partition's pairs are slice p's fine regions (pk_slices), packed words as keys.
 struct NaggSrc {
@@ -253,28 +261,41 @@ struct NaggTabs {
   uint64_t* counts[2] = {nullptr, nullptr};  // word 2: longest key, word 3: give-up flag
   uint64_t* hc[2] = {nullptr, nullptr};      // the tables' pinned host mirrors of the counts words (or none)
   uint32_t* sink = nullptr;  // pass B's stores of items without a row (the context's store-sink words)
+  uint32_t ldsw = 0;         // k_nagg's dynamic LDS words (>= agg_lds_words): the image takes the rest
+  // partitions the register form leaves to k_nagg_defer (more pairs than its registers hold, or more
+  // keys than its table): defer[0] the count (zeroed by k_nagg_order / k_nagg_pk_ovf), then the indices
+  uint32_t* defer = nullptr;
   uint32_t elect_min = 0;    // partitions of at least this many pairs elect a wave leader per hot key
+  // Hot keys split off heavy partitions (k_nagg_hot, one-level partitions only): per partition kHotW
+  // words {flag, key, rows (cursor), min row, other pairs (cursor)}; the other pairs compacted into
+  // hpairs[ps[gp] ..]; the key's rows already in the suffix of the partition's sub range
+  uint32_t* hot = nullptr;
+  uint2* hpairs = nullptr;
 };
+constexpr uint32_t kHotW = 8;
 // one partition (global index gp) of k_nagg
 template <int BLOCK, int SLOTS, bool PK>
 __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                          FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                          uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount, uint32_t cap,
                                          const NaggSrc& src, const NaggTabs& tabs, uint32_t* agg_lds) {
+  constexpr uint32_t kNw = BLOCK / kWave;
   uint32_t* tkey = agg_lds;
-  uint32_t* tcnt = tkey + cap;   // count, then the sub cursor
-  uint32_t* tmin = tcnt + cap;   // min row, then (after the main records are written) unused
-  // keys per bucket of the round, then their main offsets (8-B aligned: pass A's miss queues)
-  uint32_t* bcnt = tmin + cap + ((3 * cap) & 1u);
-  const uint32_t bwords = agg_bcnt_words(W, BLOCK);
-  uint32_t* wsum = bcnt + bwords;
-  uint32_t& ovf = wsum[BLOCK / kWave + 1];
-  uint32_t* rstart = wsum + BLOCK / kWave + 2;  // PK: stream start of every fine region (+ 2 sentinels)
+  uint32_t* tcnt = tkey + cap;  // count, then the rows before the key in the round (pass B: its cursor)
+  uint32_t* wsum = tcnt + cap;
+  uint32_t& ovf = wsum[kNw + 1];
+  uint32_t* rstart = wsum + kNw + 2;  // PK: stream start of every fine region (+ 2 sentinels)
   // hot key of a heavy partition: per-wave hot rows (then their exclusive prefix) and min rows, the
   // key's slot and its rows' total
   uint32_t* hotw = rstart + kAggMaxS2 + 2;
-  uint32_t* hotm = hotw + BLOCK / kWave;
-  uint32_t& hslot = hotm[BLOCK / kWave];
+  uint32_t* hotm = hotw + kNw;
+  uint32_t& hslot = hotm[kNw];
+  uint32_t& hrows = hotm[kNw + 1];
+  uint32_t* tmin = agg_lds + agg_fixed_words(cap, BLOCK);  // min row, until the main records are written
+  // keys per bucket of the round, then their main offsets (8-B aligned: pass A's miss queues)
+  uint32_t* bcnt = tmin + cap + (cap & 1u);
+  uint32_t* img = tmin;  // pass B: the window's sub rows, assembled
+  const uint32_t imgw = tabs.ldsw - agg_fixed_words(cap, BLOCK);
   const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
   const uint32_t p = gp - ti * tabs.P;                      // partition inside table ti
   uint32_t* __restrict__ off = tabs.off[ti];
@@ -283,7 +304,16 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   auto* fail = reinterpret_cast<uint32_t*>(tabs.counts[ti] + 3);
   const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
   // (table ti's sub rows are numbered from its first pair: ps[ti * P])
-  const uint32_t e0 = ps[gp], e1 = ps[gp + 1], total = e1 - e0, tb = ps[ti * tabs.P];
+  const uint32_t e0 = ps[gp], e1 = ps[gp + 1], tb = ps[ti * tabs.P];
+  uint32_t total = e1 - e0;
+  // a hot key split off by k_nagg_hot: its rows are in place (the suffix of the partition's sub range),
+  // the stream is the partition's other pairs, compacted
+  const uint32_t* hw = tabs.hot ? tabs.hot + uint64_t(gp) * kHotW : nullptr;
+  const bool ext = hw && hw[0];
+  if (ext) {
+    pairs = tabs.hpairs;
+    total = hw[4];
+  }
   const bool elect = total >= tabs.elect_min;  // (uniform per workgroup)
   nagg_clk(gp, 0);
   nagg_clk(gp, 7);
@@ -321,7 +351,6 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   // Slices (PK, HJ3D_NAGG_PKWAVE): wave w walks the fine regions w, w + waves, ... one after another,
   // a step being kAggU x 64 consecutive items of one region, so no item searches for its region.
   // body(v, valid): v the step's pairs, valid the bit mask of the lane's real items.
-  constexpr uint32_t kNw = BLOCK / kWave;
   const uint32_t wid = threadIdx.x / kWave;
   const auto stream = [&](auto&& body) __attribute__((always_inline)) {
     uint2 v[kAggU], nv[kAggU];
@@ -406,8 +435,9 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     // register path: pass A counts them and their min row per lane (one table update per wave at the
     // end), pass B places them at the key's range start + the wave's prefix (from pass A's per-wave
     // counts: both passes walk the stream in one order) + a running ballot count: no LDS atomic.
-    uint32_t H = empty;
-    if (HJ3D_NAGG_HOT && elect && whole && total >= 4u * BLOCK) {
+    // (split off: the key is this round's when its bucket is)
+    uint32_t H = ext && (whole || lbk(hw[1]) - c0 < c1 - c0) ? hw[1] : empty;
+    if (!ext && HJ3D_NAGG_HOT && elect && whole && total >= 4u * BLOCK) {
       if constexpr (PK) __syncthreads();  // (the region starts written above)
       const uint32_t f = uint32_t(uint64_t(total) * threadIdx.x / BLOCK);
       uint32_t key;
@@ -557,6 +587,10 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           tot += x;
           mn = min(mn, hotm[w]);
         }
+        if (ext) {  // (the stream held none of its rows)
+          tot = hw[2];
+          mn = hw[3];
+        }
         const uint32_t sl = tot ? tab_insert(tkey, H, empty, cap) : kInvalid;
         if (tot && sl == kInvalid) {
           ovf = 1;
@@ -565,6 +599,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
           tmin[sl] = min(tmin[sl], mn);
         }
         hslot = sl;
+        hrows = tot;
       }
     }
     __syncthreads();
@@ -594,6 +629,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     for (int j = 0; j < SLOTS; ++j) {
       const uint32_t s = j * BLOCK + threadIdx.x;
       cnt[j] = s < cap ? tcnt[s] : 0u;
+      if (ext && hot && s == hslot) tcnt[s] = 0;  // (its range: after every other row)
     }
     __syncthreads();
     const uint32_t nrows = block_scan_lds<BLOCK>(tcnt, cap, wsum);
@@ -604,9 +640,9 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
       if (cnt[j]) {
         const uint32_t h = tkey[s];
         const uint32_t m = mrun + bcnt[lbk(h) - c0] + rank[j];
-        const uint32_t so = e0 - tb + srun + tcnt[s];  // table ti's sub rows
+        // (table ti's sub rows; a split-off hot key's: past the partition's other rows, of every round)
+        const uint32_t so = e0 - tb + (ext && hot && s == hslot ? total : srun + tcnt[s]);
         mtmp[e0 + m] = make_uint4(hash_of(h), tmin[s], so, cnt[j]);
-        tcnt[s] = so;  // sub cursor
         mxlen = max(mxlen, cnt[j]);
       }
     }
@@ -614,65 +650,90 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     __syncthreads();
     nagg_clk(gp, 3);
     // ---- pass B: rows into their keys' sub ranges ----
-    // (hot key: its range start, from its slot's cursor, + this wave's prefix)
-    uint32_t hcur = hot && hslot != kInvalid ? tcnt[hslot] + hotw[wid_] : 0u;
-    if (HJ3D_NAGG_DIAG != 2)
-    stream([&](const uint2 (&v)[kAggU], uint32_t valid) __attribute__((always_inline)) {
-      uint32_t actm = 0;
-      uint32_t k0[kAggU];
+    // The round's first imgw rows are assembled in LDS (the image) and go out as whole lines; rows past
+    // it (a partition with more rows than the image holds) and a hot key's rows (per-wave runs) go to
+    // HBM directly. 4-B row stores scattered over a partition's whole sub range left the L2 with partial
+    // lines (config C: 2.2 GB written for 0.55 GB of sub rows and main records; build 2.06 -> 1.62 ms
+    // with no row stores at all). Tried: more sweeps over the pairs, one per image-sized slot range of
+    // keys (C: 3 sweeps, 2.36 ms against 1.87 ms for one sweep; config D's shape gained nothing).
+    uint32_t* __restrict__ gsub = sub + (e0 - tb + srun);  // the round's sub rows
+    const bool hk = hot && !ext && hslot != kInvalid;  // (uniform) rows of the hot key: to HBM, per wave
+    // (hot key: its range start + this wave's prefix)
+    uint32_t hcur = hk ? tcnt[hslot] + hotw[wid_] : 0u;
+    const uint32_t hstart = hk ? tcnt[hslot] : 0u, hlen = hk ? hrows : 0u;  // (its cursor never moves)
+    // DIRECT: rows also go to HBM (every item then stores once, to its row or the sink: a fixed store
+    // count per step); otherwise pass B writes LDS only
+    const auto passb = [&](auto direct_c) __attribute__((always_inline)) {
+      constexpr bool DIRECT = decltype(direct_c)::value;
+      stream([&](const uint2 (&v)[kAggU], uint32_t valid) __attribute__((always_inline)) {
+        uint32_t actm = 0;
+        uint32_t k0[kAggU];
 #pragma unroll
-      for (int u = 0; u < kAggU; ++u) {
-        bool inr = true;
-        if (!whole) {
-          const uint32_t lb = lbk(v[u].x);
-          inr = lb >= c0 && lb < c1;
+        for (int u = 0; u < kAggU; ++u) {
+          bool inr = true;
+          if (!whole) {
+            const uint32_t lb = lbk(v[u].x);
+            inr = lb >= c0 && lb < c1;
+          }
+          const bool a = ((valid >> u) & 1u) && inr;
+          actm |= uint32_t(a) << u;
+          k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
         }
-        const bool a = ((valid >> u) & 1u) && inr;
-        actm |= uint32_t(a) << u;
-        k0[u] = tkey[a ? slot_of(v[u].x, cap) : 0u];
-      }
 #pragma unroll
-      for (int u = 0; u < kAggU; ++u) {
-        bool a = (actm >> u) & 1u;
-        uint32_t* dst = tabs.sink;
-        if (hot) {
-          const bool h = a && v[u].x == H;
-          const uint64_t hm2 = __ballot(h);
-          if (h) dst = sub + hcur + uint32_t(__popcll(hm2 & lt));
-          hcur += uint32_t(__popcll(hm2));
-          a = a && !h;
-        }
-        const uint64_t am = elect ? __ballot(a) : 0ull;
-        if (am) {
-          const int leader = __ffsll((unsigned long long)am) - 1;
-          const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
-          const bool mine = a && v[u].x == hl;
-          const uint64_t same = __ballot(mine);
-          if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive sub slots
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl, cap)], uint32_t(__popcll(same)));
-            base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
-            if (mine) dst = sub + base + uint32_t(__popcll(same & lt));
-            a = a && !mine;
+        for (int u = 0; u < kAggU; ++u) {
+          bool a = (actm >> u) & 1u;
+          uint32_t dl = kInvalid;  // the row's place in the round's sub range
+          uint32_t* dst = tabs.sink;
+          if (hk) {
+            const bool h = a && v[u].x == H;
+            if constexpr (DIRECT) {
+              const uint64_t hm2 = __ballot(h);
+              if (h) dst = gsub + hcur + uint32_t(__popcll(hm2 & lt));
+              hcur += uint32_t(__popcll(hm2));
+            }
+            a = a && !h;
+          }
+          const uint64_t am = elect ? __ballot(a) : 0ull;
+          if (am) {
+            const int leader = __ffsll((unsigned long long)am) - 1;
+            const uint32_t hl = uint32_t(__builtin_amdgcn_readlane(int(v[u].x), leader));
+            const bool mine = a && v[u].x == hl;
+            const uint64_t same = __ballot(mine);
+            if (__popcll(same) > 1) {  // one cursor bump for the group, consecutive sub slots
+              uint32_t base = 0;
+              if (lane == leader) base = atomicAdd(&tcnt[tab_find(tkey, hl, cap)], uint32_t(__popcll(same)));
+              base = uint32_t(__builtin_amdgcn_readlane(int(base), leader));
+              if (mine) dl = base + uint32_t(__popcll(same & lt));
+              a = a && !mine;
+            }
+          }
+          if (a) {
+            const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find_away(tkey, v[u].x, cap);
+            dl = atomicAdd(&tcnt[s], 1u);
+          }
+          if constexpr (DIRECT) {
+            if (dl != kInvalid) {
+              if (dl < imgw) img[dl] = v[u].y;
+              else dst = gsub + dl;
+            }
+            *dst = v[u].y;  // (straight-line: one store per item and lane)
+          } else {
+            if (dl != kInvalid) img[dl] = v[u].y;
           }
         }
-        if (a) {
-          const uint32_t s = k0[u] == v[u].x ? slot_of(v[u].x, cap) : tab_find_away(tkey, v[u].x, cap);
-          dst = sub + atomicAdd(&tcnt[s], 1u);
-        }
-        // one store per item and lane, in straight-line code (items without a row store to the
-        // sink): a fixed store count per step
-        if (HJ3D_NAGG_DIAG != 1) *dst = v[u].y;
-      }
-    });
+      });
+    };
+    if (hk || nrows > imgw) passb(std::true_type{});
+    else passb(std::false_type{});
+    __syncthreads();
+    // the image out as whole lines (the hot key's rows, already in place, skipped)
+    for (uint32_t k = threadIdx.x; k < min(nrows, imgw); k += BLOCK)
+      if (k - hstart >= hlen) gsub[k] = img[k];
+    __syncthreads();  // (the next round's table; the next partition's)
     nagg_clk(gp, 4);
     mrun += nk;
     srun += nrows;
     c0 = c1;
-    // the barrier orders this round's LDS reads before the next round's table clear; after the last
-    // round there is none to wait for (a barrier there also waits for pass B's scattered stores to
-    // drain before the workgroup can end)
-    if (HJ3D_NAGG_ENDBAR || c0 < nbs) __syncthreads();
   }
   nagg_clk(gp, 5);
   if (threadIdx.x == 0) dcount[gp] = mrun;
@@ -682,7 +743,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
 
 // One workgroup per partition: gp = blockIdx.x, or order[blockIdx.x] (heavy first).
 template <int BLOCK, int SLOTS, bool PK>
-__global__ __launch_bounds__(BLOCK) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+__global__ __launch_bounds__(BLOCK, 4) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                 FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                                 uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
                                                 const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
@@ -788,7 +849,8 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
       if constexpr (PK) return x >> src.pk.qbits;
       else return fm.mod(x) - lo - b0;
     };
-    const bool big = m > kRegCap;
+    // (a partition whose hot key k_nagg_hot split off: k_nagg's streaming form, which knows the split)
+    const bool big = m > kRegCap || (tabs.hot && tabs.hot[uint64_t(gp) * kHotW]);
     if (!big) {
       for (uint32_t s = threadIdx.x; s < cap; s += kRegBlock) {
         tkey[s] = empty;
@@ -849,10 +911,10 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
       __syncthreads();
     }
     if (big || ovf) {
-      // more pairs than the registers hold, or more keys than one table round: k_nagg's streaming
-      // form (rounds over halves of the bucket range) on this partition, here
-      nagg_one<kRegBlock, SLOTS, PK>(gp, pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs, agg_lds);
-      __syncthreads();
+      // more pairs than the registers hold, or more keys than one table round: left to k_nagg's
+      // streaming form (k_nagg_defer, the next launch; nothing of the partition is written yet). Run in
+      // place it cost this kernel its registers: the inlined streaming code spilled the pair registers
+      if (threadIdx.x == 0) tabs.defer[1 + atomicAdd(&tabs.defer[0], 1u)] = gp;
       load(idx + gridDim.x, b ^ 1u);
       return;
     }
@@ -932,47 +994,209 @@ __global__ __launch_bounds__(kRegBlock) void k_nagg_reg(const uint2* __restrict_
   }
 }
 
+// The partitions k_nagg_reg left (tabs.defer), k_nagg's streaming form: workgroup b takes the
+// deferred partitions b, b + gridDim.x, ... (none: every workgroup exits at once).
+template <int BLOCK, int SLOTS, bool PK>
+__global__ __launch_bounds__(BLOCK, 4) void k_nagg_defer(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                      FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global,
+                                                      uint32_t W, uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount,
+                                                      uint32_t cap, NaggSrc src, NaggTabs tabs) {
+  extern __shared__ uint32_t agg_lds[];
+  const uint32_t n = tabs.defer[0];
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    nagg_one<BLOCK, SLOTS, PK>(tabs.defer[1 + i], pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs,
+                               agg_lds);
+    __syncthreads();  // (the next partition's table clear after every read of this one's)
+  }
+}
+
 // order = the partitions by size class, heavy first (> 8x the mean pairs, then > 2x, then the
 // rest), each class in index order: the aggregation takes its partitions in this order, so a Zipf hot
 // key's partition starts in the first wave of workgroups instead of extending the tail. One
 // workgroup, P <= 8192 (a stable three-way split by block scans; a full sort by size cost 27 us).
 constexpr int kOrdPer = 8;  // partitions per thread
+// Hot-key split (k_nagg_hot): partitions above 2x the mean are cut into chunks of kHotChunk pairs.
+constexpr int kHotBlock = 1024, kHotK = 16;
+constexpr uint32_t kHotChunk = uint32_t(kHotBlock) * kHotK;
+// hinfo (with tabs.hot): [0] the heavy partitions (order[0 .. nheavy)), [1 + i] the first chunk of heavy
+// partition i, [1 + nheavy] the chunk total; every partition's hot words cleared.
 __global__ __launch_bounds__(1024) void k_nagg_order(const uint32_t* __restrict__ ps, uint32_t P,
-                                                     uint32_t* __restrict__ order, NaggTabs tabs) {
-  __shared__ uint32_t wsum[16];
-  __shared__ uint32_t base;
+                                                     uint32_t* __restrict__ order, NaggTabs tabs,
+                                                     uint32_t* __restrict__ hinfo) {
+  __shared__ uint32_t wsum[16], csum[16];
+  __shared__ uint32_t base, cbase;
   if (threadIdx.x < 4 * tabs.nt) tabs.counts[threadIdx.x / 4][threadIdx.x % 4] = 0;  // (the build's counts words)
+  if (threadIdx.x == 64 && tabs.defer) tabs.defer[0] = 0;
   const uint32_t mean = P ? (ps[P] - ps[0]) / P : 0u;
-  uint32_t cls[kOrdPer];
+  uint32_t cls[kOrdPer], nch[kOrdPer];
 #pragma unroll
   for (int k = 0; k < kOrdPer; ++k) {  // thread t holds partitions kOrdPer t + k
     const uint32_t p = kOrdPer * threadIdx.x + k;
     const uint32_t sz = p < P ? ps[p + 1] - ps[p] : 0u;
     cls[k] = p >= P ? 3u : sz > 8u * mean ? 0u : sz > 2u * mean ? 1u : 2u;
+    nch[k] = (sz + kHotChunk - 1) / kHotChunk;
+    if (tabs.hot && p < P) {
+      uint32_t* hw = tabs.hot + uint64_t(p) * kHotW;
+      hw[0] = 0;
+      hw[2] = 0;
+      hw[3] = kInvalid;
+      hw[4] = 0;
+    }
   }
-  if (threadIdx.x == 0) base = 0;
+  if (threadIdx.x == 0) base = cbase = 0;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   for (uint32_t c = 0; c < 3; ++c) {
-    uint32_t t = 0;
+    uint32_t t = 0, tc = 0;
 #pragma unroll
-    for (int k = 0; k < kOrdPer; ++k) t += cls[k] == c;
-    uint32_t wt;
-    const uint32_t wpre = wave_excl_scan(t, &wt);
-    if (lane == 0) wsum[wid] = wt;
+    for (int k = 0; k < kOrdPer; ++k) {
+      t += cls[k] == c;
+      tc += cls[k] == c ? nch[k] : 0u;
+    }
+    uint32_t wt, wc;
+    const uint32_t wpre = wave_excl_scan(t, &wt), cpre = wave_excl_scan(tc, &wc);
+    if (lane == 0) {
+      wsum[wid] = wt;
+      csum[wid] = wc;
+    }
     __syncthreads();
-    uint32_t pre = 0, tot = 0;
+    uint32_t pre = 0, tot = 0, cp = 0, ctot = 0;
 #pragma unroll
     for (int w = 0; w < 16; ++w) {
       pre += w < wid ? wsum[w] : 0u;
       tot += wsum[w];
+      cp += w < wid ? csum[w] : 0u;
+      ctot += csum[w];
     }
-    uint32_t at = base + pre + wpre;
+    uint32_t at = base + pre + wpre, ch = cbase + cp + cpre;
 #pragma unroll
     for (int k = 0; k < kOrdPer; ++k)
-      if (cls[k] == c) order[at++] = kOrdPer * threadIdx.x + k;
+      if (cls[k] == c) {
+        if (hinfo && c < 2) hinfo[1 + at] = ch;  // (heavy: classes 0 and 1)
+        ch += nch[k];
+        order[at++] = kOrdPer * threadIdx.x + k;
+      }
     __syncthreads();
-    if (threadIdx.x == 0) base += tot;
+    if (threadIdx.x == 0) {
+      base += tot;
+      cbase += ctot;
+      if (hinfo && c == 1) {
+        hinfo[0] = base;
+        hinfo[1 + base] = cbase;
+      }
+    }
     __syncthreads();
+  }
+}
+
+// Hot keys of the heavy partitions, split off before the aggregation. A Zipf key can hold most of a
+// partition (config C: 829 K of its ~880 K pairs), and that partition's one workgroup then streamed it
+// twice while the rest of the chip had finished (k_nagg 1.19 ms, of which the heavy workgroup 1.0 ms;
+// the other partitions alone balance to ~0.7 ms). Here chunk c of the heavy partitions (kHotChunk pairs
+// held in registers) goes to one workgroup: it finds the partition's hot key from kHotBlock pairs
+// sampled evenly over the whole partition (every workgroup of the partition draws the same sample and
+// agrees; a key with fewer than a quarter of the votes: nothing to do), counts the key's rows and their
+// min row, claims its runs with one atomic per workgroup and writes the key's rows down from the end of
+// the partition's sub range (rows of a key have no order) and the other pairs, compacted, to
+// hpairs[ps[gp] ..]. nagg_one then streams only those (its `ext` mode) and gives the key the
+// sub range's suffix.
+__global__ __launch_bounds__(kHotBlock) void k_nagg_hot(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+                                                        const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ hinfo, NaggTabs tabs) {
+  constexpr int kNw = kHotBlock / kWave;
+  __shared__ uint32_t vk[kNw], vn[kNw], wh[kNw], wn[kNw], wm[kNw];
+  __shared__ uint32_t sH, sok, hbase, nbase;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+  const uint32_t nheavy = hinfo[0], nchunks = hinfo[1 + nheavy];
+  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
+    uint32_t lo = 0, hi = nheavy;  // the heavy partition holding chunk c: largest i with hinfo[1 + i] <= c
+    while (hi - lo > 1) {
+      const uint32_t md = (lo + hi) >> 1;
+      if (hinfo[1 + md] <= c) lo = md;
+      else hi = md;
+    }
+    const uint32_t gp = order[lo], k = c - hinfo[1 + lo];
+    const uint32_t e0 = ps[gp], total = ps[gp + 1] - e0;
+    {  // the partition's hot key: each wave votes for its lane 0's sampled key
+      const uint32_t key = pairs[e0 + uint32_t(uint64_t(total) * threadIdx.x / kHotBlock)].x;
+      const uint32_t cand = uint32_t(__builtin_amdgcn_readlane(int(key), 0));
+      const uint32_t votes = uint32_t(__popcll(__ballot(key == cand)));
+      if (lane == 0) {
+        vk[wid] = cand;
+        vn[wid] = votes;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      uint32_t best = 0, H = 0;
+      for (int w = 0; w < kNw; ++w) {
+        uint32_t sc = 0;
+        for (int w2 = 0; w2 < kNw; ++w2) sc += vk[w2] == vk[w] ? vn[w2] : 0u;
+        if (sc > best) {
+          best = sc;
+          H = vk[w];
+        }
+      }
+      sH = H;
+      sok = best >= kHotBlock / 4;
+    }
+    __syncthreads();
+    if (!sok) continue;  // (uniform: every chunk of the partition skips it)
+    const uint32_t H = sH;
+    const uint32_t c0 = k * kHotChunk, m = min(kHotChunk, total - c0);
+    uint2 v[kHotK];
+#pragma unroll
+    for (int u = 0; u < kHotK; ++u) v[u] = pairs[e0 + c0 + min(uint32_t(u) * kHotBlock + threadIdx.x, m - 1)];
+    uint32_t mn = kInvalid, nh = 0, nn = 0;
+#pragma unroll
+    for (int u = 0; u < kHotK; ++u) {
+      const bool valid = uint32_t(u) * kHotBlock + threadIdx.x < m, h = valid && v[u].x == H;
+      mn = h ? min(mn, v[u].y) : mn;
+      const uint64_t bh = __ballot(h), bv = __ballot(valid);
+      nh += uint32_t(__popcll(bh));
+      nn += uint32_t(__popcll(bv & ~bh));
+    }
+    mn = wave_min_u32(mn);
+    if (lane == 0) {
+      wh[wid] = nh;
+      wn[wid] = nn;
+      wm[wid] = mn;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {  // the waves' exclusive prefixes, the workgroup's runs claimed
+      uint32_t th = 0, tn = 0, tm = kInvalid;
+      for (int w = 0; w < kNw; ++w) {
+        const uint32_t x = wh[w], y = wn[w];
+        wh[w] = th;
+        wn[w] = tn;
+        th += x;
+        tn += y;
+        tm = min(tm, wm[w]);
+      }
+      uint32_t* hw = tabs.hot + uint64_t(gp) * kHotW;
+      hbase = th ? atomicAdd(&hw[2], th) : 0u;
+      nbase = tn ? atomicAdd(&hw[4], tn) : 0u;
+      if (th) atomicMin(&hw[3], tm);
+      if (k == 0) {  // (the partition's other chunks agree on H)
+        hw[1] = H;
+        hw[0] = 1;
+      }
+    }
+    __syncthreads();
+    const uint32_t ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u;
+    uint32_t* __restrict__ sub = tabs.sub[ti];
+    const uint32_t send = e0 - ps[ti * tabs.P] + total;  // one past the partition's last sub row
+    uint32_t hc = hbase + wh[wid], nc = nbase + wn[wid];
+#pragma unroll
+    for (int u = 0; u < kHotK; ++u) {
+      const bool valid = uint32_t(u) * kHotBlock + threadIdx.x < m, h = valid && v[u].x == H;
+      const uint64_t bh = __ballot(h), bn = __ballot(valid) & ~bh;
+      if (h) sub[send - 1 - (hc + uint32_t(__popcll(bh & lt)))] = v[u].y;
+      else if (valid) tabs.hpairs[e0 + nc + uint32_t(__popcll(bn & lt))] = v[u];
+      hc += uint32_t(__popcll(bh));
+      nc += uint32_t(__popcll(bn));
+    }
+    __syncthreads();  // (the shared words of the next chunk)
   }
 }
 
@@ -1021,8 +1245,9 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
-__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts) {
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts, uint32_t* __restrict__ defer) {
   if (threadIdx.x < 4) counts[threadIdx.x] = threadIdx.x == 3 && ctl[0] != 0 ? 1u : 0u;  // ctl[0]: the overflow count
+  if (threadIdx.x == 4) defer[0] = 0;
   __syncthreads();
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
@@ -1101,16 +1326,20 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // (n uint4) | starts | key counts, order
   if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSlot].ensure((3 * uint64_t(PT) + 6) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSlot].ensure(((5 + kHotW) * uint64_t(PT) + 16) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + PT + 1;
   uint32_t* fps = order + PT + 1;  // two levels: the fine partitions' starts (PT + 1)
+  uint32_t* defer = fps + PT + 1;  // the register form's deferred partitions (count, PT indices)
+  uint32_t* hinfo = defer + PT + 1;  // hot-key split: heavy partitions and their chunks (PT + 2)
+  uint32_t* hotw = hinfo + PT + 2;   // hot-key split: kHotW words per partition
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
   NaggTabs tabs;
   tabs.P = P;
   tabs.nt = nt;
   tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
+  tabs.defer = defer;
   // the hot-key election of the streaming form: in every partition, in partitions above 5/4 of the
   // mean only, or nowhere (HJ3D_NAGG_ELECT 1 / 2 / 0)
   tabs.elect_min = HJ3D_NAGG_ELECT == 1 ? 0u
@@ -1138,7 +1367,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     src.pk = sl.pk;
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
-    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0]);
+    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0], tabs.defer);
   } else if (two) {
     uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
     uint32_t np = 0;
@@ -1146,7 +1375,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = fps;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, nullptr);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
@@ -1158,7 +1387,14 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = pst;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs);
+    const bool hs = HJ3D_NAGG_HOTSPLIT != 0;
+    if (hs) {  // the other pairs of heavy partitions, compacted (at most every pair)
+      if ((e = ctx->scratch[kScrSortV].ensure(n * sizeof(uint2))) != hipSuccess) return e;
+      tabs.hot = hotw;
+      tabs.hpairs = ctx->scratch[kScrSortV].as<uint2>();
+    }
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, hs ? hinfo : nullptr);
+    if (hs) hipLaunchKernelGGL(k_nagg_hot, dim3(2 * G), dim3(kHotBlock), 0, s, pairs, ps, order, hinfo, tabs);
   }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
@@ -1179,18 +1415,21 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, false>),
                           reinterpret_cast<const void*>(&k_nagg<kSmallBlock, kSmallSlots, true>),
                           reinterpret_cast<const void*>(&k_nagg<1024, 10, false>),
-                          reinterpret_cast<const void*>(&k_nagg<1024, 10, true>)})
+                          reinterpret_cast<const void*>(&k_nagg<1024, 10, true>),
+                          reinterpret_cast<const void*>(&k_nagg_defer<kSmallBlock, kSmallSlots, false>),
+                          reinterpret_cast<const void*>(&k_nagg_defer<kSmallBlock, kSmallSlots, true>),
+                          reinterpret_cast<const void*>(&k_nagg_defer<1024, 10, false>),
+                          reinterpret_cast<const void*>(&k_nagg_defer<1024, 10, true>)})
       if ((e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024)) != hipSuccess) return e;
     lds_attr = true;
   }
-  // the small form's table: ~2.5 slots per bucket where that still fits two workgroups per CU (a lower
-  // load factor leaves fewer keys off their home slot: config D shape 18.06 -> 17.73 ms), else ~1.5
-  uint32_t cap512 = 0;
-  for (const double f : {double(HJ3D_NAGG_CAPF), 1.5}) {
-    const uint32_t want = uint32_t(f * W) + kSmallBlock + 64;  // + the insert slack
-    cap512 = prime_at_least(want < 2048 ? 2048 : want);
-    if (cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) break;
-  }
+  // the small form's table: ~1.5 slots per bucket, which leaves its pass-B image room for a config-D
+  // slice's rows (15.4 K pairs; 2.5 slots per bucket left 11.6 K: D shape 17.7 -> 16.6 ms)
+  const uint32_t cap512 = prime_at_least(std::max<uint32_t>(2048, uint32_t(HJ3D_NAGG_CAPF * W) + kSmallBlock + 64));
+  const bool small = HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= kSmallLds;
+  // the 1024-thread form's table (one workgroup per CU: the whole LDS, the image takes what the table leaves)
+  // (a smaller table for a larger image measured slower at config C: 1.87 -> 1.90 ms at 1.2 slots per bucket)
+  const uint32_t cap1024 = kAggCapMax;
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)
@@ -1216,23 +1455,40 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
                            capr, src, tabs, order);
     }
     if (path) *path = pk ? "nested_agg_slices_reg" : two ? "nested_agg_2l_reg" : "nested_agg_reg";
-  } else if (HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= 81920) {
-    const size_t lds = agg_lds_words(cap512, W, kSmallBlock) * sizeof(uint32_t);
+    // the partitions it left (usually none), in k_nagg's streaming form
+    if (small) {
+      tabs.ldsw = kSmallLds / 4;
+      if (pk)
+        hipLaunchKernelGGL((k_nagg_defer<kSmallBlock, kSmallSlots, true>), dim3(2 * G), dim3(kSmallBlock), kSmallLds, s,
+                           pairs, ps, t->fm, lo, nbl, nbg, W, mtmp, dcount, cap512, src, tabs);
+      else
+        hipLaunchKernelGGL((k_nagg_defer<kSmallBlock, kSmallSlots, false>), dim3(2 * G), dim3(kSmallBlock), kSmallLds,
+                           s, pairs, ps, t->fm, lo, nbl, nbg, W, mtmp, dcount, cap512, src, tabs);
+    } else {
+      tabs.ldsw = kBigLds / 4;
+      if (pk)
+        hipLaunchKernelGGL((k_nagg_defer<1024, 10, true>), dim3(G), dim3(1024), kBigLds, s, pairs, ps, t->fm, lo, nbl,
+                           nbg, W, mtmp, dcount, cap1024, src, tabs);
+      else
+        hipLaunchKernelGGL((k_nagg_defer<1024, 10, false>), dim3(G), dim3(1024), kBigLds, s, pairs, ps, t->fm, lo, nbl,
+                           nbg, W, mtmp, dcount, cap1024, src, tabs);
+    }
+  } else if (small) {
+    tabs.ldsw = kSmallLds / 4;
     if (pk)
-      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, true>), dim3(PT), dim3(kSmallBlock), kSmallLds, s, pairs, ps,
                          t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
     else
-      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), lds, s, pairs, ps,
-                         t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
+      hipLaunchKernelGGL((k_nagg<kSmallBlock, kSmallSlots, false>), dim3(PT), dim3(kSmallBlock), kSmallLds, s, pairs,
+                         ps, t->fm, lo, nbl, nbg, W, mtmp, dcount, order, cap512, src, tabs);
   } else {
-    const uint32_t cap = kAggCapMax;
-    const size_t lds = agg_lds_words(cap, W, 1024) * sizeof(uint32_t);
+    tabs.ldsw = kBigLds / 4;
     if (pk)
-      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs);
+      hipLaunchKernelGGL((k_nagg<1024, 10, true>), dim3(PT), dim3(1024), kBigLds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap1024, src, tabs);
     else
-      hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(PT), dim3(1024), lds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
-                         mtmp, dcount, order, cap, src, tabs);
+      hipLaunchKernelGGL((k_nagg<1024, 10, false>), dim3(PT), dim3(1024), kBigLds, s, pairs, ps, t->fm, lo, nbl, nbg, W,
+                         mtmp, dcount, order, cap1024, src, tabs);
   }
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // for its table and the caller, which reads the counts at the table's next use, runs the sort

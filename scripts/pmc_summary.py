@@ -38,7 +38,7 @@ KERNELS = ("k_pk_probe", "k_pk_part", "k_pk_build", "k_rp_probe_seg", "k_rp_part
            "k_scan_tiles",
            # nested (config C) and experiment-4 (config E) kernels
            "k_nagg_mains", "k_nagg_order", "k_nagg_rebase", "k_nagg_counts", "k_nagg_ps_shift", "k_nagg_pk_ovf",
-           "k_nagg", "k_rn_probe_seg", "k_expand_light",
+           "k_nagg_hot", "k_nagg_defer", "k_nagg_reg", "k_nagg", "k_rn_probe_seg", "k_expand_light",
            "k_expand_heavy_flat", "k_heavy_offsets", "k_ndu_seg", "k_ndu_heavy", "k_ndu", "k_rs_scatter", "k_rs_hist",
            "k_pk_split", "k_xpart", "k_dv_part", "k_dv_bits", "k_dv_merge")
 

@@ -557,6 +557,45 @@ def _zipf_keys(rng, n, dom, theta):
     return np.searchsorted(c, rng.random(n)).astype(np.uint32)
 
 
+@pytest.mark.parametrize("explicit,nb,path", [(False, 200_003, "nested_agg"), (True, 400_009, "nested_agg_reg")],
+                         ids=["streaming_implicit_rows", "register_form_explicit_rows"])
+def test_build_many_hot_key_split(ctx, explicit, nb, path):
+    """Two nested tables in one hj3d_build_many whose heavy partitions are dominated by one Zipf key
+    each: k_nagg_hot splits the key off before the aggregation (its rows written down from the end of
+    the partition's sub range, the other pairs compacted), in both tables (table 1's sub rows are
+    numbered from its own first pair) and with explicit row ids; with ~25 K pairs per partition the
+    streaming aggregation runs, with ~13 K the register form, which leaves the split partitions to
+    the streaming form (k_nagg_defer). Counters, output checksums and statistics equal the oracle's
+    per table (HtNested1::insert, ht_nested.hh:287-311)."""
+    import hj3d
+    rng = np.random.default_rng(77 + explicit)
+    n, dom = 5_000_000, 600_000
+    rels, brow = [], []
+    for k in range(2):
+        r = np.zeros((n, 3), np.uint32)
+        r[:, 1] = (_zipf_keys(rng, n, dom, 0.9 + 0.2 * k) * 7 + k) % dom
+        if explicit:
+            r[:, 2] = np.sort(rng.choice(2_000_000_000, n, replace=False)).astype(np.uint32)
+        rels.append(r)
+        brow.append(2 if explicit else None)
+    P = O.tuples3(rng.integers(0, dom, 700_000, dtype=np.uint32), np.zeros(700_000, np.uint32))
+    exp = [O.nested_plan(rels[k], 1, P, 0, nb, True, brow=brow[k]) for k in range(2)]
+    ts = [hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb) for _ in range(2)]
+    dr = [dev(r) for r in rels]
+    ctx.build_many(ts, [hj3d.Rel(dr[k], 1, row_word=brow[k]) for k in range(2)])
+    dP = dev(P)
+    for k in range(2):
+        assert ts[k].build_path() == path, ts[k].build_path()
+        got = ctx.probe(ts[k], hj3d.Rel(dP, 0), unnest=True)
+        e = exp[k]
+        assert (got.n_matched, got.n_cmps, got.n_out) == (e.c_probe, e.c_cmp, e.c_unnest), k
+        assert {f: getattr(got, f) for f in ("sum_a", "sum_b", "sum_h", "xor_h")} == \
+            {f: e.out[f] for f in ("sum_a", "sum_b", "sum_h", "xor_h")}, k
+        assert {f: ts[k].stats()[f] for f in STAT_KEYS} == {f: e.stats[f] for f in STAT_KEYS}, k
+    for t in ts:
+        t.close()
+
+
 @pytest.mark.parametrize("explicit", [1, 0], ids=["r1_explicit", "r0_explicit"])
 def test_build_many_mixed_row_modes(ctx, explicit):
     """hj3d_build_many partitions both relations in one pass. With one relation on implicit rows and
