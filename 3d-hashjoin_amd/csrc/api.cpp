@@ -200,7 +200,6 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
     case HJ3D_OPT_PK_BUILD: ctx->pk_build = value != 0; return HJ3D_OK;
     case HJ3D_OPT_NESTED_PK: ctx->nested_pk = value != 0; return HJ3D_OK;
     case HJ3D_OPT_SYNC_BUILD: ctx->sync_build = value != 0; return HJ3D_OK;
-    case HJ3D_OPT_NESTED_2L: ctx->nested_2l = value != 0; return HJ3D_OK;
     case HJ3D_OPT_RP_UNFUSED: ctx->rp_unfused = value != 0; return HJ3D_OK;
     case HJ3D_OPT_DIAG_GBAR:
       if (value < 0) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_DIAG_GBAR: >= 0");

@@ -97,7 +97,6 @@ struct hj3d_ctx {
   uint32_t pk_stage = 0;          // HJ3D_OPT_PK_STAGE: carry-flush threshold of its partitioner (0 = the stage)
   bool pk_build = false;          // HJ3D_OPT_PK_BUILD: the slice build (pk_build) for every chaining table it takes
   bool nested_pk = false;         // HJ3D_OPT_NESTED_PK: the nested aggregation build on pk_slices always
-  bool nested_2l = false;         // HJ3D_OPT_NESTED_2L: the exact two-level partition + register aggregation
   bool rp_unfused = false;        // HJ3D_OPT_RP_UNFUSED: small build partitions as histogram + scatter launches
   bool sync_build = false;        // HJ3D_OPT_SYNC_BUILD: nested builds resolved before hj3d_build returns
   // control words of the packed probe (chain_pk.hip): zero between probes (its last workgroup
@@ -288,13 +287,6 @@ hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStrea
 // P .. 2P - 1 (ps[P .. 2P]), its pairs follow r's.
 hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t W, uint2* out,
                                  uint32_t* ps, uint32_t* nparts, hipStream_t s, const hj3d_rel* r1 = nullptr);
-// The same into narrow partitions (Wf buckets, up to 8192 of them), exact under any skew: a fine
-// histogram, the whole-segment scatter into coarse partitions of C fine ones, then the split of
-// every coarse partition (k_rp_hist2, k_rp_wscatter, k_rp_split2). Partition p is out[fps[p] ..
-// fps[p+1]). Uses kScrPHist, kScrSortV, kScrPStart. hipErrorNotSupported beyond 8192 partitions
-// or where one level suffices.
-hipError_t radix_partition_pairs_2l(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t Wf, uint2* out,
-                                    uint32_t* fps, uint32_t* nparts, hipStream_t s);
 // after every chaining build: buckets of <= 32 entries sorted by row (single-pass probe order)
 hipError_t sort_small_buckets(hj3d_ctx* ctx, hj3d_table* t, hipStream_t s);
 // sel (nullable, <= 2 predicates): the selection fused into the probe-side partitioner; tuples

@@ -31,81 +31,33 @@
 namespace hj3d {
 namespace {
 
-#ifndef HJ3D_NAGG_WMAX
-#define HJ3D_NAGG_WMAX 6144
-#endif
-constexpr uint32_t kAggW = HJ3D_NAGG_WMAX;  // max buckets per partition (one LDS table round at fill <= ~1.3)
-
-// LDS hash table slots (prime, sized per build: ~1.6 slots per bucket of the partition + the insert
-// slack below; at most 10223): with double hashing every probe step visits all slots (double
-// hashing measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6). The table
-// lives in dynamic LDS, so small partitions (config E) run two 512-thread workgroups per CU.
+// max buckets per partition (one LDS table round at fill <= ~1.3)
+constexpr uint32_t kAggW = 6144;
+// LDS hash table slots (prime, sized per build: ~1.5 slots per bucket of the partition + the insert
+// slack; at most 10223): with double hashing every probe step visits all slots (double hashing
+// measured 2.25 -> 1.94 ms against linear probing for uniform keys at load ~0.6). The table lives in
+// dynamic LDS, so small partitions (configs D, E) run two 512-thread workgroups per CU.
 constexpr uint32_t kAggCapMax = 10223;
-// new keys are admitted while fewer than cap - BLOCK - 64 are in the table: at most BLOCK inserts
-// race past the test, so the table never fills and every probe sequence ends
 constexpr uint32_t kAggRounds = 1;  // initial rounds per partition (2, 3: slower under Zipf, pairs re-read)
 constexpr uint32_t kAggMinSpan = 384;  // smallest bucket range per round before giving up
-#ifndef HJ3D_NAGG_U
-#define HJ3D_NAGG_U 8
-#endif
-constexpr int kAggU = HJ3D_NAGG_U;   // pairs per thread and step (the next step's in flight)
-#ifndef HJ3D_NAGG_SMALL
-#define HJ3D_NAGG_SMALL 1  // small partitions: two 512-thread workgroups per CU with a smaller table (0: A/B)
-#endif
-#ifndef HJ3D_NAGG_SB
-#define HJ3D_NAGG_SB 512  // threads of the small-partition form (A/B: 256, four workgroups per CU)
-#endif
-constexpr int kSmallBlock = HJ3D_NAGG_SB;
+constexpr int kAggU = 8;  // pairs per thread and step (the next step's in flight; 4 / 16: slower)
+// the small-partition form: two 512-thread workgroups per CU (256 threads, four per CU: slower)
+constexpr int kSmallBlock = 512;
 constexpr int kSmallSlots = 6144 / kSmallBlock;  // table slots per thread (cap <= 6144)
 constexpr size_t kSmallLds = 81920, kBigLds = 160 * 1024;  // dynamic LDS of the two forms (two / one per CU)
-#ifndef HJ3D_NAGG_PER_CU
-#define HJ3D_NAGG_PER_CU 2  // target partitions per CU when the table is small (A/B: 4 with 256 threads)
-#endif
-#ifndef HJ3D_NAGG_WHOLE
-#define HJ3D_NAGG_WHOLE 1  // a round over the partition's whole bucket range skips the per-pair range test (0: A/B)
-#endif
-#ifndef HJ3D_NAGG_PKWAVE
-#define HJ3D_NAGG_PKWAVE 1  // slices: each wave walks whole fine regions (0: every lane searches its item's region)
-#endif
-#ifndef HJ3D_NAGG_PKW
-#define HJ3D_NAGG_PKW 1536  // buckets per partition on the packed slices (0: the kAggW-based width).
-// Uniform keys, 1e9 tuples / 1e8 buckets: 26.1 ms (5,357 buckets, one 1024-thread workgroup per CU)
-// -> 19.9 ms (2,048) -> 18.5 ms (1,536; two 512-thread workgroups per CU, a quarter of the sub-row
-// window); 1,024 exceeds the 65,536 slices (profiles/r04n_ab_pkw.log)
-#endif
-#ifndef HJ3D_NAGG_REG
-#define HJ3D_NAGG_REG 1  // partitions of at most ~14 K expected pairs: the register form k_nagg_reg (0: A/B)
-#endif
-#ifndef HJ3D_NAGG_REG_SLOTS
-#define HJ3D_NAGG_REG_SLOTS 4  // largest register-form table: SLOTS x 1024 slots (6: A/B, config E's 5,701)
-#endif
-#ifndef HJ3D_NAGG_REG_FILL
-#define HJ3D_NAGG_REG_FILL 0.85  // largest mean partition (fraction of the register capacity) for k_nagg_reg
-#endif
-#ifndef HJ3D_NAGG_2L
-// one-level partitions too large for k_nagg_reg: the exact two-level partition + k_nagg_reg. Off by
-// default: at config C it measured 2.93 against 2.25 ms for the one-level partition + k_nagg (the
-// narrow partitions' fixed costs outweigh the saved pair traffic); HJ3D_OPT_NESTED_2L
-// turns it on per context (tests, A/B)
-#define HJ3D_NAGG_2L 0
-#endif
-#ifndef HJ3D_NAGG_WAVES
-#define HJ3D_NAGG_WAVES 1  // partition count rounded up to whole waves of workgroups (0: A/B)
-#endif
-
-#ifndef HJ3D_NAGG_CAPF
-#define HJ3D_NAGG_CAPF 1.5  // small form: LDS table slots per bucket of the partition (+ the insert slack)
-#endif
-#ifndef HJ3D_NAGG_HOT
-#define HJ3D_NAGG_HOT 1  // heavy partitions: the hot key's rows on the register path (0: A/B)
-#endif
-#ifndef HJ3D_NAGG_ELECT
-#define HJ3D_NAGG_ELECT 2  // hot-key wave leader election: 2 partitions above 5/4 of the mean size (default), 1 every partition, 0 none
-#endif
-#ifndef HJ3D_NAGG_HOTSPLIT
-#define HJ3D_NAGG_HOTSPLIT 1  // heavy one-level partitions: hot key split off first (k_nagg_hot; 0: A/B)
-#endif
-
+constexpr double kSmallCapF = 1.5;  // small form: table slots per bucket of the partition (+ the insert slack)
+constexpr uint32_t kPartsPerCu = 2;  // target partitions per CU (4: config E 0.27 -> 0.34 ms)
+// buckets per partition on the packed slices. Uniform keys, 1e9 tuples / 1e8 buckets: 26.1 ms (5,357
+// buckets, one 1024-thread workgroup per CU) -> 19.9 ms (2,048) -> 18.5 ms (1,536; two 512-thread
+// workgroups per CU, a quarter of the sub-row window); 1,024 exceeds the 65,536 slices
+// (profiles/r04n_ab_pkw.log)
+constexpr uint32_t kPkW = 1536;
+// the register form k_nagg_reg: mean partitions of at most kRegFill of its capacity, tables of at most
+// kRegSlots x 1024 slots (6, which takes config E's 5,701: 0.27 -> 0.29 ms)
+constexpr double kRegFill = 0.85;
+constexpr uint32_t kRegSlots = 4;
+// the streaming form's hot-key wave leader election: in partitions above 5/4 of the mean size (in
+// every partition: measured slower; duplicates inside a wave are rare elsewhere)
 #ifndef HJ3D_NAGG_CLK
 #define HJ3D_NAGG_CLK 0  // diagnostic: per-workgroup phase clocks of k_nagg (read by hj3d_diag_nagg_clk)
 #endif
@@ -116,7 +68,13 @@ __device__ uint64_t g_nagg_clk[kClkParts * kClkPts];
 // point k of partition gp's timeline: 100 MHz wall clock (point 7: the workgroup's dispatch index)
 __device__ __forceinline__ void nagg_clk(uint32_t gp, int k) {
 #if HJ3D_NAGG_CLK
-  if (threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + k] = k == 7 ? blockIdx.x : wall_clock64();
+  if (threadIdx.x == 0 && gp < kClkParts) {
+    g_nagg_clk[gp * kClkPts + k] = k == 7 ? blockIdx.x : wall_clock64();
+    // point 6: where the workgroup runs, {XCC_ID, HW_ID} (CU, SH, SE of wave 0)
+    if (k == 0)
+      g_nagg_clk[gp * kClkPts + 6] = (uint64_t(__builtin_amdgcn_s_getreg((31 << 11) | 20)) << 32) |
+                                     uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
+  }
 #else
   (void)gp;
   (void)k;
@@ -348,13 +306,13 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   // the compiler waits for the batch in flight with a counted s_waitcnt at its use, not vmcnt(0) right
   // after issuing it (a data-dependent number of loads, or of stores in pass B, made every step wait
   // for the next step's loads). Contiguous form: item i0 + u * BLOCK + tid of the partition.
-  // Slices (PK, HJ3D_NAGG_PKWAVE): wave w walks the fine regions w, w + waves, ... one after another,
+  // Slices (PK): wave w walks the fine regions w, w + waves, ... one after another,
   // a step being kAggU x 64 consecutive items of one region, so no item searches for its region.
   // body(v, valid): v the step's pairs, valid the bit mask of the lane's real items.
   const uint32_t wid = threadIdx.x / kWave;
   const auto stream = [&](auto&& body) __attribute__((always_inline)) {
     uint2 v[kAggU], nv[kAggU];
-    if constexpr (PK && HJ3D_NAGG_PKWAVE) {
+    if constexpr (PK) {
       const auto rlen = [&](uint32_t r) __attribute__((always_inline)) { return rstart[r + 1] - rstart[r]; };
       const auto skip = [&](uint32_t r) __attribute__((always_inline)) {  // the next non-empty region from r
         while (r < src.S2 && rlen(r) == 0) r += kNw;
@@ -424,10 +382,10 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   const uint32_t wid_ = threadIdx.x / kWave;
   while (c0 < nbs) {
     const uint32_t c1 = min(nbs, c0 + span);
-    const bool whole = HJ3D_NAGG_WHOLE && c0 == 0 && c1 == nbs;
+    const bool whole = c0 == 0 && c1 == nbs;
     // a key that no key of this round is: its bucket lies outside [b0 + c0, b0 + c1)
     const uint32_t empty = PK ? (c1 << src.pk.qbits) : uint32_t((uint64_t(lo) + b0 + c1) % nb_global);
-    // Hot key (HJ3D_NAGG_HOT; heavy partitions, one round over the whole range): a Zipf key holding
+    // Hot key (heavy partitions, one round over the whole range): a Zipf key holding
     // most of a partition's rows (config C: 829 K of ~880 K) made its workgroup the launch's
     // critical path (1.2 of 1.34 ms), each of its rows paying the wave-leader election in both
     // passes. The key is found from BLOCK pairs sampled evenly over the partition (each wave votes for
@@ -437,7 +395,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     // counts: both passes walk the stream in one order) + a running ballot count: no LDS atomic.
     // (split off: the key is this round's when its bucket is)
     uint32_t H = ext && (whole || lbk(hw[1]) - c0 < c1 - c0) ? hw[1] : empty;
-    if (!ext && HJ3D_NAGG_HOT && elect && whole && total >= 4u * BLOCK) {
+    if (!ext && elect && whole && total >= 4u * BLOCK) {
       if constexpr (PK) __syncthreads();  // (the region starts written above)
       const uint32_t f = uint32_t(uint64_t(total) * threadIdx.x / BLOCK);
       uint32_t key;
@@ -764,11 +722,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_nagg(const uint2* __restrict__ pai
 // of the partition's sub range, and the image goes out as whole lines. Per pair: 8 B read + 4 B
 // written. A partition with more pairs than kRegCap (a Zipf hot key's) or more distinct keys than
 // the table holds takes k_nagg's streaming form (nagg_one) in place, in the same workgroup.
-#ifndef HJ3D_NAGG_REGK
-#define HJ3D_NAGG_REGK 16
-#endif
 constexpr int kRegBlock = 1024;
-constexpr int kRegK = HJ3D_NAGG_REGK;                          // pairs per lane
+constexpr int kRegK = 16;                                      // pairs per lane (20, 24: spills)
 constexpr uint32_t kRegCap = uint32_t(kRegK) * kRegBlock;      // pairs per partition (16384)
 __host__ __device__ constexpr uint32_t reg_lds_words(uint32_t cap, uint32_t W) {
   return 3 * cap + W + kRegCap + kRegBlock / 64 + 2 + 2 * (kAggMaxS2 + 2);
@@ -1287,51 +1242,36 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // time, latency-bound, so a last wave of a few partitions costs as long as a full one): config C
   // 9.6M buckets -> 1792 partitions of 5357 (7 waves) instead of 1563 of 6144 (6.1 waves, run as 7).
   const uint32_t G = uint32_t(ctx->num_cus);
-  uint32_t W = uint32_t((uint64_t(nbl) + HJ3D_NAGG_PER_CU * G - 1) / (HJ3D_NAGG_PER_CU * G));
+  uint32_t W = uint32_t((uint64_t(nbl) + kPartsPerCu * G - 1) / (kPartsPerCu * G));
   W = W < 1024 ? 1024 : W > kAggW ? kAggW : W;
   bool pk = false;  // more than 2048 partitions: the packed partitioner's slices (pk_slices)
   {
     const uint64_t P0 = (uint64_t(nbl) + W - 1) / W, P1 = (P0 + G - 1) / G * G;
     const uint64_t W1 = (uint64_t(nbl) + P1 - 1) / P1;
-    if (HJ3D_NAGG_WAVES && P1 <= 2048 && W1 >= 1024) W = uint32_t(W1);
+    if (P1 <= 2048 && W1 >= 1024) W = uint32_t(W1);
     if (P0 > 2048 || ctx->nested_pk) {
       pk = true;
       W = uint32_t(W1 >= 1024 ? W1 : W);
-      // the slices take any partition count: HJ3D_NAGG_PKW buckets per partition (0: as above),
+      // the slices take any partition count: kPkW buckets per partition,
       // narrow enough for the small form's two workgroups per CU and a small sub-row window
       // (at most 65536 slices: pk_slices' two levels of 1024 x 64)
-      if (HJ3D_NAGG_PKW) W = std::min<uint32_t>(W, std::max<uint32_t>(HJ3D_NAGG_PKW, (nbl + 65535) / 65536));
-    }
-  }
-  // one level too coarse for the register form (config C: 1792 partitions of ~56 K pairs): the exact
-  // two-level partition into up to 8192 narrow ones (radix_partition_pairs_2l; skew-safe, unlike the
-  // slices' fixed regions), rounded to whole waves of the aggregation's workgroups
-  bool two = false;
-  if (!pk && nt == 1 && (HJ3D_NAGG_2L || ctx->nested_2l) && double(n) * W / nbl > 0.85 * kRegCap) {
-    uint64_t Pf = std::max<uint64_t>((uint64_t(nbl) + 8191) / 8192, uint64_t(double(n) / (0.6 * kRegCap)));
-    Pf = std::min<uint64_t>((Pf + G - 1) / G * G, 8192);
-    const uint32_t Wf = uint32_t((uint64_t(nbl) + Pf - 1) / Pf);
-    const uint32_t Pf2 = (nbl + Wf - 1) / Wf, C = (Pf2 + 1023) / 1024;
-    if (Wf >= 64 && C >= 2 && C <= 16) {
-      two = true;
-      W = Wf;
+      W = std::min<uint32_t>(W, std::max<uint32_t>(kPkW, (nbl + 65535) / 65536));
     }
   }
   const uint32_t P = (nbl + W - 1) / W;
   if (pk && nt > 1) return hipErrorNotSupported;  // one table at a time on the slices
-  if (!pk && uint64_t(P) * nt > (two ? 8192u : 2048u)) return hipErrorNotSupported;  // k_nagg_order's limit
+  if (!pk && uint64_t(P) * nt > 2048u) return hipErrorNotSupported;  // k_nagg_order's limit
   const uint32_t PT = P * nt;  // partitions over every table
-  if (path) *path = pk ? "nested_agg_slices" : two ? "nested_agg_2l" : "nested_agg";
+  if (path) *path = pk ? "nested_agg_slices" : "nested_agg";
   // scratch: pairs (n uint2; PK: the fine regions of pk_slices) | main records before compaction
   // (n uint4) | starts | key counts, order
   if (!pk && (e = ctx->scratch[kScrPairs].ensure(n * sizeof(uint2))) != hipSuccess) return e;
   if ((e = ctx->scratch[kScrSortK].ensure(n * sizeof(uint4))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSlot].ensure(((5 + kHotW) * uint64_t(PT) + 16) * sizeof(uint32_t))) != hipSuccess) return e;
+  if ((e = ctx->scratch[kScrSlot].ensure(((4 + kHotW) * uint64_t(PT) + 16) * sizeof(uint32_t))) != hipSuccess) return e;
   uint4* mtmp = ctx->scratch[kScrSortK].as<uint4>();
   uint32_t* dcount = ctx->scratch[kScrSlot].as<uint32_t>();  // PT + 1 (scanned in place into the main bases)
   uint32_t* order = dcount + PT + 1;
-  uint32_t* fps = order + PT + 1;  // two levels: the fine partitions' starts (PT + 1)
-  uint32_t* defer = fps + PT + 1;  // the register form's deferred partitions (count, PT indices)
+  uint32_t* defer = order + PT + 1;  // the register form's deferred partitions (count, PT indices)
   uint32_t* hinfo = defer + PT + 1;  // hot-key split: heavy partitions and their chunks (PT + 2)
   uint32_t* hotw = hinfo + PT + 2;   // hot-key split: kHotW words per partition
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
@@ -1340,11 +1280,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   tabs.nt = nt;
   tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
   tabs.defer = defer;
-  // the hot-key election of the streaming form: in every partition, in partitions above 5/4 of the
-  // mean only, or nowhere (HJ3D_NAGG_ELECT 1 / 2 / 0)
-  tabs.elect_min = HJ3D_NAGG_ELECT == 1 ? 0u
-                   : HJ3D_NAGG_ELECT == 2 ? uint32_t(std::min<uint64_t>(5 * n / (4 * uint64_t(PT)), 0xFFFFFFFFull))
-                                          : 0xFFFFFFFFu;
+  // the hot-key election of the streaming form: in partitions above 5/4 of the mean only
+  tabs.elect_min = uint32_t(std::min<uint64_t>(5 * n / (4 * uint64_t(PT)), 0xFFFFFFFFull));
   for (uint32_t k = 0; k < nt; ++k) {
     tabs.pbase[k] = k ? uint32_t(rr[0].n) : 0u;
     tabs.off[k] = tt[k]->off.as<uint32_t>();
@@ -1368,14 +1305,6 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
     hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0], tabs.defer);
-  } else if (two) {
-    uint2* pw = ctx->scratch[kScrPairs].as<uint2>();
-    uint32_t np = 0;
-    if ((e = radix_partition_pairs_2l(ctx, t, rr[0], W, pw, fps, &np, s)) != hipSuccess) return e;
-    if (np != P) return hipErrorNotSupported;
-    pairs = pw;
-    ps = fps;
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, nullptr);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
@@ -1387,14 +1316,13 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = pst;
-    const bool hs = HJ3D_NAGG_HOTSPLIT != 0;
-    if (hs) {  // the other pairs of heavy partitions, compacted (at most every pair)
+    {  // the other pairs of heavy partitions, compacted (at most every pair)
       if ((e = ctx->scratch[kScrSortV].ensure(n * sizeof(uint2))) != hipSuccess) return e;
       tabs.hot = hotw;
       tabs.hpairs = ctx->scratch[kScrSortV].as<uint2>();
     }
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, hs ? hinfo : nullptr);
-    if (hs) hipLaunchKernelGGL(k_nagg_hot, dim3(2 * G), dim3(kHotBlock), 0, s, pairs, ps, order, hinfo, tabs);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, hinfo);
+    hipLaunchKernelGGL(k_nagg_hot, dim3(2 * G), dim3(kHotBlock), 0, s, pairs, ps, order, hinfo, tabs);
   }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
@@ -1425,8 +1353,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   }
   // the small form's table: ~1.5 slots per bucket, which leaves its pass-B image room for a config-D
   // slice's rows (15.4 K pairs; 2.5 slots per bucket left 11.6 K: D shape 17.7 -> 16.6 ms)
-  const uint32_t cap512 = prime_at_least(std::max<uint32_t>(2048, uint32_t(HJ3D_NAGG_CAPF * W) + kSmallBlock + 64));
-  const bool small = HJ3D_NAGG_SMALL && cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= kSmallLds;
+  const uint32_t cap512 = prime_at_least(std::max<uint32_t>(2048, uint32_t(kSmallCapF * W) + kSmallBlock + 64));
+  const bool small = cap512 <= 6144 && agg_lds_words(cap512, W, kSmallBlock) * 4 <= kSmallLds;
   // the 1024-thread form's table (one workgroup per CU: the whole LDS, the image takes what the table leaves)
   // (a smaller table for a larger image measured slower at config C: 1.87 -> 1.90 ms at 1.2 slots per bucket)
   const uint32_t cap1024 = kAggCapMax;
@@ -1434,8 +1362,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)
   const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
-  const bool reg = HJ3D_NAGG_REG && double(n) / PT <= HJ3D_NAGG_REG_FILL * kRegCap &&
-                   capr <= uint32_t(HJ3D_NAGG_REG_SLOTS) * kRegBlock && reg_lds_words(capr, W) * 4 <= 160 * 1024;
+  const bool reg = double(n) / PT <= kRegFill * kRegCap &&
+                   capr <= kRegSlots * kRegBlock && reg_lds_words(capr, W) * 4 <= 160 * 1024;
   if (reg) {
     const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);
     const dim3 gr(std::min<uint32_t>(PT, G)), bl(kRegBlock);
@@ -1454,7 +1382,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
         hipLaunchKernelGGL((k_nagg_reg<false, 6>), gr, bl, lds, s, pairs, ps, t->fm, lo, nbl, nbg, W, PT, mtmp, dcount,
                            capr, src, tabs, order);
     }
-    if (path) *path = pk ? "nested_agg_slices_reg" : two ? "nested_agg_2l_reg" : "nested_agg_reg";
+    if (path) *path = pk ? "nested_agg_slices_reg" : "nested_agg_reg";
     // the partitions it left (usually none), in k_nagg's streaming form
     if (small) {
       tabs.ldsw = kSmallLds / 4;

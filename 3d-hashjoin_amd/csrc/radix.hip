@@ -578,165 +578,6 @@ __global__ __launch_bounds__(kPBlock) void k_rp_wscatter(RelTiles rt, FastMod fm
   flush_carry();
 }
 
-// ---- exact two-level build-side partition (narrow partitions under skew) ----
-// k_rp_hist2 counts per workgroup and FINE partition (Pf <= kMaxFine buckets ranges of Wf buckets;
-// coarse partition p1 = fine partitions [p1 C, p1 C + C)), claims the workgroup's run in every coarse
-// partition on its cursor (as k_rp_hist does) and adds its fine counts to the fine totals. Level 1 is
-// k_rp_wscatter over the coarse partitions; level 2 (k_rp_split2) regroups every coarse partition
-// into its C fine ones, each chunk claiming its runs on the fine cursors: every fine partition ends
-// up contiguous at its exact start (coarse start + the totals of the fine partitions before it).
-constexpr uint32_t kMaxFine = 8192;
-__global__ __launch_bounds__(kPBlock) void k_rp_hist2(RelView r, FastMod fm, uint32_t lo, uint32_t nbl, FastDiv fwf,
-                                                      uint32_t Pf, uint32_t C, uint32_t P1, uint32_t ntiles,
-                                                      uint32_t* __restrict__ hist1, uint32_t* __restrict__ cur1,
-                                                      uint32_t* __restrict__ ftot) {
-  __shared__ uint32_t cnt[kMaxFine];
-  for (uint32_t p = threadIdx.x; p < Pf; p += kPBlock) cnt[p] = 0;
-  __syncthreads();
-  uint32_t key[kPRounds];
-#pragma unroll
-  for (int j = 0; j < kPRounds; ++j) {
-    const uint64_t i = uint64_t(blockIdx.x) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-    key[j] = i < r.n ? r.key(i) : 0u;
-  }
-  for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
-    uint32_t bl[kPRounds];
-#pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = uint64_t(tile) * kPTile + uint64_t(j) * kPBlock + threadIdx.x;
-      bl[j] = i < r.n ? fm.mod(murmur32(key[j])) - lo : nbl;
-    }
-    const uint64_t nbase = uint64_t(tile + gridDim.x) * kPTile;
-#pragma unroll
-    for (int j = 0; j < kPRounds; ++j) {
-      const uint64_t i = nbase + uint64_t(j) * kPBlock + threadIdx.x;
-      key[j] = i < r.n ? r.key(i) : 0u;
-    }
-#pragma unroll
-    for (int j = 0; j < kPRounds; ++j)
-      if (bl[j] < nbl) atomicAdd(&cnt[fwf.div(bl[j])], 1u);
-  }
-  __syncthreads();
-  for (uint32_t f = threadIdx.x; f < Pf; f += kPBlock)
-    if (cnt[f]) atomicAdd(&ftot[f], cnt[f]);
-  for (uint32_t p1 = threadIdx.x; p1 < P1; p1 += kPBlock) {
-    uint32_t c = 0;
-    for (uint32_t k = 0; k < C; ++k) c += p1 * C + k < Pf ? cnt[p1 * C + k] : 0u;
-    hist1[uint64_t(blockIdx.x) * P1 + p1] = c ? atomicAdd(&cur1[p1], c) : 0u;
-  }
-}
-
-// Level 2: chunk c (kS2Chunk pairs) of coarse partition p1 -> its fine partitions. Wave-level
-// multi-split by the fine index (one ballot per bit of it, one LDS atomic per fine partition and
-// wave), one cursor claim per fine partition and chunk, the chunk staged fine-major in LDS and written
-// with consecutive lanes on consecutive pairs. The chunks of a coarse partition follow from its size
-// (each workgroup scans the coarse sizes in LDS: no extra launch). fps[f] = start of fine partition f.
-constexpr int kS2Block = 256, kS2Rounds = 8;
-constexpr uint32_t kS2Chunk = kS2Block * kS2Rounds;  // 2048 pairs
-constexpr uint32_t kS2MaxC = 16;
-__global__ __launch_bounds__(kS2Block) void k_rp_split2(const uint2* __restrict__ in, const uint32_t* __restrict__ ps1,
-                                                        uint32_t P1, uint32_t C, uint32_t cbits, uint32_t Pf, FastMod fm,
-                                                        uint32_t lo, FastDiv fwf, const uint32_t* __restrict__ ftot,
-                                                        uint32_t* __restrict__ fcur, uint32_t* __restrict__ fps,
-                                                        uint2* __restrict__ out) {
-  __shared__ uint32_t cps[kPBlock + 1];  // first chunk of every coarse partition (P1 <= 1024)
-  __shared__ uint32_t wsum[kS2Block / kWave];
-  __shared__ uint2 stage[kS2Chunk];
-  __shared__ uint8_t cof[kS2Chunk];
-  __shared__ uint32_t tcnt[kS2MaxC], tstart[kS2MaxC], dbase[kS2MaxC];
-  const uint32_t me = threadIdx.x;
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-  // chunks per coarse partition, exclusive scan (4 per thread)
-  {
-    constexpr int kPer = (kPBlock + kS2Block - 1) / kS2Block;
-    uint32_t c[kPer], loc = 0;
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t p1 = me * kPer + k;
-      c[k] = p1 < P1 ? (ps1[p1 + 1] - ps1[p1] + kS2Chunk - 1) / kS2Chunk : 0u;
-      loc += c[k];
-      // an empty coarse partition: its fine partitions start (and end) at its start
-      if (blockIdx.x == 0 && p1 < P1 && c[k] == 0)
-        for (uint32_t i = 0; i < C && p1 * C + i < Pf; ++i) fps[p1 * C + i] = ps1[p1];
-    }
-    uint32_t wt;
-    const uint32_t pre = wave_excl_scan(loc, &wt);
-    if (lane == 0) wsum[wid] = wt;
-    __syncthreads();
-    uint32_t run = pre;
-    for (int w = 0; w < wid; ++w) run += wsum[w];
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const uint32_t p1 = me * kPer + k;
-      if (p1 <= P1) cps[p1] = run;
-      run += c[k];
-    }
-    if (me == kS2Block - 1) cps[P1] = run;  // the total (P1 = 1024 is past every thread's entries)
-    if (blockIdx.x == 0 && me == 0) fps[Pf] = ps1[P1];
-  }
-  if (me < kS2MaxC) tcnt[me] = 0;
-  __syncthreads();
-  const uint32_t nchunks = cps[P1];
-  for (uint32_t c = blockIdx.x; c < nchunks; c += gridDim.x) {
-    uint32_t lo1 = 0, hi1 = P1;  // largest p1 with cps[p1] <= c
-    while (hi1 - lo1 > 1) {
-      const uint32_t md = (lo1 + hi1) >> 1;
-      if (cps[md] <= c) lo1 = md; else hi1 = md;
-    }
-    const uint32_t p1 = lo1, k = c - cps[p1];
-    const uint32_t base = ps1[p1] + k * kS2Chunk, len = min(kS2Chunk, ps1[p1 + 1] - base);
-    uint2 v[kS2Rounds];
-#pragma unroll
-    for (int j = 0; j < kS2Rounds; ++j) v[j] = in[base + min(uint32_t(j) * kS2Block + me, len - 1)];
-    uint32_t fi[kS2Rounds], rk[kS2Rounds];
-#pragma unroll
-    for (int j = 0; j < kS2Rounds; ++j) {
-      const bool valid = uint32_t(j) * kS2Block + me < len;
-      const uint32_t f = valid ? fwf.div(fm.mod(v[j].x) - lo) - p1 * C : 0u;
-      fi[j] = f;
-      uint64_t m = __ballot(valid);
-      for (uint32_t b = 0; b < cbits; ++b) {
-        const uint64_t mb = __ballot(valid && ((f >> b) & 1u));
-        m &= ((f >> b) & 1u) ? mb : ~mb;
-      }
-      const bool leader = (m & lt) == 0;
-      uint32_t wb = 0;
-      if (valid && leader) wb = atomicAdd(&tcnt[f], uint32_t(__popcll(m)));
-      wb = __shfl(wb, valid ? __ffsll((unsigned long long)m) - 1 : lane, kWave);
-      rk[j] = valid ? wb + uint32_t(__popcll(m & lt)) : kInvalid;
-    }
-    __syncthreads();
-    if (me < 64) {  // runs of the chunk: stage starts, cursor claims, fine starts
-      const uint32_t i = uint32_t(lane);
-      const uint32_t n = i < C ? tcnt[i] : 0u;
-      uint32_t tot;
-      const uint32_t pre = wave_excl_scan(n, &tot);
-      uint32_t fs = 0;  // start of fine partition p1 C + i: the coarse start + the totals before it
-      const uint32_t ft = i < C && p1 * C + i < Pf ? ftot[p1 * C + i] : 0u;
-      const uint32_t fpre = wave_excl_scan(ft, &tot);
-      fs = ps1[p1] + fpre;
-      if (i < C) {
-        tstart[i] = pre;
-        dbase[i] = fs + (n ? atomicAdd(&fcur[p1 * C + i], n) : 0u) - pre;
-        tcnt[i] = 0;
-        if (k == 0 && p1 * C + i < Pf) fps[p1 * C + i] = fs;
-      }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < kS2Rounds; ++j) {
-      if (rk[j] == kInvalid) continue;
-      const uint32_t q = tstart[fi[j]] + rk[j];
-      stage[q] = v[j];
-      cof[q] = uint8_t(fi[j]);
-    }
-    __syncthreads();
-    for (uint32_t q = me; q < len; q += kS2Block) put(out + dbase[cof[q]] + q, stage[q]);
-    __syncthreads();
-  }
-}
-
 // Block-wide exclusive scan of a[0..n) in LDS (in place); returns the total. BLOCK threads.
 template <int BLOCK>
 __device__ uint32_t lds_excl_scan(uint32_t* a, uint32_t n, uint32_t* wsum) {
@@ -1732,58 +1573,6 @@ hipError_t radix_partition_pairs(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_
   if (pl.P * (r1 ? 2u : 1u) > kMaxParts) return hipErrorNotSupported;
   *nparts = pl.P;
   return partition_pairs(ctx, t, r, pl, out, ps, s, -1, -1, r1);
-}
-
-hipError_t radix_partition_pairs_2l(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint32_t Wf, uint2* out,
-                                    uint32_t* fps, uint32_t* nparts, hipStream_t s) {
-  hipError_t e;
-  const uint32_t nbl = t->nb_local;
-  if (r.n == 0 || r.n >= (1ull << 31) || Wf < 1) return hipErrorNotSupported;
-  const uint32_t Pf = uint32_t((uint64_t(nbl) + Wf - 1) / Wf);
-  const uint32_t C = (Pf + kPBlock - 1) / kPBlock;  // fine partitions per coarse one
-  if (Pf > kMaxFine || C > kS2MaxC || C < 2) return hipErrorNotSupported;
-  const uint32_t W1 = Wf * C, P1 = uint32_t((uint64_t(nbl) + W1 - 1) / W1);
-  uint32_t cbits = 0;
-  while ((1u << cbits) < C) ++cbits;
-  const uint32_t ntiles = uint32_t((r.n + kPTile - 1) / kPTile);
-  const uint32_t g = ntiles < uint32_t(ctx->num_cus) ? ntiles : uint32_t(ctx->num_cus);
-  // scratch: hist1 (g x P1) | ftot (Pf) | fcur (Pf) in kScrPHist; the coarse pairs in kScrSortV
-  if ((e = ctx->scratch[kScrPHist].ensure((uint64_t(P1) * g + 2ull * Pf) * sizeof(uint32_t))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrSortV].ensure(r.n * sizeof(uint2))) != hipSuccess) return e;
-  if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(P1) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
-  uint32_t* hist1 = ctx->scratch[kScrPHist].as<uint32_t>();
-  uint32_t* ftot = hist1 + uint64_t(P1) * g;
-  uint32_t* fcur = ftot + Pf;
-  uint2* coarse = ctx->scratch[kScrSortV].as<uint2>();
-  uint32_t* ps1 = ctx->scratch[kScrPStart].as<uint32_t>();
-  if (!ctx->part_cur.p) {
-    if ((e = ctx->part_cur.ensure(2 * (kMaxParts + 1) * sizeof(uint32_t))) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(ctx->part_cur.p, 0, ctx->part_cur.bytes, s)) != hipSuccess) return e;
-  }
-  uint32_t* cur = ctx->part_cur.as<uint32_t>() + (ctx->part_parity & 1u) * (kMaxParts + 1);
-  uint32_t* cur_next = ctx->part_cur.as<uint32_t>() + ((ctx->part_parity + 1) & 1u) * (kMaxParts + 1);
-  ctx->part_parity ^= 1u;
-  if ((e = hipMemsetAsync(ftot, 0, 2ull * Pf * sizeof(uint32_t), s)) != hipSuccess) return e;
-  const RelView v = view_of(r);
-  const uint32_t lo = uint32_t(t->desc.bucket_lo);
-  const FastDiv fwf = make_div(Wf), fw1 = make_div(W1);
-  hipLaunchKernelGGL(k_rp_hist2, dim3(g), dim3(kPBlock), 0, s, v, t->fm, lo, nbl, fwf, Pf, C, P1, ntiles, hist1, cur,
-                     ftot);
-  RelTiles rt;
-  rt.r0 = rt.r1 = v;
-  rt.nt0 = ntiles;
-  rt.P = P1;
-  if (r.row_off != HJ3D_ROW_IMPLICIT)
-    hipLaunchKernelGGL((k_rp_wscatter<1, true>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
-                       cur, cur_next, ps1, coarse);
-  else
-    hipLaunchKernelGGL((k_rp_wscatter<1, false>), dim3(g), dim3(kPBlock), 0, s, rt, t->fm, lo, nbl, fw1, P1, ntiles, hist1,
-                       cur, cur_next, ps1, coarse);
-  hipLaunchKernelGGL(k_rp_split2, dim3(ctx->num_cus * 4), dim3(kS2Block), 0, s, static_cast<const uint2*>(coarse),
-                     static_cast<const uint32_t*>(ps1), P1, C, cbits, Pf, t->fm, lo, fwf,
-                     static_cast<const uint32_t*>(ftot), fcur, fps, out);
-  *nparts = Pf;
-  return hipGetLastError();
 }
 
 hipError_t radix_build(hj3d_ctx* ctx, hj3d_table* t, const hj3d_rel& r, hipStream_t s, bool* rows_sorted) {

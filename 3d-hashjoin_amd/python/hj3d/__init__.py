@@ -27,7 +27,7 @@ PROBE_UNIQUE, PROBE_UNNEST, PROBE_EMIT, PROBE_CHECKSUM, PROBE_ACCUMULATE = 0x1, 
 T_BUILD, T_PROBE, T_PROBE_KERNEL, T_PARTITION, T_SCATTER, T_HIST = range(6)
 OPT_FORCE_DIRECT, OPT_RADIX_MIN, OPT_NESTED_SORT, OPT_SEL_UNFUSED, OPT_PACKED_PROBE = 1, 2, 4, 5, 6
 OPT_PROBE_ITEMS = 7
-OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_SYNC_BUILD, OPT_NESTED_2L = 8, 9, 10, 11, 13, 14
+OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_SYNC_BUILD = 8, 9, 10, 11, 13
 OPT_RP_UNFUSED = 15
 OPT_DIAG_GBAR = 16
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
@@ -431,11 +431,6 @@ class Context:
     def pk_build(self, on: bool = True):
         """Test hook: chaining builds take the two-level slice build (pk_build) whenever it applies."""
         self.set_option(OPT_PK_BUILD, int(on))
-
-    def nested_2l(self, on: bool = True):
-        """Nested builds too coarse for the register aggregation take the exact two-level partition
-        (HJ3D_OPT_NESTED_2L; off by default, tests and A/B)."""
-        self.set_option(OPT_NESTED_2L, int(on))
 
     def rp_unfused(self, on: bool = True):
         """Small build partitions as two launches (histogram, scatter) instead of the fused

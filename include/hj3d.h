@@ -192,11 +192,7 @@ enum {
    * gave up), so the build relation's device memory may be released as soon as the call returns.
    * Default: the table finishes at its next use (see hj3d_build). */
   HJ3D_OPT_SYNC_BUILD = 13,
-  /* HJ3D_OPT_NESTED_2L (0/1, default 0): a nested build whose one-level partitions are too large for
-   * the register aggregation takes the exact two-level partition into narrow partitions (up to 8192,
-   * skew-safe) and aggregates them in registers. Measured slower at config C (2.93 against 2.25 ms),
-   * so off by default; kept for A/B measurements and its parity test. */
-  HJ3D_OPT_NESTED_2L = 14,
+  /* 14: retired (the two-level nested partition, measured slower than the one-level one) */
   /* HJ3D_OPT_RP_UNFUSED (0/1, default 0): small implicit-row build partitions run as two launches
    * (histogram, then scatter) instead of the fused one-launch partition with its grid barrier
    * (A/B measurements and the parity test of both forms). The fused form runs only when the
@@ -290,9 +286,8 @@ hj3d_status hj3d_table_export(hj3d_ctx* ctx, const hj3d_table* t, uint32_t* off,
                               uint64_t* n_payload, uint64_t* n_sub);
 /* Which build made the table's current content (diagnostic, static string): chaining "radix",
  * "slices" (pk_slices, tables beyond the radix build's range) or "direct"; nested "nested_agg",
- * "nested_agg_slices" (more than 2048 partitions), "nested_agg_2l" (the exact two-level partition
- * into narrow partitions), each with "_reg" appended when the register form aggregated them,
- * "nested_sort" or "nested_radix"; "none" before a
+ * "nested_agg_slices" (more than 2048 partitions), each with "_reg" appended when the register form
+ * aggregated them, or "nested_sort"; "none" before a
  * build. A nested table whose build has not been resolved yet (no use since hj3d_build) reports the
  * path that was started, with "?" appended ("nested_agg?"): the getter never waits or builds. Replaces
  * nothing of the reference (which has one insert path). */

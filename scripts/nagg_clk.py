@@ -95,6 +95,21 @@ def main():
     out["longest"] = [{"start": round(float(starts[i]), 1), "total": round(float(tot[i]), 1),
                        "pass_A": round(float(us(x[i, 2] - x[i, 1])), 1), "pass_B": round(float(us(x[i, 4] - x[i, 3])), 1)}
                       for i in top]
+    # workgroups running at once on one CU (point 6: XCC_ID << 32 | HW_ID; CU_ID bits 8-11, SH 12,
+    # SE 13-15): the largest overlap of [start, exit] intervals per CU, and the CUs seen
+    hw = x[:, 6].astype(np.uint64)
+    cu = ((hw >> np.uint64(32)) & np.uint64(0xF)) * np.uint64(1 << 8) + ((hw >> np.uint64(8)) & np.uint64(0xFF))
+    occ = {}
+    for c in np.unique(cu):
+        idx = np.where(cu == c)[0]
+        ev = sorted([(x[i, 0], 1) for i in idx] + [(x[i, 5], -1) for i in idx], key=lambda t: (t[0], t[1]))
+        cur = best = 0
+        for _, d in ev:
+            cur += d
+            best = max(best, cur)
+        occ[best] = occ.get(best, 0) + 1
+    out["cus_seen"] = int(len(np.unique(cu)))
+    out["max_concurrent_per_cu_hist"] = {str(k): v for k, v in sorted(occ.items())}
     print(json.dumps(out))
 
 

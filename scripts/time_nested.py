@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--domain", type=float, default=1e7)
     ap.add_argument("--theta", type=float, default=0.8)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--mode", default="agg", choices=["agg", "slices", "sort", "2l"])
+    ap.add_argument("--mode", default="agg", choices=["agg", "slices", "sort"])
     ap.add_argument("--label", default=os.path.basename(os.path.dirname(os.environ.get("HJ3D_LIB", "default/x"))))
     a = ap.parse_args()
     import torch
@@ -36,7 +36,6 @@ def main():
     nb = ctx.num_distinct(rel, dom)
     ctx.nested_sort(a.mode == "sort")
     ctx.nested_pk(a.mode == "slices")
-    ctx.nested_2l(a.mode == "2l")
     t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
     t.reserve(n)
     for _ in range(2):

@@ -703,33 +703,3 @@ def test_nested_probe_two_level_slices(ctx, plan):
     finally:
         ctx.radix_min(1 << 20)
         ctx.pk_slice_max(0)
-
-
-@pytest.mark.parametrize("zipf", [False, True], ids=["uniform", "zipf"])
-def test_nested_build_two_level_partition(ctx, zipf):
-    """Nested builds whose one-level partitions are too large for the register form take the exact
-    two-level partition (radix_partition_pairs_2l: fine histogram, whole-segment scatter into coarse
-    partitions, split into up to 8192 narrow ones) and the register aggregation, with Zipf hot keys'
-    partitions streamed inside it. 12M build tuples over 300K buckets: 1024 narrow partitions of
-    ~12K pairs. Counters, output checksums and statistics equal the oracle's."""
-    import hj3d
-    rng = np.random.default_rng(53 + zipf)
-    nb, nS, dom = 300_000, 12_000_000, 300_000  # ~1 key per bucket (NB = #dv, as the plans size it)
-    Sa = (np.minimum(rng.zipf(1.4, nS) - 1, dom - 1) if zipf else rng.integers(0, dom, nS)).astype(np.uint32)
-    Rk = rng.permutation(dom).astype(np.uint32)[:400_000]
-    R = O.tuples3(Rk, np.zeros_like(Rk))
-    S = O.tuples3(np.arange(nS, dtype=np.uint32), Sa)
-    e = O.nested_plan(S, 1, R, 0, nb, True)
-    ctx.nested_2l(True)
-    try:
-        t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
-        got = hj3d.exp1_plan(ctx, "Nrs", dev(R), dev(S), nb, table=t)
-        path = t.build_path()
-        st = t.stats()
-        t.close()
-    finally:
-        ctx.nested_2l(False)
-    assert path == "nested_agg_2l_reg", path
-    assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == (e.c_probe, e.c_cmp, e.c_unnest, e.c_top)
-    assert got["out"] == e.out
-    assert {k: st[k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}
