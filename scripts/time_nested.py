@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--theta", type=float, default=0.8)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--mode", default="agg", choices=["agg", "slices", "sort"])
+    ap.add_argument("--opt", action="append", default=[],
+                    help="raw engine option K=V (hj3d_ctx_set_option), e.g. for a library of an older revision")
     ap.add_argument("--label", default=os.path.basename(os.path.dirname(os.environ.get("HJ3D_LIB", "default/x"))))
     a = ap.parse_args()
     import torch
@@ -36,6 +38,9 @@ def main():
     nb = ctx.num_distinct(rel, dom)
     ctx.nested_sort(a.mode == "sort")
     ctx.nested_pk(a.mode == "slices")
+    for kv in a.opt:
+        k, v = kv.split("=")
+        ctx.set_option(int(k), int(v))
     t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
     t.reserve(n)
     for _ in range(2):
