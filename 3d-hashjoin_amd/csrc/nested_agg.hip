@@ -1198,6 +1198,66 @@ __global__ __launch_bounds__(kBlock) void k_nagg_mains(const uint4* __restrict__
   for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[m0 + i] = mtmp[ps[gp] + i];
 }
 
+// The three launches above in one, for at most 2048 partitions (the one-level paths): workgroup gp
+// takes its main-record base from the key counts of its table's partitions before it (a block sum
+// over <= 2048 words read from L2, instead of a scan launch), adds it to its buckets' directory words,
+// moves its main records to their final slots, and the first workgroup of each table writes the
+// table's counts (and their host copy). Nothing for a table whose build gave up.
+__global__ __launch_bounds__(kBlock) void k_nagg_fin(const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
+                                                     const uint32_t* __restrict__ dcount, NaggTabs tabs, uint32_t nbl,
+                                                     uint32_t W) {
+  __shared__ uint64_t red[2][kBlock / kWave];
+  const uint32_t gp = blockIdx.x, ti = tabs.nt > 1 && gp >= tabs.P ? 1u : 0u, p = gp - ti * tabs.P;
+  const uint32_t t0 = ti * tabs.P;
+  uint64_t* counts = tabs.counts[ti];
+  const bool failed = reinterpret_cast<const uint32_t*>(counts + 3)[0] != 0;
+  // keys of the table's partitions before gp, and of all of them
+  uint64_t before = 0, all = 0;
+  for (uint32_t k = t0 + threadIdx.x; k < t0 + tabs.P; k += kBlock) {
+    const uint32_t c = dcount[k];
+    before += k < gp ? c : 0u;
+    all += c;
+  }
+  before = wave_sum(before);
+  all = wave_sum(all);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wid] = before;
+    red[1][wid] = all;
+  }
+  __syncthreads();
+  uint32_t base = 0;
+  uint64_t tot = 0;
+#pragma unroll
+  for (int w = 0; w < kBlock / kWave; ++w) {
+    base += uint32_t(red[0][w]);
+    tot += red[1][w];
+  }
+  if (p == 0 && threadIdx.x == 0) {
+    uint64_t c0 = 0, c1 = 0;
+    if (!failed) {
+      c0 = ps[t0 + tabs.P] - ps[t0];
+      c1 = tot;
+      counts[0] = c0;
+      counts[1] = c1;
+      tabs.off[ti][nbl] = uint32_t(c1);
+    }
+    if (uint64_t* h = tabs.hc[ti]) {  // the host's copy (words 2 and 3 were final when k_nagg ended)
+      h[0] = c0;
+      h[1] = c1;
+      h[2] = counts[2];
+      h[3] = counts[3];
+    }
+  }
+  if (failed) return;
+  uint32_t* __restrict__ off = tabs.off[ti];
+  const uint32_t b0 = p * W, nbs = min(W, nbl - b0);
+  for (uint32_t k = threadIdx.x; k < nbs; k += kBlock) off[b0 + k] += base;
+  uint4* __restrict__ mains = tabs.main[ti];
+  const uint32_t n = dcount[gp], e0 = ps[gp];
+  for (uint32_t i = threadIdx.x; i < n; i += kBlock) mains[base + i] = mtmp[e0 + i];
+}
+
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
 __global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts, uint32_t* __restrict__ defer) {
@@ -1316,13 +1376,16 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     if (np != P) return hipErrorNotSupported;
     pairs = pw;
     ps = pst;
-    {  // the other pairs of heavy partitions, compacted (at most every pair)
+    // the hot-key split where the mean partition holds at least a chunk (heavier partitions then last
+    // long enough to matter; config E's ~8 K pairs: no launch)
+    const bool hs = double(n) / PT >= double(kHotChunk);
+    if (hs) {  // the other pairs of heavy partitions, compacted (at most every pair)
       if ((e = ctx->scratch[kScrSortV].ensure(n * sizeof(uint2))) != hipSuccess) return e;
       tabs.hot = hotw;
       tabs.hpairs = ctx->scratch[kScrSortV].as<uint2>();
     }
-    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, hinfo);
-    hipLaunchKernelGGL(k_nagg_hot, dim3(2 * G), dim3(kHotBlock), 0, s, pairs, ps, order, hinfo, tabs);
+    hipLaunchKernelGGL(k_nagg_order, dim3(1), dim3(1024), 0, s, ps, PT, order, tabs, hs ? hinfo : nullptr);
+    if (hs) hipLaunchKernelGGL(k_nagg_hot, dim3(2 * G), dim3(kHotBlock), 0, s, pairs, ps, order, hinfo, tabs);
   }
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
@@ -1421,10 +1484,14 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // no host wait here: if a partition gave up (fail, counts word 3), the kernels below do nothing
   // for its table and the caller, which reads the counts at the table's next use, runs the sort
   // build instead
-  if ((e = exclusive_scan_u32(ctx, dcount, dcount, PT, s)) != hipSuccess) return e;
-  hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock), nt), dim3(kBlock), 0, s, tabs, nbl,
-                     FastDiv32::make(W), dcount);
-  hipLaunchKernelGGL(k_nagg_mains, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs, nbl);
+  if (!pk) {  // (at most 2048 partitions)
+    hipLaunchKernelGGL(k_nagg_fin, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs, nbl, W);
+  } else {
+    if ((e = exclusive_scan_u32(ctx, dcount, dcount, PT, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock), nt), dim3(kBlock), 0, s, tabs, nbl,
+                       FastDiv32::make(W), dcount);
+    hipLaunchKernelGGL(k_nagg_mains, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs, nbl);
+  }
   for (uint32_t k = 0; k < nt; ++k) tt[k]->n_build = rr[k].n;
   return hipGetLastError();
 }

@@ -564,9 +564,10 @@ def test_build_many_hot_key_split(ctx, explicit, nb, path):
     each: k_nagg_hot splits the key off before the aggregation (its rows written down from the end of
     the partition's sub range, the other pairs compacted), in both tables (table 1's sub rows are
     numbered from its own first pair) and with explicit row ids; with ~25 K pairs per partition the
-    streaming aggregation runs, with ~13 K the register form, which leaves the split partitions to
-    the streaming form (k_nagg_defer). Counters, output checksums and statistics equal the oracle's
-    per table (HtNested1::insert, ht_nested.hh:287-311)."""
+    streaming aggregation runs after the split, with ~13 K (less than a chunk of the split on average:
+    no split) the register form, which leaves its partitions too large for its registers to the
+    streaming form (k_nagg_defer). Counters, output checksums and statistics equal the oracle's per
+    table (HtNested1::insert, ht_nested.hh:287-311)."""
     import hj3d
     rng = np.random.default_rng(77 + explicit)
     n, dom = 5_000_000, 600_000
