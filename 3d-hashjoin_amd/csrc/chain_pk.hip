@@ -39,6 +39,11 @@ constexpr int kPkTBits = 32 - __builtin_clz(uint32_t(kPkTile - 1));  // bits of 
 constexpr uint32_t kPkSeg = 16;                                     // pairs per region segment (128 B)
 constexpr uint32_t kPkStage = 17408;  // LDS stage (pairs): the tile + the carried pairs (< kPkSeg per slice)
 static_assert(kPkTile <= kPkStage && kPkStage < 65536, "the tile alone fits the stage; stage offsets in 16 bits");
+// the stage of the two-slices-per-thread form (64-B segments: carries of < 8 pairs, ~3.5 on average per
+// slice, so the tile and ~7 K carried pairs; with its 16 KB of slice words and 15.5 KB of segment
+// words it fills the LDS)
+constexpr uint32_t kPkStage2 = 15872;
+constexpr uint32_t kPkMaxP1 = 2 * kPkBlock;  // slices one partition level takes (two per thread)
 constexpr uint32_t kSortedMaxPk = 32;
 constexpr uint32_t kOvfFlag = 0x80000000u;
 
@@ -60,32 +65,50 @@ __device__ __forceinline__ void pk_ovf_append(bool me, uint2 e, uint2* __restric
 }
 
 // ---- k_pk_part: the probe relation -> packed pairs in per-(workgroup, slice) regions ----
-// Regions: region[(g * P + p) * cap + k], counts[g * P + p] pairs. One slice per thread (P <= 1024):
-// thread p carries slice p's < 16 leftover pairs in registers. SEL: a one-word selection fused in.
+// Regions: region[(g * P + p) * cap + k], counts[g * P + p] pairs. PPT slices per thread (P <= 1024
+// PPT): thread t carries slices t + k * 1024's leftover pairs (< one segment each) in registers. PPT = 1:
+// 128-B segments; PPT = 2 (1024 < P <= 2048, one partition level instead of two: config D's
+// 2.5e7-bucket rank at 4 GPUs): 64-B segments, a smaller carry and stage. SEL: a one-word selection
+// fused in.
 // Memory ordering: vmcnt counts loads and stores together, in issue order, so a load can only be
 // waited for together with every older store. The next tile's keys are loaded right after this tile's
 // stage is built (loading two tiles ahead, so that the wait would never cover this tile's region
 // stores, spilled registers and measured slower).
-template <bool IMPLICIT, bool SEL>
+template <int PPT>
+struct PkPartGeom {
+  static constexpr uint32_t kSeg = kPkSeg / PPT;                          // pairs per region segment
+  static constexpr uint32_t kStage = PPT == 1 ? kPkStage : kPkStage2;      // LDS stage (pairs)
+};
+template <bool IMPLICIT, bool SEL, int PPT>
 __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint32_t ntiles, uint32_t cap,
                                                       uint2* __restrict__ region, uint32_t* __restrict__ counts,
                                                       uint2* __restrict__ ovf, uint64_t* __restrict__ ctl,
                                                       SelRange sel, uint32_t stage_lim) {
-  __shared__ uint2 stage[kPkStage];
-  __shared__ uint32_t loc[kPkBlock];
-  __shared__ uint32_t sbase[kPkBlock];
-  __shared__ uint2 seginfo[kPkStage / kPkSeg];  // whole segment: {region index | kOvfFlag + slice, stage start}
+  constexpr uint32_t SEG = PkPartGeom<PPT>::kSeg, STAGE = PkPartGeom<PPT>::kStage;
+  __shared__ uint2 stage[STAGE];
+  __shared__ uint32_t loc[kPkBlock * PPT];
+  __shared__ uint32_t sbase[kPkBlock * PPT];
+  __shared__ uint2 seginfo[STAGE / SEG];  // whole segment: {region index | kOvfFlag + slice, stage start}
   __shared__ uint32_t wsum[kPkBlock / kWave];
   const uint32_t me = threadIdx.x, P = pk.P, n = uint32_t(r.n);
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const uint32_t my_reg = (blockIdx.x * P + me) * cap;  // region of slice `me` (host: G * P * cap < 2^31)
-  uint2 creg[kPkSeg - 1];
-  // my_cur: pairs taken by slice `me`'s region so far; my_end: where its region stopped taking
-  // pairs (cap, or the start of the first segment that did not fit: after a mid-stream carry flush
-  // the cursor is no longer segment-aligned, so a segment may straddle the region's end)
-  uint32_t my_kc = 0, my_cur = 0, my_end = cap;
+  // this thread's slices sl(k) = me + k * 1024 and their regions (host: G * P * cap < 2^31)
+  const auto sl = [&](int k) __attribute__((always_inline)) { return me + uint32_t(k) * kPkBlock; };
+  uint32_t my_reg[PPT];
+  uint2 creg[PPT][SEG - 1];
+  // my_cur: pairs taken by the slice's region so far; my_end: where its region stopped taking pairs
+  // (cap, or the start of the first segment that did not fit: after a mid-stream carry flush the
+  // cursor is no longer segment-aligned, so a segment may straddle the region's end)
+  uint32_t my_kc[PPT], my_cur[PPT], my_end[PPT];
 #pragma unroll
-  for (int j = 0; j < int(kPkSeg) - 1; ++j) creg[j] = make_uint2(0, 0);
+  for (int k = 0; k < PPT; ++k) {
+    my_reg[k] = (blockIdx.x * P + sl(k)) * cap;
+    my_kc[k] = 0;
+    my_cur[k] = 0;
+    my_end[k] = cap;
+#pragma unroll
+    for (int j = 0; j < int(SEG) - 1; ++j) creg[k][j] = make_uint2(0, 0);
+  }
   uint32_t ha[kPkRounds], pa[SEL ? kPkRounds : 1];
   // explicit rows: loaded with the key at tile prefetch and kept in registers (the row word shares
   // the key's line; loading it again after the ranking phase fetched that line twice: 15.4 B per
@@ -110,18 +133,21 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   auto to_ovf = [&](uint2 e, uint32_t p, bool me_) __attribute__((always_inline)) {  // packed pair of slice p -> {h, row}
     pk_ovf_append(me_, make_uint2(pk.hash_of(e.x, p), e.y), ovf, ctl);
   };
-  auto flush_carry = [&]() __attribute__((always_inline)) {  // partial segment at the cursor
+  auto flush_carry = [&]() __attribute__((always_inline)) {  // partial segments at the cursors
 #pragma unroll
-    for (int j = 0; j < int(kPkSeg) - 1; ++j) {
-      const bool v = me < P && uint32_t(j) < my_kc;
-      const uint32_t o = my_cur + j;
-      if (v && o < my_end) region[my_reg + o] = creg[j];
-      to_ovf(creg[j], me, v && o >= my_end);
+    for (int k = 0; k < PPT; ++k) {
+#pragma unroll
+      for (int j = 0; j < int(SEG) - 1; ++j) {
+        const bool v = sl(k) < P && uint32_t(j) < my_kc[k];
+        const uint32_t o = my_cur[k] + j;
+        if (v && o < my_end[k]) region[my_reg[k] + o] = creg[k][j];
+        to_ovf(creg[k][j], sl(k), v && o >= my_end[k]);
+      }
+      my_cur[k] += my_kc[k];
+      my_kc[k] = 0;
     }
-    my_cur += my_kc;
-    my_kc = 0;
   };
-  // exclusive scan of one value per thread (one slice per thread)
+  // exclusive scan of one value per thread
   auto scan = [&](uint32_t v, uint32_t* total) __attribute__((always_inline)) {
     uint32_t x = v;
 #pragma unroll
@@ -145,9 +171,9 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
   uint32_t npassed = 0;
   auto process = [&](uint32_t tile, uint32_t (&h)[kPkRounds], uint32_t (&pw)[SEL ? kPkRounds : 1],
                      uint32_t (&rw)[IMPLICIT ? 1 : kPkRounds]) __attribute__((always_inline)) {
-    // loc[me] is cleared right after its count is read (nothing touches it again in the tile) and no
-    // barrier ends the tile: the next tile's first LDS writes (stage, seginfo, sbase) come after its
-    // ranking barrier, which every thread reaches only when done reading
+    // a slice counter is cleared right after its count is read (nothing touches it again in the tile)
+    // and no barrier ends the tile: the next tile's first LDS writes (stage, seginfo, sbase) come after
+    // its ranking barrier, which every thread reaches only when done reading
     const uint32_t base = tile * kPkTile;
     uint32_t rk[kPkRounds];
     // hash, bucket, slice, rank: the LDS atomics are unconditional (invalid tuples add 0 to slot 0)
@@ -171,32 +197,50 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       }
     }
     __syncthreads();
-    const uint32_t my_c = me < P ? loc[me] : 0u;
-    loc[me] = 0;
-    const auto seg_counts = [&]() __attribute__((always_inline)) {
-      const uint32_t L = my_kc + my_c;
-      return (L << 16) | (L / kPkSeg);
+    uint32_t my_c[PPT];
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      my_c[k] = sl(k) < P ? loc[sl(k)] : 0u;
+      loc[sl(k)] = 0;
+    }
+    // per slice (L << 16) | L / SEG, L = its carry + this tile's pairs; the thread's slices in a row
+    const auto seg_counts = [&](int k) __attribute__((always_inline)) {
+      const uint32_t L = my_kc[k] + my_c[k];
+      return (L << 16) | (L / SEG);
+    };
+    const auto seg_sum = [&]() __attribute__((always_inline)) {
+      uint32_t t = 0;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) t += seg_counts(k);
+      return t;
     };
     uint32_t tot;
-    uint32_t pre = scan(seg_counts(), &tot);
+    uint32_t pre = scan(seg_sum(), &tot);
     if ((tot >> 16) > stage_lim) {  // too many carried pairs: write them out; the tile alone fits
       flush_carry();
-      pre = scan(seg_counts(), &tot);
+      pre = scan(seg_sum(), &tot);
     }
-    const uint32_t my_loc = pre >> 16, my_fseg = pre & 0xFFFFu, nfull = tot & 0xFFFFu;
-    const uint32_t my_len = my_kc + my_c;
-    if (me < P) {
-      sbase[me] = my_loc + my_kc;
+    const uint32_t nfull = tot & 0xFFFFu;
+    uint32_t my_loc[PPT], my_len[PPT];
 #pragma unroll
-      for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_kc) stage[my_loc + j] = creg[j];
-      for (uint32_t sg = 0; sg < my_len / kPkSeg; ++sg) {
-        // segment-aligned (cap is a multiple of kPkSeg) unless a mid-stream flush moved the cursor:
-        // a segment goes to the region only whole, else (all of it) to the overflow list
-        const uint32_t o = my_cur + sg * kPkSeg;
-        const bool fit = o + kPkSeg <= my_end;
-        if (!fit && o < my_end) my_end = o;
-        seginfo[my_fseg + sg] = make_uint2(fit ? my_reg + o : (kOvfFlag | me), my_loc + sg * kPkSeg);
+    for (int k = 0; k < PPT; ++k) {
+      my_loc[k] = pre >> 16;
+      const uint32_t my_fseg = pre & 0xFFFFu;
+      pre += seg_counts(k);
+      my_len[k] = my_kc[k] + my_c[k];
+      if (sl(k) < P) {
+        sbase[sl(k)] = my_loc[k] + my_kc[k];
+#pragma unroll
+        for (int j = 0; j < int(SEG) - 1; ++j)
+          if (uint32_t(j) < my_kc[k]) stage[my_loc[k] + j] = creg[k][j];
+        for (uint32_t sg = 0; sg < my_len[k] / SEG; ++sg) {
+          // segment-aligned (cap is a multiple of SEG) unless a mid-stream flush moved the cursor:
+          // a segment goes to the region only whole, else (all of it) to the overflow list
+          const uint32_t o = my_cur[k] + sg * SEG;
+          const bool fit = o + SEG <= my_end[k];
+          if (!fit && o < my_end[k]) my_end[k] = o;
+          seginfo[my_fseg + sg] = make_uint2(fit ? my_reg[k] + o : (kOvfFlag | sl(k)), my_loc[k] + sg * SEG);
+        }
       }
     }
     __syncthreads();
@@ -212,10 +256,10 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
     }
     load(h, pw, rw, tile + gridDim.x);  // the next tile (keys past the end load nothing)
     __syncthreads();
-    // whole segments: kPkSeg consecutive lanes store one 128-B segment
-    for (uint32_t kk = me; kk < nfull * kPkSeg; kk += kPkBlock) {
-      const uint2 si = seginfo[kk / kPkSeg];
-      const uint32_t j = kk % kPkSeg;
+    // whole segments: SEG consecutive lanes store one segment
+    for (uint32_t kk = me; kk < nfull * SEG; kk += kPkBlock) {
+      const uint2 si = seginfo[kk / SEG];
+      const uint32_t j = kk % SEG;
       const uint2 e = stage[si.y + j];
       const bool spill = si.x & kOvfFlag;
       if (!spill)
@@ -223,21 +267,27 @@ __global__ __launch_bounds__(kPkBlock) void k_pk_part(RelView r, PkGeom pk, uint
       to_ovf(e, si.x & ~kOvfFlag, spill);
     }
     // the run's tail (< one segment) becomes the slice's carry
-    if (me < P) {
-      const uint32_t F = my_len - my_len % kPkSeg;
 #pragma unroll
-      for (int j = 0; j < int(kPkSeg) - 1; ++j)
-        if (uint32_t(j) < my_len - F) creg[j] = stage[my_loc + F + j];
-      my_cur += F;
-      my_kc = my_len - F;
+    for (int k = 0; k < PPT; ++k) {
+      if (sl(k) < P) {
+        const uint32_t F = my_len[k] - my_len[k] % SEG;
+#pragma unroll
+        for (int j = 0; j < int(SEG) - 1; ++j)
+          if (uint32_t(j) < my_len[k] - F) creg[k][j] = stage[my_loc[k] + F + j];
+        my_cur[k] += F;
+        my_kc[k] = my_len[k] - F;
+      }
     }
   };
-  loc[me] = 0;
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) loc[sl(k)] = 0;
   __syncthreads();
   load(ha, pa, wa, blockIdx.x);
   for (uint32_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) process(tile, ha, pa, wa);
   flush_carry();
-  if (me < P) counts[blockIdx.x * P + me] = min(my_cur, my_end);
+#pragma unroll
+  for (int k = 0; k < PPT; ++k)
+    if (sl(k) < P) counts[blockIdx.x * P + sl(k)] = min(my_cur[k], my_end[k]);
   // n_probe: every scanned tuple (the reference's probe count), or the selection's passing tuples
   if constexpr (SEL) {
     uint32_t c = npassed;
@@ -1040,14 +1090,17 @@ PkPlan pk_plan(const hj3d_ctx* ctx, uint32_t nbl, uint64_t n_build) {
   const uint32_t ncu = uint32_t(ctx->num_cus);
   if (P >= ncu / 2) {
     uint32_t Pq = (P + ncu - 1) / ncu * ncu;
-    if (P <= uint32_t(kPkBlock) && Pq > uint32_t(kPkBlock)) Pq = kPkBlock;
+    if (P <= kPkMaxP1 && Pq > kPkMaxP1) Pq = kPkMaxP1;
     P = Pq;
     W = (nbl + P - 1) / P;
     P = (nbl + W - 1) / W;
   }
   pl.W = W;
   pl.P = P;
-  pl.C = (P + kPkBlock - 1) / kPkBlock;  // slices per coarse range of the first level
+  // slices per coarse range of the first level: one level up to kPkMaxP1 slices (k_pk_part's two
+  // slices per thread beyond 1024: config D's 2.5e7-bucket rank at 4 GPUs, 2048 slices, without the
+  // k_pk_split pass); beyond, coarse ranges of 1024 slices' worth
+  pl.C = P <= kPkMaxP1 ? 1u : (P + kPkBlock - 1) / kPkBlock;
   pl.W1 = W * pl.C;
   pl.P1 = (nbl + pl.W1 - 1) / pl.W1;
   return pl;
@@ -1124,13 +1177,22 @@ hipError_t pk_probe(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint3
   {
     KernelSpan tm(ctx, HJ3D_T_SCATTER);
     const uint32_t c32 = uint32_t(cap);
+    // (one level beyond 1024 slices: two slices per partitioning thread)
+    const uint32_t slim2 = slim < kPkStage2 ? slim : kPkStage2;
+#define HJ3D_PKP_LAUNCH(IMP, SEL)                                                                                   \
+  if (pl.P1 > uint32_t(kPkBlock))                                                                                   \
+    tm.launch(k_pk_part<IMP, SEL, 2>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, \
+              slim2);                                                                                               \
+  else                                                                                                              \
+    tm.launch(k_pk_part<IMP, SEL, 1>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
     if (sel) {
-      if (imp) tm.launch(k_pk_part<true, true>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
-      else tm.launch(k_pk_part<false, true>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
+      if (imp) HJ3D_PKP_LAUNCH(true, true)
+      else HJ3D_PKP_LAUNCH(false, true)
     } else {
-      if (imp) tm.launch(k_pk_part<true, false>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
-      else tm.launch(k_pk_part<false, false>, dim3(G), dim3(kPkBlock), s, v, pk1, ntiles, c32, region, counts, ovf, ctl, sr, slim);
+      if (imp) HJ3D_PKP_LAUNCH(true, false)
+      else HJ3D_PKP_LAUNCH(false, false)
     }
+#undef HJ3D_PKP_LAUNCH
   }
   if ((e = hipGetLastError()) != hipSuccess) return e;
   const uint2* pregion = region;
@@ -1246,10 +1308,10 @@ hipError_t pk_slices(hj3d_ctx* ctx, const hj3d_table* t, const hj3d_rel& r, uint
   const RelView v = view_of(r);
   SelRange sr{};
   if (r.row_off == HJ3D_ROW_IMPLICIT)
-    hipLaunchKernelGGL((k_pk_part<true, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
+    hipLaunchKernelGGL((k_pk_part<true, false, 1>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
                        counts, ovf, ctl, sr, kPkStage);
   else
-    hipLaunchKernelGGL((k_pk_part<false, false>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
+    hipLaunchKernelGGL((k_pk_part<false, false, 1>), dim3(G), dim3(kPkBlock), 0, s, v, pk1, ntiles, uint32_t(cap), region,
                        counts, ovf, ctl, sr, kPkStage);
   // (C = 1: the split only regroups each slice's G regions into S2)
   hipLaunchKernelGGL(k_pk_split, dim3(P1 * S2), dim3(kSpBlock), 0, s, static_cast<const uint2*>(region),

@@ -75,30 +75,32 @@ def check_csr(ctx, name, emit=True):
         assert np.array_equal(S[host[:, 0], 1], R[host[:, 1], 0]), name
 
 
-# slice bounds that give C = 2, 8 and 32 slices per coarse range at 2^20 buckets (P rounded up to
-# whole waves of 256 workgroups)
-@pytest.mark.parametrize("w", [1024, 256, 64, 32])
+# slice bounds at 2^20 buckets (P rounded up to whole waves of 256 workgroups): 1024 slices (one level,
+# one slice per partitioning thread), 2048 (one level, two per thread, 64-B segments), and two levels
+# with C = 4, 16 and 32 slices per coarse range
+@pytest.mark.parametrize("w", [1024, 512, 256, 64, 32])
 def test_two_level_uniform_equals_reference(pk, w):
     pk.pk_slice_max(w)
     check_csr(pk, "exp1_R1048576_S8388608_uni")
 
 
-@pytest.mark.parametrize("w", [128, 16])
+@pytest.mark.parametrize("w", [128, 100, 16])
 def test_two_level_zipf_region_overflow_equals_reference(pk, w):
     """Zipf(1) probe keys: a hot slice overflows its regions at both levels (k_pk_part's and
-    k_pk_split's), the overflow list is probed against the table in HBM."""
+    k_pk_split's; w = 100: one level of 1536 slices, two per partitioning thread), the overflow list
+    is probed against the table in HBM."""
     pk.pk_slice_max(w)
     check_csr(pk, "exp1_R131072_S1048576_zipf1")
 
 
-@pytest.mark.parametrize("two_level", [False, True])
+@pytest.mark.parametrize("two_level", [False, "two_per_thread", True])
 def test_carry_flush_with_region_overflow(pk, two_level):
     """after a mid-stream carry flush the partitioner's region cursor is not segment
     aligned, so a whole segment can straddle the region's end; it must go to the overflow list
     whole and the region's count stop at its start. Forced here: flush after every tile
     (HJ3D_OPT_PK_STAGE = 1), ~1024 slices, Zipf(1) keys that overflow the hot slice's regions."""
     pk.pk_stage(1)
-    pk.pk_slice_max(16 if two_level else 128)
+    pk.pk_slice_max(100 if two_level == "two_per_thread" else 16 if two_level else 128)
     check_csr(pk, "exp1_R131072_S1048576_zipf1")
     check_csr(pk, "exp1_R1048576_S8388608_uni")
 
@@ -129,15 +131,16 @@ def test_bucket_range_shards_on_packed_paths(pk, w):
 def test_pk_plan_geometry(ctx):
     """The slice plan the bench's configs land on (host-side arithmetic, checked on the device's CU
     count): config B and every config-D rank size fit one LDS slice per probe workgroup with whole
-    waves of workgroups; above 1024 slices two levels with C slices per coarse range."""
+    waves of workgroups; up to 2048 slices one level (two slices per partitioning thread above 1024:
+    config D's rank at 4 GPUs), above that two levels with C slices per coarse range."""
     import hj3d
     for nbl, n_build, levels in ((10_000_000, 10_000_000, 1), (12_500_000, 12_500_000, 1),
-                                 (25_000_000, 25_000_000, 2), (50_000_000, 50_000_000, 2),
+                                 (25_000_000, 25_000_000, 1), (50_000_000, 50_000_000, 2),
                                  (100_000_000, 100_000_000, 2)):
         pl = ctx.pk_plan(nbl, n_build)
         assert pl["P"] * pl["W"] >= nbl and (pl["P"] - 1) * pl["W"] < nbl
         assert (pl["C"] > 1) == (levels == 2), (nbl, pl)
-        assert pl["P1"] <= 1024 and pl["P1"] * pl["W1"] >= nbl
+        assert pl["P1"] <= (2048 if levels == 1 else 1024) and pl["P1"] * pl["W1"] >= nbl
         # the slice image at fill n_build / nbl: W directory words + 2 words per entry (+ 6 sigma)
         fill = n_build / nbl
         assert pl["W"] * (1 + 2 * fill) + 12 * (pl["W"] * fill) ** 0.5 <= 39552, (nbl, pl)
