@@ -113,6 +113,11 @@ struct hj3d_ctx {
   // (the timeout flag is also written into the built table's counts word 3, tagged with the launch's
   // sequence number gbar_seq, and checked by the table's getters)
   hj3d::DevBuf gbar;
+  // the slice-path nested build's decoupled look-back (nested_agg.hip): words 0-1 ticket and finish
+  // counters (zeroed by the launch before k_nagg), then one status word per partition tagged with
+  // nagg_epoch (no other use; cleared when allocated)
+  hj3d::DevBuf nagg_lb;
+  uint32_t nagg_epoch = 0;
   uint64_t gbar_target = 0;
   uint64_t gbar_seq = 0;
   uint64_t diag_gbar = 0;  // HJ3D_OPT_DIAG_GBAR: barrier timeout in 100 MHz ticks, workgroup 0 never arrives

@@ -229,11 +229,14 @@ struct NaggTabs {
   // hpairs[ps[gp] ..]; the key's rows already in the suffix of the partition's sub range
   uint32_t* hot = nullptr;
   uint2* hpairs = nullptr;
+  // slice path: decoupled look-back instead of the scan / rebase / mains launches (nested_agg_finish)
+  uint64_t* lbw = nullptr;  // [0] partition ticket, [1] finished workgroups, then the status words
+  uint32_t lb_epoch = 0;
 };
 constexpr uint32_t kHotW = 8;
 // one partition (global index gp) of k_nagg
 template <int BLOCK, int SLOTS, bool PK>
-__device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
+__device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                          FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                          uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount, uint32_t cap,
                                          const NaggSrc& src, const NaggTabs& tabs, uint32_t* agg_lds) {
@@ -565,7 +568,7 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     if (ovf) {  // too many distinct keys for one round: retry the first half of the range
       if (c1 - c0 <= kAggMinSpan) {  // > ~24 keys per bucket: the sort-based build instead
         if (threadIdx.x == 0) atomicOr(fail, 1u);
-        return;
+        return 0;
       }
       span = (c1 - c0 + 1) / 2;
       __syncthreads();
@@ -581,6 +584,12 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
     }
     __syncthreads();
     const uint32_t nk = block_scan_lds<BLOCK>(bcnt, c1 - c0, wsum);  // bcnt[k] = first main of bucket c0 + k
+    // slice path's look-back: the partition's key count is final after its last round's pass A, so it is
+    // published here, long before the workgroup looks back (after pass B); waiting for predecessors'
+    // counts at the end of their pass B stalled every workgroup behind the slowest (D shape 39 ms)
+    if (PK && tabs.lbw && c1 == nbs && threadIdx.x == 0)
+      __hip_atomic_store(tabs.lbw + 2 + gp, (uint64_t(tabs.lb_epoch & 0x3FFFFFFFu) << 34) | (1ull << 32) | (mrun + nk),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
     uint32_t cnt[SLOTS];
 #pragma unroll
@@ -697,6 +706,94 @@ __device__ __forceinline__ void nagg_one(uint32_t gp, const uint2* __restrict__ 
   if (threadIdx.x == 0) dcount[gp] = mrun;
   const uint64_t wm = wave_max(uint64_t(mxlen));
   if ((threadIdx.x & 63) == 0 && wm) atomicMax(maxlen, (unsigned long long)wm);
+  return mrun;
+}
+
+// The slice path's finish inside k_nagg (one table; partitions taken in ticket order, so every
+// partition before gp has a running or finished workgroup): publish the partition's key count, find
+// its main-record base by a decoupled look-back over the status words (64 predecessors per step, one
+// per lane of wave 0: the nearest inclusive prefix plus the aggregates after it), publish the
+// inclusive prefix, move the main records to their final slots and rebase the partition's directory
+// words; the last workgroup to finish writes the table's counts (and their host copy) and resets the
+// ticket. Status word: epoch << 34 | flag << 32 | value (flag 1 aggregate, 2 inclusive prefix), each an
+// 8-B relaxed agent-scope atomic (MI355X_MICROARCH.md, inter-workgroup hand-off: the word carries all
+// the data; acquire / release forms write back or invalidate the XCD's L2 and, issued by every
+// workgroup, slowed the whole launch 2x: D shape 16.4 -> 32 ms). A
+// look-back that waits 0.2 s sets the table's give-up flag (the sort build replaces it) instead of
+// hanging. Replaces exclusive_scan_u32 + k_nagg_rebase + k_nagg_mains (config D's Nrs table: ~1.2 ms).
+__device__ __forceinline__ void nagg_lb_finish(uint32_t gp, uint32_t nk, uint32_t P, uint32_t W, uint32_t nbl,
+                                               const uint4* __restrict__ mtmp, const uint32_t* __restrict__ ps,
+                                               const NaggTabs& tabs, uint32_t* bw) {
+  uint64_t* st = tabs.lbw + 2;
+  const uint64_t ep = uint64_t(tabs.lb_epoch & 0x3FFFFFFFu);
+  const auto pack = [&](uint64_t f, uint64_t v) __attribute__((always_inline)) { return (ep << 34) | (f << 32) | v; };
+  uint64_t* counts = tabs.counts[0];
+  // (the aggregate is usually out already, from the last round's pass A; a partition that gave up
+  // publishes its 0 here)
+  if (threadIdx.x == 0) __hip_atomic_store(st + gp, pack(1, nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kWave) {
+    const int lane = threadIdx.x;
+    uint64_t prefix = 0;
+    int64_t j = int64_t(gp) - 1;
+    const uint64_t t0 = wall_clock64();
+    while (j >= 0) {
+      const uint64_t w = int64_t(lane) <= j
+                             ? __hip_atomic_load(st + (j - lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : pack(2, 0);
+      const bool ok = (w >> 34) == ep && ((w >> 32) & 3u) != 0;
+      const uint64_t im = __ballot(ok && ((w >> 32) & 3u) == 2), bad = __ballot(!ok);
+      const int fi = im ? __ffsll((unsigned long long)im) - 1 : 64;
+      const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
+      if (bad & upto) {  // a predecessor has not published yet
+        if (wall_clock64() - t0 > 20000000ull) {
+          if (lane == 0) atomicOr(reinterpret_cast<uint32_t*>(counts + 3), 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      prefix += wave_sum(lane <= fi ? (w & 0xFFFFFFFFull) : 0ull);
+      if (fi < 64) break;
+      j -= kWave;
+    }
+    if (lane == 0) {
+      __hip_atomic_store(st + gp, pack(2, prefix + nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      bw[0] = uint32_t(prefix);
+    }
+  }
+  __syncthreads();
+  const uint32_t base = bw[0];
+  // (the partition's main records and directory words were written by this workgroup: L2-warm)
+  uint4* __restrict__ mains = tabs.main[0];
+  const uint32_t e0 = ps[gp];
+  for (uint32_t i = threadIdx.x; i < nk; i += blockDim.x) mains[base + i] = mtmp[e0 + i];
+  uint32_t* __restrict__ off = tabs.off[0];
+  const uint32_t b0 = gp * W, nbs = min(W, nbl - b0);
+  for (uint32_t k = threadIdx.x; k < nbs; k += blockDim.x) off[b0 + k] += base;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint64_t done = __hip_atomic_fetch_add(tabs.lbw + 1, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == P - 1) {  // the last workgroup: every other one has published and finished
+      const bool failed = __hip_atomic_load(reinterpret_cast<uint32_t*>(counts + 3), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT) != 0;
+      uint64_t c0 = 0, c1 = 0;
+      if (!failed) {
+        c0 = ps[P] - ps[0];
+        c1 = __hip_atomic_load(st + (P - 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xFFFFFFFFull;
+        counts[0] = c0;
+        counts[1] = c1;
+        off[nbl] = uint32_t(c1);
+      }
+      if (uint64_t* h = tabs.hc[0]) {  // the host's copy
+        h[0] = c0;
+        h[1] = c1;
+        h[2] = __hip_atomic_load(counts + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        h[3] = __hip_atomic_load(counts + 3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __hip_atomic_store(tabs.lbw, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(tabs.lbw + 1, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 // One workgroup per partition: gp = blockIdx.x, or order[blockIdx.x] (heavy first).
@@ -707,6 +804,22 @@ __global__ __launch_bounds__(BLOCK, 4) void k_nagg(const uint2* __restrict__ pai
                                                 const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
                                                 NaggTabs tabs) {
   extern __shared__ uint32_t agg_lds[];
+  if (PK && tabs.lbw) {  // partitions in ticket order (the look-back waits only on earlier tickets)
+    uint32_t* bw = agg_lds + 2 * cap;  // (the block-scan words: free before and after nagg_one)
+    if (threadIdx.x == 0)
+      bw[0] = uint32_t(__hip_atomic_fetch_add(tabs.lbw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    const uint32_t gp = bw[0];
+    __syncthreads();
+    const uint32_t nk = nagg_one<BLOCK, SLOTS, PK>(gp, pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src,
+                                                   tabs, agg_lds);
+    __syncthreads();
+    nagg_lb_finish(gp, nk, src.pk.P, W, nbl, mtmp, ps, tabs, bw);
+#if HJ3D_NAGG_CLK
+    if (threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + 6] = wall_clock64();  // (finish end)
+#endif
+    return;
+  }
   nagg_one<BLOCK, SLOTS, PK>(PK || !order ? blockIdx.x : order[blockIdx.x], pairs, ps, fm, lo, nbl, nb_global, W, mtmp,
                              dcount, cap, src, tabs, agg_lds);
 }
@@ -1260,9 +1373,11 @@ __global__ __launch_bounds__(kBlock) void k_nagg_fin(const uint4* __restrict__ m
 
 // pk_slices' region overflows -> the give-up flag (the sort build replaces the table); the packed
 // partitioner's control words back to zero, the invariant of the probes that share them
-__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts, uint32_t* __restrict__ defer) {
+__global__ void k_nagg_pk_ovf(uint64_t* __restrict__ ctl, uint64_t* __restrict__ counts, uint32_t* __restrict__ defer,
+                              uint64_t* __restrict__ lbw) {
   if (threadIdx.x < 4) counts[threadIdx.x] = threadIdx.x == 3 && ctl[0] != 0 ? 1u : 0u;  // ctl[0]: the overflow count
   if (threadIdx.x == 4) defer[0] = 0;
+  if (lbw && threadIdx.x >= 8 && threadIdx.x < 10) lbw[threadIdx.x - 8] = 0;  // the look-back's counters
   __syncthreads();
   if (threadIdx.x < 8) ctl[threadIdx.x] = 0;
 }
@@ -1335,9 +1450,31 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   uint32_t* hinfo = defer + PT + 1;  // hot-key split: heavy partitions and their chunks (PT + 2)
   uint32_t* hotw = hinfo + PT + 2;   // hot-key split: kHotW words per partition
   if ((e = ctx->ensure_ctl()) != hipSuccess) return e;
+  auto prime_at_least = [](uint32_t x) {
+    for (;; ++x) {
+      bool pr = x > 1;
+      for (uint32_t d = 2; d * d <= x && pr; ++d) pr = x % d != 0;
+      if (pr) return x;
+    }
+  };
+  const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
+  const bool reg = double(n) / PT <= kRegFill * kRegCap &&
+                   capr <= kRegSlots * kRegBlock && reg_lds_words(capr, W) * 4 <= 160 * 1024;
   NaggTabs tabs;
   tabs.P = P;
   tabs.nt = nt;
+  // the slice path's streaming aggregation finishes by decoupled look-back (no scan / rebase / mains)
+  uint64_t* lbw = nullptr;
+  if (pk && !reg) {
+    const size_t need = (uint64_t(PT) + 2) * sizeof(uint64_t);
+    if (ctx->nagg_lb.bytes < need) {
+      if ((e = ctx->nagg_lb.ensure(need)) != hipSuccess) return e;
+      if ((e = hipMemsetAsync(ctx->nagg_lb.p, 0, ctx->nagg_lb.bytes, s)) != hipSuccess) return e;
+    }
+    lbw = ctx->nagg_lb.as<uint64_t>();
+    tabs.lbw = lbw;
+    tabs.lb_epoch = ++ctx->nagg_epoch;
+  }
   tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
   tabs.defer = defer;
   // the hot-key election of the streaming form: in partitions above 5/4 of the mean only
@@ -1364,7 +1501,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     src.pk = sl.pk;
     ps = sl.ps;
     // region overflows (skewed keys) -> the give-up flag; the control words back to zero
-    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0], tabs.defer);
+    hipLaunchKernelGGL(k_nagg_pk_ovf, dim3(1), dim3(64), 0, s, ctx->ctl.as<uint64_t>(), tabs.counts[0], tabs.defer,
+                       lbw);
   } else {
     if ((e = ctx->scratch[kScrPStart].ensure((uint64_t(PT) + 2) * sizeof(uint32_t))) != hipSuccess) return e;
     uint32_t* pst = ctx->scratch[kScrPStart].as<uint32_t>();
@@ -1390,13 +1528,6 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // table size: a prime >= 1.5 slots per bucket (about one key per bucket: NB = #dv / b) + the
   // insert slack; a partition with more keys retries its range in halves. Two 512-thread
   // workgroups per CU when the LDS fits twice (config E), else one 1024-thread one.
-  auto prime_at_least = [](uint32_t x) {
-    for (;; ++x) {
-      bool pr = x > 1;
-      for (uint32_t d = 2; d * d <= x && pr; ++d) pr = x % d != 0;
-      if (pr) return x;
-    }
-  };
   static bool lds_attr = false;  // dynamic LDS above 64 KB
   if (!lds_attr) {
     for (const void* k : {reinterpret_cast<const void*>(&k_nagg_reg<true, 4>),
@@ -1424,9 +1555,6 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   const uint32_t lo = uint32_t(t->desc.bucket_lo), nbg = uint32_t(t->desc.num_buckets);
   // the register form (k_nagg_reg) where the partitions' mean pair count fits its registers with room
   // (a larger partition takes k_nagg's streaming form inside it)
-  const uint32_t capr = prime_at_least(uint32_t(1.5 * W) + kRegBlock + 64);
-  const bool reg = double(n) / PT <= kRegFill * kRegCap &&
-                   capr <= kRegSlots * kRegBlock && reg_lds_words(capr, W) * 4 <= 160 * 1024;
   if (reg) {
     const size_t lds = reg_lds_words(capr, W) * sizeof(uint32_t);
     const dim3 gr(std::min<uint32_t>(PT, G)), bl(kRegBlock);
@@ -1486,7 +1614,7 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   // build instead
   if (!pk) {  // (at most 2048 partitions)
     hipLaunchKernelGGL(k_nagg_fin, dim3(PT), dim3(kBlock), 0, s, mtmp, ps, dcount, tabs, nbl, W);
-  } else {
+  } else if (!lbw) {
     if ((e = exclusive_scan_u32(ctx, dcount, dcount, PT, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(k_nagg_rebase, dim3(grid_for(ctx, nbl, kBlock), nt), dim3(kBlock), 0, s, tabs, nbl,
                        FastDiv32::make(W), dcount);

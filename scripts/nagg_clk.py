@@ -95,6 +95,13 @@ def main():
     out["longest"] = [{"start": round(float(starts[i]), 1), "total": round(float(tot[i]), 1),
                        "pass_A": round(float(us(x[i, 2] - x[i, 1])), 1), "pass_B": round(float(us(x[i, 4] - x[i, 3])), 1)}
                       for i in top]
+    # slice path with the look-back finish (HJ3D_NAGG_CLK builds): point 6 = the finish's end
+    if a.workload == "D":
+        fin = us(x[:, 6] - x[:, 5])
+        out["finish"] = {"median": round(float(np.median(fin)), 2), "p90": round(float(np.percentile(fin, 90)), 2),
+                         "max": round(float(fin.max()), 2)}
+        print(json.dumps(out))
+        return
     # workgroups running at once on one CU (point 6: XCC_ID << 32 | HW_ID; CU_ID bits 8-11, SH 12,
     # SE 13-15): the largest overlap of [start, exit] intervals per CU, and the CUs seen
     hw = x[:, 6].astype(np.uint64)
