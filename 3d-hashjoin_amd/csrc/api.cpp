@@ -205,6 +205,10 @@ hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value) {
       if (value < 0) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_DIAG_GBAR: >= 0");
       ctx->diag_gbar = uint64_t(value);
       return HJ3D_OK;
+    case HJ3D_OPT_DIAG_LOOKBACK:
+      if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_DIAG_LOOKBACK: 0 .. 2^32-1");
+      ctx->diag_lb = uint64_t(value);
+      return HJ3D_OK;
     case HJ3D_OPT_PK_STAGE:
       if (value < 0 || value > 0xFFFFFFFFll) return fail(ctx, HJ3D_EINVAL, "HJ3D_OPT_PK_STAGE: >= 0");
       ctx->pk_stage = uint32_t(value);

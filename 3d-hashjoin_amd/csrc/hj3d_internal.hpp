@@ -120,6 +120,7 @@ struct hj3d_ctx {
   uint32_t nagg_epoch = 0;
   uint64_t gbar_target = 0;
   uint64_t gbar_seq = 0;
+  uint64_t diag_lb = 0;    // HJ3D_OPT_DIAG_LOOKBACK: slice-path look-back wait limit in 100 MHz ticks, partition 0 silent
   uint64_t diag_gbar = 0;  // HJ3D_OPT_DIAG_GBAR: barrier timeout in 100 MHz ticks, workgroup 0 never arrives
   hipError_t ensure_ctl() {
     if (ctl.p) return hipSuccess;

@@ -232,6 +232,8 @@ struct NaggTabs {
   // slice path: decoupled look-back instead of the scan / rebase / mains launches (nested_agg_finish)
   uint64_t* lbw = nullptr;  // [0] partition ticket, [1] finished workgroups, then the status words
   uint32_t lb_epoch = 0;
+  uint32_t lb_skip0 = 0;             // HJ3D_OPT_DIAG_LOOKBACK: partition 0 never publishes (tests)
+  uint64_t lb_ticks = 20000000ull;   // a look-back's wait limit (100 MHz ticks: 0.2 s)
 };
 constexpr uint32_t kHotW = 8;
 // one partition (global index gp) of k_nagg
@@ -587,7 +589,7 @@ __device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restric
     // slice path's look-back: the partition's key count is final after its last round's pass A, so it is
     // published here, long before the workgroup looks back (after pass B); waiting for predecessors'
     // counts at the end of their pass B stalled every workgroup behind the slowest (D shape 39 ms)
-    if (PK && tabs.lbw && c1 == nbs && threadIdx.x == 0)
+    if (PK && tabs.lbw && c1 == nbs && threadIdx.x == 0 && !(tabs.lb_skip0 && gp == 0))
       __hip_atomic_store(tabs.lbw + 2 + gp, (uint64_t(tabs.lb_epoch & 0x3FFFFFFFu) << 34) | (1ull << 32) | (mrun + nk),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
@@ -730,7 +732,8 @@ __device__ __forceinline__ void nagg_lb_finish(uint32_t gp, uint32_t nk, uint32_
   uint64_t* counts = tabs.counts[0];
   // (the aggregate is usually out already, from the last round's pass A; a partition that gave up
   // publishes its 0 here)
-  if (threadIdx.x == 0) __hip_atomic_store(st + gp, pack(1, nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const bool publish = !(tabs.lb_skip0 && gp == 0);
+  if (threadIdx.x == 0 && publish) __hip_atomic_store(st + gp, pack(1, nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (threadIdx.x < kWave) {
     const int lane = threadIdx.x;
     uint64_t prefix = 0;
@@ -745,7 +748,7 @@ __device__ __forceinline__ void nagg_lb_finish(uint32_t gp, uint32_t nk, uint32_
       const int fi = im ? __ffsll((unsigned long long)im) - 1 : 64;
       const uint64_t upto = fi >= 63 ? ~0ull : ((2ull << fi) - 1);
       if (bad & upto) {  // a predecessor has not published yet
-        if (wall_clock64() - t0 > 20000000ull) {
+        if (wall_clock64() - t0 > tabs.lb_ticks) {
           if (lane == 0) atomicOr(reinterpret_cast<uint32_t*>(counts + 3), 1u);
           break;
         }
@@ -757,7 +760,7 @@ __device__ __forceinline__ void nagg_lb_finish(uint32_t gp, uint32_t nk, uint32_
       j -= kWave;
     }
     if (lane == 0) {
-      __hip_atomic_store(st + gp, pack(2, prefix + nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (publish) __hip_atomic_store(st + gp, pack(2, prefix + nk), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       bw[0] = uint32_t(prefix);
     }
   }
@@ -1474,6 +1477,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
     lbw = ctx->nagg_lb.as<uint64_t>();
     tabs.lbw = lbw;
     tabs.lb_epoch = ++ctx->nagg_epoch;
+    tabs.lb_skip0 = ctx->diag_lb ? 1u : 0u;
+    if (ctx->diag_lb) tabs.lb_ticks = ctx->diag_lb;
   }
   tabs.sink = reinterpret_cast<uint32_t*>(ctx->ctl.as<uint64_t>() + 64);  // ctl words [64, 128): store sink
   tabs.defer = defer;

@@ -30,6 +30,7 @@ OPT_PROBE_ITEMS = 7
 OPT_PK_SLICE, OPT_PK_STAGE, OPT_PK_BUILD, OPT_NESTED_PK, OPT_SYNC_BUILD = 8, 9, 10, 11, 13
 OPT_RP_UNFUSED = 15
 OPT_DIAG_GBAR = 16
+OPT_DIAG_LOOKBACK = 17
 SEL_LT, SEL_LE, SEL_GT, SEL_GE, SEL_EQ, SEL_NE, SEL_RANGE = range(7)
 SEL_MAX = 4
 SEL_OPS = {"<": SEL_LT, "<=": SEL_LE, ">": SEL_GT, ">=": SEL_GE, "==": SEL_EQ, "!=": SEL_NE, "range": SEL_RANGE}
@@ -442,6 +443,12 @@ class Context:
         `ticks` of the 100 MHz clock and its workgroup 0 never arrives, so the barrier fails (tests
         of the failure path; 0 = off)."""
         self.set_option(OPT_DIAG_GBAR, int(ticks))
+
+    def diag_lookback(self, ticks: int = 0):
+        """Diagnostic (HJ3D_OPT_DIAG_LOOKBACK): in the nested build on the packed slices, partition 0
+        never publishes its count and the look-back waits at most `ticks` of the 100 MHz clock, so
+        the build gives up and the sort build replaces the table (tests of that path; 0 = off)."""
+        self.set_option(OPT_DIAG_LOOKBACK, int(ticks))
 
     def sync_build(self, on: bool = True):
         """Nested builds finished inside hj3d_build (HJ3D_OPT_SYNC_BUILD): the build relation may

@@ -205,7 +205,13 @@ enum {
   /* HJ3D_OPT_DIAG_GBAR (ticks of the 100 MHz clock, default 0 = off): diagnostic for the failure path
    * above. The fused partition's barrier then times out after this many ticks, and its workgroup 0
    * never arrives, so every barrier of such a build times out (tests). */
-  HJ3D_OPT_DIAG_GBAR = 16
+  HJ3D_OPT_DIAG_GBAR = 16,
+  /* HJ3D_OPT_DIAG_LOOKBACK (ticks of the 100 MHz clock, default 0 = off): diagnostic of the nested
+   * build on the packed slices (the aggregation form that finishes by decoupled look-back: each
+   * partition's main-record base waits on its predecessors' published counts, at most 0.2 s, after
+   * which the build gives up and the sort build replaces the table). Partition 0 then never
+   * publishes and the wait limit is this many ticks, so every such build gives up (tests). */
+  HJ3D_OPT_DIAG_LOOKBACK = 17
 };
 hj3d_status hj3d_ctx_set_option(hj3d_ctx* ctx, int option, int64_t value);
 /* Timing events for a host's own phase timers (the bench's build / probe boundaries): HIP events

@@ -225,6 +225,39 @@ def test_nested_agg_build_vs_oracle(ctx, nb, zipf):
         ctx.nested_pk(False)
 
 
+def test_nested_slices_lookback_timeout_falls_back(ctx):
+    """The slice-path aggregation build's failure path (HJ3D_OPT_DIAG_LOOKBACK: partition 0 never
+    publishes its count, so every successor's look-back runs out after 1 ms and sets the give-up
+    flag): the sort build replaces the table and the join equals the oracle's; the look-back words
+    are left in step, so the next build on the same context takes the slice path again and is exact."""
+    import hj3d
+    rng = np.random.default_rng(17)
+    nR, nS, nb = 100_000, 400_000, 20_000  # 20 partitions of ~20K pairs: the streaming form (not registers)
+    R = O.tuples3(rng.permutation(nR).astype(np.uint32), np.zeros(nR, np.uint32))
+    S = O.tuples3(np.arange(nS, dtype=np.uint32), rng.integers(0, nR, nS).astype(np.uint32))
+    e = O.nested_plan(S, 1, R, 0, nb, True)
+    dR, dS = dev(R), dev(S)
+    ctx.radix_min(0)
+    ctx.nested_pk(True)
+    try:
+        for diag, want in ((100_000, "nested_sort"), (0, "nested_agg_slices"), (100_000, "nested_sort"),
+                           (0, "nested_agg_slices")):
+            ctx.diag_lookback(diag)
+            t = hj3d.Table(ctx, hj3d.HJ3D_NESTED, nb)
+            got = hj3d.exp1_plan(ctx, "Nrs", dR, dS, nb, table=t)
+            path = t.build_path()
+            t.close()
+            assert path == want, (diag, path)
+            assert (got["c_probe"], got["c_cmp"], got["c_unnest"], got["c_top"]) == \
+                (e.c_probe, e.c_cmp, e.c_unnest, e.c_top), (diag, path)
+            assert got["out"] == e.out, (diag, path)
+            assert {k: got["stats"][k] for k in STAT_KEYS} == {k: e.stats[k] for k in STAT_KEYS}, (diag, path)
+    finally:
+        ctx.diag_lookback(0)
+        ctx.radix_min(1 << 20)
+        ctx.nested_pk(False)
+
+
 @pytest.mark.parametrize("path", ["default", "partitioned"])
 @pytest.mark.parametrize("name,g", EXP4, ids=[n for n, _ in EXP4])
 def test_exp4_plans_bit_exact(ctx, name, g, path):
