@@ -65,7 +65,8 @@ constexpr uint32_t kRegSlots = 4;
 #if HJ3D_NAGG_CLK
 __device__ uint64_t g_nagg_clk[kClkParts * kClkPts];
 #endif
-// point k of partition gp's timeline: 100 MHz wall clock (point 7: the workgroup's dispatch index)
+// point k of partition gp's timeline: 100 MHz wall clock (point 7: the workgroup's dispatch index, or
+// with the look-back finish the finish's end)
 __device__ __forceinline__ void nagg_clk(uint32_t gp, int k) {
 #if HJ3D_NAGG_CLK
   if (threadIdx.x == 0 && gp < kClkParts) {
@@ -241,7 +242,8 @@ template <int BLOCK, int SLOTS, bool PK>
 __device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                          FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
                                          uint4* __restrict__ mtmp, uint32_t* __restrict__ dcount, uint32_t cap,
-                                         const NaggSrc& src, const NaggTabs& tabs, uint32_t* agg_lds) {
+                                         const NaggSrc& src, const NaggTabs& tabs, uint32_t* agg_lds,
+                                         bool lb = false) {
   constexpr uint32_t kNw = BLOCK / kWave;
   uint32_t* tkey = agg_lds;
   uint32_t* tcnt = tkey + cap;  // count, then the rows before the key in the round (pass B: its cursor)
@@ -589,7 +591,7 @@ __device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restric
     // slice path's look-back: the partition's key count is final after its last round's pass A, so it is
     // published here, long before the workgroup looks back (after pass B); waiting for predecessors'
     // counts at the end of their pass B stalled every workgroup behind the slowest (D shape 39 ms)
-    if (PK && tabs.lbw && c1 == nbs && threadIdx.x == 0 && !(tabs.lb_skip0 && gp == 0))
+    if (lb && c1 == nbs && threadIdx.x == 0 && !(tabs.lb_skip0 && gp == 0))
       __hip_atomic_store(tabs.lbw + 2 + gp, (uint64_t(tabs.lb_epoch & 0x3FFFFFFFu) << 34) | (1ull << 32) | (mrun + nk),
                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // sub ranges: exclusive scan of the counts in slot order; tcnt becomes the sub cursor
@@ -799,7 +801,8 @@ __device__ __forceinline__ void nagg_lb_finish(uint32_t gp, uint32_t nk, uint32_
   }
 }
 
-// One workgroup per partition: gp = blockIdx.x, or order[blockIdx.x] (heavy first).
+// One workgroup per partition: gp = blockIdx.x, or order[blockIdx.x] (heavy first), or a ticket (the
+// slice path's look-back finish; one call site of nagg_one for both: two inlined copies spilled).
 template <int BLOCK, int SLOTS, bool PK>
 __global__ __launch_bounds__(BLOCK, 4) void k_nagg(const uint2* __restrict__ pairs, const uint32_t* __restrict__ ps,
                                                 FastMod fm, uint32_t lo, uint32_t nbl, uint32_t nb_global, uint32_t W,
@@ -807,24 +810,26 @@ __global__ __launch_bounds__(BLOCK, 4) void k_nagg(const uint2* __restrict__ pai
                                                 const uint32_t* __restrict__ order, uint32_t cap, NaggSrc src,
                                                 NaggTabs tabs) {
   extern __shared__ uint32_t agg_lds[];
-  if (PK && tabs.lbw) {  // partitions in ticket order (the look-back waits only on earlier tickets)
-    uint32_t* bw = agg_lds + 2 * cap;  // (the block-scan words: free before and after nagg_one)
+  const bool lb = PK && tabs.lbw;
+  uint32_t* bw = agg_lds + 2 * cap;  // (the block-scan words: free before and after nagg_one)
+  uint32_t gp;
+  if (lb) {  // partitions in ticket order (the look-back waits only on earlier tickets)
     if (threadIdx.x == 0)
       bw[0] = uint32_t(__hip_atomic_fetch_add(tabs.lbw, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     __syncthreads();
-    const uint32_t gp = bw[0];
+    gp = bw[0];
     __syncthreads();
-    const uint32_t nk = nagg_one<BLOCK, SLOTS, PK>(gp, pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src,
-                                                   tabs, agg_lds);
-    __syncthreads();
-    nagg_lb_finish(gp, nk, src.pk.P, W, nbl, mtmp, ps, tabs, bw);
-#if HJ3D_NAGG_CLK
-    if (threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + 6] = wall_clock64();  // (finish end)
-#endif
-    return;
+  } else {
+    gp = PK || !order ? blockIdx.x : order[blockIdx.x];
   }
-  nagg_one<BLOCK, SLOTS, PK>(PK || !order ? blockIdx.x : order[blockIdx.x], pairs, ps, fm, lo, nbl, nb_global, W, mtmp,
-                             dcount, cap, src, tabs, agg_lds);
+  const uint32_t nk = nagg_one<BLOCK, SLOTS, PK>(gp, pairs, ps, fm, lo, nbl, nb_global, W, mtmp, dcount, cap, src, tabs,
+                                                 agg_lds, lb);
+  if (!lb) return;
+  __syncthreads();
+  nagg_lb_finish(gp, nk, src.pk.P, W, nbl, mtmp, ps, tabs, bw);
+#if HJ3D_NAGG_CLK
+  if (threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + 7] = wall_clock64();  // (finish end)
+#endif
 }
 
 // ---- k_nagg_reg: the partition held in registers, its sub rows assembled in LDS ----
@@ -1467,6 +1472,8 @@ hipError_t nested_build_agg_many(hj3d_ctx* ctx, hj3d_table* const* tt, const hj3
   tabs.P = P;
   tabs.nt = nt;
   // the slice path's streaming aggregation finishes by decoupled look-back (no scan / rebase / mains)
+  // (tried on the one-level paths too, when no partition is heavy: config E build 0.258-0.261 ->
+  // 0.266 ms, `profiles/r06v_E_lookback_ab.jsonl`; k_nagg_fin kept there)
   uint64_t* lbw = nullptr;
   if (pk && !reg) {
     const size_t need = (uint64_t(PT) + 2) * sizeof(uint64_t);

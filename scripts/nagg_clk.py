@@ -88,20 +88,18 @@ def main():
                               "max": round(float(tot.max()), 2)}
     starts = us(x[:, 0] - t0)
     out["start_deciles_us"] = [round(float(np.percentile(starts, q)), 1) for q in range(0, 101, 10)]
-    ends = us(x[:, 5] - t0)
+    ends = us(np.maximum(x[:, 5], np.where(x[:, 7] > x[:, 5], x[:, 7], 0)) - t0)
     out["end_deciles_us"] = [round(float(np.percentile(ends, q)), 1) for q in range(0, 101, 10)]
     # the longest workgroups (heavy partitions): start, total and pass times (last round), us
     top = np.argsort(-tot)[:8]
     out["longest"] = [{"start": round(float(starts[i]), 1), "total": round(float(tot[i]), 1),
                        "pass_A": round(float(us(x[i, 2] - x[i, 1])), 1), "pass_B": round(float(us(x[i, 4] - x[i, 3])), 1)}
                       for i in top]
-    # slice path with the look-back finish (HJ3D_NAGG_CLK builds): point 6 = the finish's end
-    if a.workload == "D":
-        fin = us(x[:, 6] - x[:, 5])
+    # the look-back finish (HJ3D_NAGG_CLK builds): point 7 = the finish's end (else the dispatch index)
+    if (x[:, 7] > x[:, 5]).all():
+        fin = us(x[:, 7] - x[:, 5])
         out["finish"] = {"median": round(float(np.median(fin)), 2), "p90": round(float(np.percentile(fin, 90)), 2),
                          "max": round(float(fin.max()), 2)}
-        print(json.dumps(out))
-        return
     # workgroups running at once on one CU (point 6: XCC_ID << 32 | HW_ID; CU_ID bits 8-11, SH 12,
     # SE 13-15): the largest overlap of [start, exit] intervals per CU, and the CUs seen
     hw = x[:, 6].astype(np.uint64)
@@ -109,7 +107,7 @@ def main():
     occ = {}
     for c in np.unique(cu):
         idx = np.where(cu == c)[0]
-        ev = sorted([(x[i, 0], 1) for i in idx] + [(x[i, 5], -1) for i in idx], key=lambda t: (t[0], t[1]))
+        ev = sorted([(x[i, 0], 1) for i in idx] + [(max(x[i, 5], x[i, 7]), -1) for i in idx], key=lambda t: (t[0], t[1]))
         cur = best = 0
         for _, d in ev:
             cur += d
