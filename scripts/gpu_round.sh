@@ -34,25 +34,28 @@ if [[ $PART == *t* ]]; then
   tail -2 gpurun_out/${TAG}_pytest.log
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 || { tail -5 gpurun_out/${TAG}_smoke.log; exit 1; }
 fi
+# (PMC passes first: their summary goes into the box's profiles/ too, so the bench line that follows
+# cites the PMC file of the same library as roofline.pmc_source, pmc_same_library true)
 if [[ $PART == *b* ]]; then
-  step bench B
-  timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
-  tail -1 gpurun_out/${TAG}_bench.log | cut -c1-400
   step rocprof B
   prof ${TAG} --steps 5 --warmup 2
   step pmc B
   bash scripts/gpu_pmc.sh ${TAG} || exit 1
-  python scripts/pmc_summary.py ${TAG} --out gpurun_out/${TAG}_pmc.json
+  python scripts/pmc_summary.py ${TAG} --out gpurun_out/${TAG}_pmc.json && cp gpurun_out/${TAG}_pmc.json profiles/ || exit 1
+  step bench B
+  timeout -k 10 600 python bench.py > gpurun_out/${TAG}_bench.log 2>&1 || { tail -20 gpurun_out/${TAG}_bench.log; exit 1; }
+  tail -1 gpurun_out/${TAG}_bench.log | cut -c1-400
 fi
 if [[ $PART == *c* ]]; then
   for w in C E; do
-    step bench $w
-    timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 > gpurun_out/${TAG}_$w.log 2>&1 || { tail -20 gpurun_out/${TAG}_$w.log; exit 1; }
-    tail -1 gpurun_out/${TAG}_$w.log | cut -c1-300
     prof ${TAG}_$w --workload $w --steps 3 --warmup 1
     step pmc $w
     BENCH_ARGS="--workload $w" bash scripts/gpu_pmc.sh ${TAG}_$w || exit 1
-    python scripts/pmc_summary.py ${TAG}_$w --workload $w --out gpurun_out/${TAG}_${w}_pmc.json
+    python scripts/pmc_summary.py ${TAG}_$w --workload $w --out gpurun_out/${TAG}_${w}_pmc.json &&
+      cp gpurun_out/${TAG}_${w}_pmc.json profiles/ || exit 1
+    step bench $w
+    timeout -k 10 600 python bench.py --workload $w --steps 10 --warmup 2 > gpurun_out/${TAG}_$w.log 2>&1 || { tail -20 gpurun_out/${TAG}_$w.log; exit 1; }
+    tail -1 gpurun_out/${TAG}_$w.log | cut -c1-300
   done
 fi
 if [[ $PART == *d* ]]; then
