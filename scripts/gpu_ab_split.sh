@@ -6,9 +6,13 @@ cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 TAG=${TAG:-split}
 lib_for() { [ "$1" = default ] && echo "" || echo "$GRAFT_REPO_ROOT/3d-hashjoin_amd/variants/$1/libhj3d.so"; }
-timeout -k 10 600 python -u -m pytest tests/test_gpu_pk_levels.py tests/test_gpu_parity.py -k "pk or slice or nested_agg_build or lookback" -m gpu -x -q \
-  --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/${TAG}_tests.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests.log; exit 1; }
-tail -1 gpurun_out/${TAG}_tests.log
+# (parity with every variant; KEXPR: the -k expression, TESTS: the files)
+for v in $VARIANTS; do
+  HJ3D_LIB=$(lib_for $v) timeout -k 10 600 python -u -m pytest ${TESTS:-tests/test_gpu_pk_levels.py tests/test_gpu_parity.py} \
+    -k "${KEXPR:-pk or slice or nested_agg_build or lookback}" -m gpu -x -q --timeout 300 --timeout-method thread \
+    -p no:cacheprovider > gpurun_out/${TAG}_tests_$v.log 2>&1 || { tail -30 gpurun_out/${TAG}_tests_$v.log; exit 1; }
+  echo "tests $v: $(tail -1 gpurun_out/${TAG}_tests_$v.log)"
+done
 for r in $(seq 1 ${ROUNDS:-2}); do
   for v in $VARIANTS; do
     HJ3D_LIB=$(lib_for $v) timeout -k 10 300 python scripts/time_pk.py --nR 1e8 --nS 1e9 --reps 5 --label $v > gpurun_out/${TAG}_run.log 2>&1 || { tail -5 gpurun_out/${TAG}_run.log; exit 1; }
