@@ -65,8 +65,8 @@ constexpr uint32_t kRegSlots = 4;
 #if HJ3D_NAGG_CLK
 __device__ uint64_t g_nagg_clk[kClkParts * kClkPts];
 #endif
-// point k of partition gp's timeline: 100 MHz wall clock (point 7: the workgroup's dispatch index, or
-// with the look-back finish the finish's end)
+// point k of partition gp's timeline: 100 MHz wall clock (point 7: the end of the last round's pass-B
+// sweep, before the image goes out, or with the look-back finish the finish's end)
 __device__ __forceinline__ void nagg_clk(uint32_t gp, int k) {
 #if HJ3D_NAGG_CLK
   if (threadIdx.x == 0 && gp < kClkParts) {
@@ -697,6 +697,9 @@ __device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restric
     if (hk || nrows > imgw) passb(std::true_type{});
     else passb(std::false_type{});
     __syncthreads();
+#if HJ3D_NAGG_CLK
+    if (!lb && threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + 7] = wall_clock64();  // (sweep end)
+#endif
     // the image out as whole lines (the hot key's rows, already in place, skipped)
     for (uint32_t k = threadIdx.x; k < min(nrows, imgw); k += BLOCK)
       if (k - hstart >= hlen) gsub[k] = img[k];

@@ -88,14 +88,27 @@ def main():
                               "max": round(float(tot.max()), 2)}
     starts = us(x[:, 0] - t0)
     out["start_deciles_us"] = [round(float(np.percentile(starts, q)), 1) for q in range(0, 101, 10)]
-    ends = us(np.maximum(x[:, 5], np.where(x[:, 7] > x[:, 5], x[:, 7], 0)) - t0)
+    ends = us(np.maximum(x[:, 5], x[:, 7]) - t0)
     out["end_deciles_us"] = [round(float(np.percentile(ends, q)), 1) for q in range(0, 101, 10)]
     # the longest workgroups (heavy partitions): start, total and pass times (last round), us
     top = np.argsort(-tot)[:8]
     out["longest"] = [{"start": round(float(starts[i]), 1), "total": round(float(tot[i]), 1),
                        "pass_A": round(float(us(x[i, 2] - x[i, 1])), 1), "pass_B": round(float(us(x[i, 4] - x[i, 3])), 1)}
                       for i in top]
-    # the look-back finish (HJ3D_NAGG_CLK builds): point 7 = the finish's end (else the dispatch index)
+    # point 7: the end of pass B's sweep (before the image write-out), or with the look-back finish the
+    # finish's end
+    if ((x[:, 7] >= x[:, 3]) & (x[:, 7] <= x[:, 4])).all():
+        for nm, d in (("pass_B_sweep", us(x[:, 7] - x[:, 3])), ("pass_B_writeout", us(x[:, 4] - x[:, 7]))):
+            out[nm] = {"median": round(float(np.median(d)), 2), "p90": round(float(np.percentile(d, 90)), 2),
+                       "max": round(float(d.max()), 2)}
+        # the first-started half against the rest
+        first = x[:, 0] <= np.percentile(x[:, 0], 40)
+        out["pass_B_sweep_first_vs_rest"] = [round(float(np.median(us(x[first, 7] - x[first, 3]))), 2),
+                                              round(float(np.median(us(x[~first, 7] - x[~first, 3]))), 2)]
+        out["pass_B_writeout_first_vs_rest"] = [round(float(np.median(us(x[first, 4] - x[first, 7]))), 2),
+                                                 round(float(np.median(us(x[~first, 4] - x[~first, 7]))), 2)]
+        out["pass_A_first_vs_rest"] = [round(float(np.median(us(x[first, 2] - x[first, 1]))), 2),
+                                       round(float(np.median(us(x[~first, 2] - x[~first, 1]))), 2)]
     if (x[:, 7] > x[:, 5]).all():
         fin = us(x[:, 7] - x[:, 5])
         out["finish"] = {"median": round(float(np.median(fin)), 2), "p90": round(float(np.percentile(fin, 90)), 2),
