@@ -1,8 +1,8 @@
-# Same-box A/B of config E's bench line (build_ms / probe_ms) over variant libraries:
+# Same-box A/B of config E's (WORKLOAD: or C's) bench line (build_ms / probe_ms) over variant libraries:
 #   VARIANTS  "default" and/or names under 3d-hashjoin_amd/variants/ (HJ3D_LIB); TAG names the files;
 #   ROUNDS    alternating rounds (default 3); KEXPR: the nested / exp4 parity tests run first with
 #             every variant.
-# One JSON line per run in gpurun_out/${TAG}_E_ab.jsonl.
+# One JSON line per run in gpurun_out/${TAG}_${WORKLOAD:-E}_ab.jsonl.
 cd "$GRAFT_REPO_ROOT" || exit 2
 export TMPDIR=/tmp
 TAG=${TAG:-eab}
@@ -16,7 +16,7 @@ for v in $VARIANTS; do
 done
 for r in $(seq 1 ${ROUNDS:-3}); do
   for v in $VARIANTS; do
-    HJ3D_LIB=$(lib_for $v) timeout -k 10 200 python bench.py --workload E --steps 20 --warmup 3 --no-cpu-baseline --no-mintime > gpurun_out/${TAG}_E_$v.log 2>&1 || { tail -5 gpurun_out/${TAG}_E_$v.log; exit 1; }
-    python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_E_$v.log').read().strip().splitlines()[-1]); print(json.dumps({'label':'$v','round':$r,'build_ms':d['build_ms'],'probe_ms':d['probe_ms'],'ok':d['verified_bit_exact']}))"
+    HJ3D_LIB=$(lib_for $v) timeout -k 10 200 python bench.py --workload ${WORKLOAD:-E} --steps 20 --warmup 3 --no-cpu-baseline --no-mintime > gpurun_out/${TAG}_${WORKLOAD:-E}_$v.log 2>&1 || { tail -5 gpurun_out/${TAG}_${WORKLOAD:-E}_$v.log; exit 1; }
+    python3 -c "import json,sys; d=json.loads(open('gpurun_out/${TAG}_${WORKLOAD:-E}_$v.log').read().strip().splitlines()[-1]); print(json.dumps({'label':'$v','round':$r,'build_ms':d['build_ms'],'probe_ms':d['probe_ms'],'ok':d['verified_bit_exact']}))"
   done
-done | tee gpurun_out/${TAG}_E_ab.jsonl
+done | tee gpurun_out/${TAG}_${WORKLOAD:-E}_ab.jsonl
