@@ -701,8 +701,8 @@ __device__ __forceinline__ uint32_t nagg_one(uint32_t gp, const uint2* __restric
     if (!lb && threadIdx.x == 0 && gp < kClkParts) g_nagg_clk[gp * kClkPts + 7] = wall_clock64();  // (sweep end)
 #endif
     // the image out as whole lines (the hot key's rows, already in place, skipped), non-temporal
-    // (same box, three runs each: E build 0.2598 -> 0.2581 ms, C 1.866 -> 1.850 ms, D shape 16.57 ->
-    // 16.29 ms; r06z_ntw_*)
+    // (same box: D shape 16.57 -> 16.29 ms, E build 0.2598 -> 0.2581 ms, C within noise; r06z_ntw_*,
+    // r06z_ntc_C_ab.jsonl)
     for (uint32_t k = threadIdx.x; k < min(nrows, imgw); k += BLOCK)
       if (k - hstart >= hlen) __builtin_nontemporal_store(img[k], gsub + k);
     __syncthreads();  // (the next round's table; the next partition's)
